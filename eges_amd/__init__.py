@@ -1,0 +1,13 @@
+"""eges_amd — MI355X-native batched secp256k1 sender recovery for the EGES / Geec chain.
+
+Hot path: crypto.Ecrecover -> Keccak-256 address (and crypto.VerifySignature, types.Sender),
+executed by hand-written HIP kernels for gfx950 behind the C-ABI in include/eges.h.
+The Python modules mirror the reference's Go API (crypto, crypto/secp256k1, core/types) so
+the parity tests read like the reference's own tests.
+"""
+from . import _lib  # noqa: F401  (raises ImportError if libeges.so is missing: no fallback)
+from .engine import (device_count, ecrecover_batch, ecrecover_batch_dev, init, keccak256,  # noqa: F401
+                     sender_batch, synth_sign_dev, verify_batch)
+
+__all__ = ["init", "device_count", "ecrecover_batch", "sender_batch", "verify_batch", "keccak256",
+           "ecrecover_batch_dev", "synth_sign_dev"]

@@ -1,0 +1,550 @@
+// C-ABI of libeges.so (include/eges.h): device management, staging, multi-GPU sharding.
+//
+// Replaces the reference's cgo seam (crypto/secp256k1/secp256.go:45-134, ext.h:18-75). There is
+// no CPU compute path here: every recovery / verification runs on gfx950 through the kernels in
+// k_*.hip, and the entries fail with EGES_E_NODEVICE when no such device is usable.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "eges.h"
+#include "launch.h"
+
+namespace {
+
+using namespace eges;
+
+constexpr size_t CHUNK = size_t(1) << 21;  // signatures per device pass (bounds scratch memory)
+
+thread_local std::string t_err;
+
+int set_err(int rc, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  t_err = buf;
+  return rc;
+}
+
+#define HIPCHK(expr)                                                                                \
+  do {                                                                                              \
+    hipError_t e_ = (expr);                                                                         \
+    if (e_ != hipSuccess) return set_err(EGES_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+struct Dev {
+  int id = -1;
+  int cus = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t last = nullptr;  // completion of the last engine work (workspace users serialise on it)
+  uint32_t* gtab = nullptr;
+  uint32_t* ws = nullptr;
+  int mb_recover = 0, mb_verify = 0, mb_synth = 0;
+  uint8_t* buf = nullptr;  // per-call device scratch, grown on demand
+  size_t buf_cap = 0;
+  std::mutex mu;
+};
+
+std::mutex g_mu;
+std::vector<Dev*> g_devs;
+bool g_inited = false;
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct DevGuard {  // restores the caller's current device
+  int prev = -1;
+  explicit DevGuard(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    (void)hipSetDevice(d);
+  }
+  ~DevGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int dev_ensure_buf(Dev& d, size_t bytes) {
+  if (bytes <= d.buf_cap) return EGES_SUCCESS;
+  if (d.buf) {
+    HIPCHK(hipStreamSynchronize(d.stream));
+    HIPCHK(hipEventSynchronize(d.last));
+    HIPCHK(hipFree(d.buf));
+    d.buf = nullptr;
+    d.buf_cap = 0;
+  }
+  size_t cap = std::max(bytes, size_t(64) << 20);
+  if (hipMalloc(&d.buf, cap) != hipSuccess) return set_err(EGES_E_NOMEM, "hipMalloc(%zu) failed", cap);
+  d.buf_cap = cap;
+  return EGES_SUCCESS;
+}
+
+int init_device(int id, Dev** out) {
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, id));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return set_err(EGES_E_NODEVICE, "device %d is %s, the engine is built for gfx950 only", id, prop.gcnArchName);
+  DevGuard g(id);
+  Dev* d = new Dev();
+  d->id = id;
+  d->cus = prop.multiProcessorCount;
+  HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&d->last, hipEventDisableTiming));
+  d->mb_recover = occupancy_recover() * d->cus;
+  d->mb_verify = occupancy_verify() * d->cus;
+  d->mb_synth = occupancy_synth() * d->cus;
+  const int mb = std::max(d->mb_recover, std::max(d->mb_verify, d->mb_synth));
+  HIPCHK(hipMalloc(&d->gtab, gtab_bytes()));
+  HIPCHK(hipMalloc(&d->ws, ws_bytes_per_block() * (size_t)mb));
+  HIPCHK(launch_init_gtab(d->gtab, d->stream));
+  HIPCHK(hipEventRecord(d->last, d->stream));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  *out = d;
+  return EGES_SUCCESS;
+}
+
+int ensure_init() {
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_inited && !g_devs.empty()) return EGES_SUCCESS;
+  }
+  int rc = eges_init(0, 0);
+  return rc;
+}
+
+Dev* dev_by_id(int id) {
+  for (Dev* d : g_devs)
+    if (d->id == id) return d;
+  return nullptr;
+}
+
+// Enqueue on `st` after all previous engine work on this device; record completion.
+struct Serial {
+  Dev& d;
+  hipStream_t st;
+  Serial(Dev& dev, hipStream_t s) : d(dev), st(s) { (void)hipStreamWaitEvent(st, d.last, 0); }
+  ~Serial() { (void)hipEventRecord(d.last, st); }
+};
+
+// ------------------------------------------------------------------ device-side pipelines
+// All pointers device pointers; d.mu held by the caller.
+int run_recover_dev(Dev& d, const uint8_t* msg, const uint8_t* sig, size_t n, uint8_t* pub, uint8_t* addr,
+                    uint8_t* status, hipStream_t st) {
+  const size_t c = std::min(n, CHUNK);
+  const size_t n_pad = align_up(c, 64);
+  int rc = dev_ensure_buf(d, n_pad * REC_ROWS * 4);
+  if (rc) return rc;
+  uint32_t* rec = reinterpret_cast<uint32_t*>(d.buf);
+  Serial ser(d, st);
+  for (size_t off = 0; off < n; off += CHUNK) {
+    const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
+    HIPCHK(launch_prep_ecrecover(msg + off * 32, sig + off * 65, m, (uint32_t)n_pad, rec, st));
+    RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr ? addr + off * 20 : nullptr, pub ? pub + off * 65 : nullptr,
+                    d.gtab, d.ws};
+    HIPCHK(launch_recover(p, d.mb_recover, st));
+  }
+  return EGES_SUCCESS;
+}
+
+int run_sender_dev(Dev& d, const uint8_t* sighash, const uint8_t* r, const uint8_t* s, const uint8_t* v,
+                   const uint8_t* vflags, size_t n, int signer, uint64_t chain_id, uint8_t* addr, uint8_t* status,
+                   hipStream_t st) {
+  const size_t c = std::min(n, CHUNK);
+  const size_t n_pad = align_up(c, 64);
+  int rc = dev_ensure_buf(d, n_pad * REC_ROWS * 4);
+  if (rc) return rc;
+  uint32_t* rec = reinterpret_cast<uint32_t*>(d.buf);
+  Serial ser(d, st);
+  for (size_t off = 0; off < n; off += CHUNK) {
+    const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
+    HIPCHK(launch_prep_sender(sighash + off * 32, r + off * 32, s + off * 32, v + off * 32, vflags ? vflags + off : nullptr,
+                              m, (uint32_t)n_pad, signer, chain_id, rec, st));
+    RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr + off * 20, nullptr, d.gtab, d.ws};
+    HIPCHK(launch_recover(p, d.mb_recover, st));
+  }
+  return EGES_SUCCESS;
+}
+
+int run_verify_dev(Dev& d, const uint8_t* pub, const uint8_t* publen, const uint8_t* msg, const uint8_t* sig, size_t n,
+                   uint8_t* ok, hipStream_t st) {
+  Serial ser(d, st);
+  for (size_t off = 0; off < n; off += CHUNK) {
+    const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
+    VerifyParams p{pub + off * 65, publen + off, msg + off * 32, sig + off * 64, m, ok + off, d.gtab, d.ws};
+    HIPCHK(launch_verify(p, d.mb_verify, st));
+  }
+  return EGES_SUCCESS;
+}
+
+// ------------------------------------------------------------------ host-buffer pipelines
+// Copies the inputs of [off, off+cnt) to device scratch, runs, copies outputs back. Synchronous.
+struct HostJob {
+  enum Kind { RECOVER, SENDER, VERIFY } kind;
+  // inputs
+  const uint8_t *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr, *e = nullptr;
+  int signer = 0;
+  uint64_t chain_id = 0;
+  // outputs
+  uint8_t *pub = nullptr, *addr = nullptr, *status = nullptr;
+};
+
+int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
+  std::lock_guard<std::mutex> lk(d.mu);
+  DevGuard g(d.id);
+  for (size_t base = off; base < off + cnt; base += CHUNK) {
+    const size_t m = std::min(CHUNK, off + cnt - base);
+    const size_t m_pad = align_up(m, 64);
+    // layout: inputs | rec | outputs
+    size_t in_bytes = 0;
+    switch (j.kind) {
+      case HostJob::RECOVER: in_bytes = m * (32 + 65); break;
+      case HostJob::SENDER: in_bytes = m * (32 * 4 + 1); break;
+      case HostJob::VERIFY: in_bytes = m * (65 + 1 + 32 + 64); break;
+    }
+    const size_t rec_bytes = (j.kind == HostJob::VERIFY) ? 0 : m_pad * REC_ROWS * 4;
+    const size_t out_bytes = m * (65 + 20 + 1);
+    const size_t o_in = 0, o_rec = align_up(in_bytes, 256), o_out = o_rec + align_up(rec_bytes, 256);
+    int rc = dev_ensure_buf(d, o_out + out_bytes);
+    if (rc) return rc;
+    uint8_t* B = d.buf;
+    hipStream_t st = d.stream;
+    HIPCHK(hipStreamWaitEvent(st, d.last, 0));
+    uint8_t* o_pub = B + o_out;
+    uint8_t* o_addr = o_pub + m * 65;
+    uint8_t* o_st = o_addr + m * 20;
+    if (j.kind == HostJob::RECOVER) {
+      uint8_t* dm = B + o_in;
+      uint8_t* ds = dm + m * 32;
+      HIPCHK(hipMemcpyAsync(dm, j.a + base * 32, m * 32, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(ds, j.b + base * 65, m * 65, hipMemcpyHostToDevice, st));
+      uint32_t* rec = reinterpret_cast<uint32_t*>(B + o_rec);
+      HIPCHK(launch_prep_ecrecover(dm, ds, (uint32_t)m, (uint32_t)m_pad, rec, st));
+      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, j.addr ? o_addr : nullptr, j.pub ? o_pub : nullptr,
+                      d.gtab, d.ws};
+      HIPCHK(launch_recover(p, d.mb_recover, st));
+    } else if (j.kind == HostJob::SENDER) {
+      uint8_t* dh = B + o_in;
+      uint8_t* dr = dh + m * 32;
+      uint8_t* dsv = dr + m * 32;
+      uint8_t* dv = dsv + m * 32;
+      uint8_t* df = dv + m * 32;
+      HIPCHK(hipMemcpyAsync(dh, j.a + base * 32, m * 32, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(dr, j.b + base * 32, m * 32, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(dsv, j.c + base * 32, m * 32, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(dv, j.d + base * 32, m * 32, hipMemcpyHostToDevice, st));
+      if (j.e) HIPCHK(hipMemcpyAsync(df, j.e + base, m, hipMemcpyHostToDevice, st));
+      uint32_t* rec = reinterpret_cast<uint32_t*>(B + o_rec);
+      HIPCHK(launch_prep_sender(dh, dr, dsv, dv, j.e ? df : nullptr, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id,
+                                rec, st));
+      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
+      HIPCHK(launch_recover(p, d.mb_recover, st));
+    } else {
+      uint8_t* dp = B + o_in;
+      uint8_t* dl = dp + m * 65;
+      uint8_t* dm = dl + m;
+      uint8_t* ds = dm + m * 32;
+      HIPCHK(hipMemcpyAsync(dp, j.a + base * 65, m * 65, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(dl, j.b + base, m, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(dm, j.c + base * 32, m * 32, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(ds, j.d + base * 64, m * 64, hipMemcpyHostToDevice, st));
+      VerifyParams p{dp, dl, dm, ds, (uint32_t)m, o_st, d.gtab, d.ws};
+      HIPCHK(launch_verify(p, d.mb_verify, st));
+    }
+    HIPCHK(hipEventRecord(d.last, st));
+    if (j.pub) HIPCHK(hipMemcpyAsync(j.pub + base * 65, o_pub, m * 65, hipMemcpyDeviceToHost, st));
+    if (j.addr) HIPCHK(hipMemcpyAsync(j.addr + base * 20, o_addr, m * 20, hipMemcpyDeviceToHost, st));
+    if (j.status) HIPCHK(hipMemcpyAsync(j.status + base, o_st, m, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return EGES_SUCCESS;
+}
+
+// Contiguous index shards across the engine's devices.
+int run_host(const HostJob& j, size_t n) {
+  if (n == 0) return EGES_SUCCESS;
+  int rc = ensure_init();
+  if (rc) return rc;
+  std::vector<Dev*> devs;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    devs = g_devs;
+  }
+  if (devs.empty()) return set_err(EGES_E_NODEVICE, "no gfx950 device available");
+  // small batches stay on one device (a Geec block of 1000 txs is one tile set)
+  size_t ndev = std::min(devs.size(), std::max<size_t>(1, n / 65536));
+  const size_t per = (n + ndev - 1) / ndev;
+  if (ndev == 1) return run_host_shard(*devs[0], j, 0, n);
+  std::vector<int> rcs(ndev, EGES_SUCCESS);
+  std::vector<std::string> errs(ndev);
+  std::vector<std::thread> th;
+  for (size_t i = 0; i < ndev; ++i) {
+    const size_t lo = i * per, hi = std::min(n, lo + per);
+    if (lo >= hi) continue;
+    th.emplace_back([&, i, lo, hi] {
+      rcs[i] = run_host_shard(*devs[i], j, lo, hi - lo);
+      if (rcs[i]) errs[i] = t_err;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (size_t i = 0; i < ndev; ++i)
+    if (rcs[i]) return set_err(rcs[i], "device %d: %s", devs[i]->id, errs[i].c_str());
+  return EGES_SUCCESS;
+}
+
+// ------------------------------------------------------------------ host Keccak-256
+const uint64_t RC[24] = {0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808AULL, 0x8000000080008000ULL,
+                         0x000000000000808BULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
+                         0x000000000000008AULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000AULL,
+                         0x000000008000808BULL, 0x800000000000008BULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
+                         0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800AULL, 0x800000008000000AULL,
+                         0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+// rho offsets in the pi-permuted visiting order of the lane walk x,y -> y,2x+3y
+const int ROTC[24] = {1, 3, 6, 10, 15, 21, 28, 36, 45, 55, 2, 14, 27, 41, 56, 8, 25, 43, 62, 18, 39, 61, 20, 44};
+const int PILN[24] = {10, 7, 11, 17, 18, 3, 5, 16, 8, 21, 24, 4, 15, 23, 19, 13, 12, 2, 20, 14, 22, 9, 6, 1};
+
+inline uint64_t rol(uint64_t x, int s) { return (x << s) | (x >> (64 - s)); }
+
+void keccakf_host(uint64_t st[25]) {
+  for (int round = 0; round < 24; ++round) {
+    uint64_t bc[5];
+    for (int i = 0; i < 5; ++i) bc[i] = st[i] ^ st[i + 5] ^ st[i + 10] ^ st[i + 15] ^ st[i + 20];
+    for (int i = 0; i < 5; ++i) {
+      const uint64_t t = bc[(i + 4) % 5] ^ rol(bc[(i + 1) % 5], 1);
+      for (int j = 0; j < 25; j += 5) st[j + i] ^= t;
+    }
+    uint64_t t = st[1];
+    for (int i = 0; i < 24; ++i) {
+      const int j = PILN[i];
+      const uint64_t tmp = st[j];
+      st[j] = rol(t, ROTC[i]);
+      t = tmp;
+    }
+    for (int j = 0; j < 25; j += 5) {
+      for (int i = 0; i < 5; ++i) bc[i] = st[j + i];
+      for (int i = 0; i < 5; ++i) st[j + i] ^= (~bc[(i + 1) % 5]) & bc[(i + 2) % 5];
+    }
+    st[0] ^= RC[round];
+  }
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+int eges_abi_version(void) { return EGES_ABI_VERSION; }
+
+const char* eges_last_error(void) { return t_err.c_str(); }
+
+int eges_init(uint32_t device_mask, uint32_t flags) {
+  (void)flags;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_inited && !g_devs.empty()) return EGES_SUCCESS;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+    return set_err(EGES_E_NODEVICE, "no HIP device visible");
+  std::string errs;
+  for (int i = 0; i < count && i < 32; ++i) {
+    if (device_mask && !((device_mask >> i) & 1u)) continue;
+    Dev* d = nullptr;
+    int rc = init_device(i, &d);
+    if (rc == EGES_SUCCESS) g_devs.push_back(d);
+    else errs += t_err + "; ";
+  }
+  if (g_devs.empty()) return set_err(EGES_E_NODEVICE, "no usable gfx950 device (%s)", errs.c_str());
+  g_inited = true;
+  return EGES_SUCCESS;
+}
+
+void eges_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (Dev* d : g_devs) {
+    std::lock_guard<std::mutex> dl(d->mu);
+    DevGuard g(d->id);
+    (void)hipStreamSynchronize(d->stream);
+    (void)hipFree(d->gtab);
+    (void)hipFree(d->ws);
+    if (d->buf) (void)hipFree(d->buf);
+    (void)hipEventDestroy(d->last);
+    (void)hipStreamDestroy(d->stream);
+  }
+  for (Dev* d : g_devs) delete d;
+  g_devs.clear();
+  g_inited = false;
+}
+
+int eges_device_count(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return (int)g_devs.size();
+}
+
+int eges_ecrecover_batch(const uint8_t* msg, const uint8_t* sig, size_t n, uint8_t* pub_out, uint8_t* addr_out,
+                         uint8_t* status) {
+  if (n == 0) return EGES_SUCCESS;
+  if (!msg || !sig) return set_err(EGES_E_NULLPTR, "msg/sig is NULL");
+  std::vector<uint8_t> tmp;
+  HostJob j;
+  j.kind = HostJob::RECOVER;
+  j.a = msg;
+  j.b = sig;
+  j.pub = pub_out;
+  j.addr = addr_out;
+  if (!status) {
+    tmp.resize(n);
+    status = tmp.data();
+  }
+  j.status = status;
+  return run_host(j, n);
+}
+
+int eges_sender_batch(const uint8_t* sighash, const uint8_t* r, const uint8_t* s, const uint8_t* v, const uint8_t* vflags,
+                      size_t n, int signer, uint64_t chain_id, uint8_t* addr_out, uint8_t* status) {
+  if (n == 0) return EGES_SUCCESS;
+  if (!sighash || !r || !s || !v || !addr_out || !status) return set_err(EGES_E_NULLPTR, "NULL argument");
+  if (signer < 0 || signer > 2) return set_err(EGES_E_INVALID_ARG, "bad signer %d", signer);
+  HostJob j;
+  j.kind = HostJob::SENDER;
+  j.a = sighash;
+  j.b = r;
+  j.c = s;
+  j.d = v;
+  j.e = vflags;
+  j.signer = signer;
+  j.chain_id = chain_id;
+  j.addr = addr_out;
+  j.status = status;
+  return run_host(j, n);
+}
+
+int eges_verify_batch(const uint8_t* pub, const uint8_t* publen, const uint8_t* msg, const uint8_t* sig, size_t n,
+                      uint8_t* ok_out) {
+  if (n == 0) return EGES_SUCCESS;
+  if (!pub || !publen || !msg || !sig || !ok_out) return set_err(EGES_E_NULLPTR, "NULL argument");
+  HostJob j;
+  j.kind = HostJob::VERIFY;
+  j.a = pub;
+  j.b = publen;
+  j.c = msg;
+  j.d = sig;
+  j.status = ok_out;
+  return run_host(j, n);
+}
+
+int eges_ecdsa_recover(unsigned char* pubkey_out65, const unsigned char* sigdata65, const unsigned char* msgdata32) {
+  if (!pubkey_out65 || !sigdata65 || !msgdata32) return 0;
+  uint8_t st = EGES_RECOVER_FAILED;
+  uint8_t pub[65];
+  if (eges_ecrecover_batch(msgdata32, sigdata65, 1, pub, nullptr, &st) != EGES_SUCCESS) return 0;
+  if (st != EGES_OK) return 0;
+  std::memcpy(pubkey_out65, pub, 65);
+  return 1;
+}
+
+int eges_ecdsa_verify(const unsigned char* sigdata64, const unsigned char* msgdata32, const unsigned char* pubkeydata,
+                      size_t pubkeylen) {
+  if (!sigdata64 || !msgdata32 || !pubkeydata) return 0;
+  if (pubkeylen != 33 && pubkeylen != 65) return 0;  // eckey_pubkey_parse accepts only these sizes
+  uint8_t pub[65] = {0};
+  std::memcpy(pub, pubkeydata, pubkeylen);
+  const uint8_t len = (uint8_t)pubkeylen;
+  uint8_t ok = 0;
+  if (eges_verify_batch(pub, &len, msgdata32, sigdata64, 1, &ok) != EGES_SUCCESS) return 0;
+  return ok ? 1 : 0;
+}
+
+int eges_ecrecover_batch_dev(int device, const uint8_t* msg, const uint8_t* sig, size_t n, uint8_t* pub_out,
+                             uint8_t* addr_out, uint8_t* status, void* stream) {
+  if (n == 0) return EGES_SUCCESS;
+  if (!msg || !sig || !status) return set_err(EGES_E_NULLPTR, "NULL argument");
+  int rc = ensure_init();
+  if (rc) return rc;
+  Dev* d = dev_by_id(device);
+  if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
+  std::lock_guard<std::mutex> lk(d->mu);
+  DevGuard g(device);
+  return run_recover_dev(*d, msg, sig, n, pub_out, addr_out, status, stream ? (hipStream_t)stream : d->stream);
+}
+
+int eges_sender_batch_dev(int device, const uint8_t* sighash, const uint8_t* r, const uint8_t* s, const uint8_t* v,
+                          const uint8_t* vflags, size_t n, int signer, uint64_t chain_id, uint8_t* addr_out,
+                          uint8_t* status, void* stream) {
+  if (n == 0) return EGES_SUCCESS;
+  if (!sighash || !r || !s || !v || !addr_out || !status) return set_err(EGES_E_NULLPTR, "NULL argument");
+  if (signer < 0 || signer > 2) return set_err(EGES_E_INVALID_ARG, "bad signer %d", signer);
+  int rc = ensure_init();
+  if (rc) return rc;
+  Dev* d = dev_by_id(device);
+  if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
+  std::lock_guard<std::mutex> lk(d->mu);
+  DevGuard g(device);
+  return run_sender_dev(*d, sighash, r, s, v, vflags, n, signer, chain_id, addr_out, status,
+                        stream ? (hipStream_t)stream : d->stream);
+}
+
+int eges_verify_batch_dev(int device, const uint8_t* pub, const uint8_t* publen, const uint8_t* msg, const uint8_t* sig,
+                          size_t n, uint8_t* ok_out, void* stream) {
+  if (n == 0) return EGES_SUCCESS;
+  if (!pub || !publen || !msg || !sig || !ok_out) return set_err(EGES_E_NULLPTR, "NULL argument");
+  int rc = ensure_init();
+  if (rc) return rc;
+  Dev* d = dev_by_id(device);
+  if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
+  std::lock_guard<std::mutex> lk(d->mu);
+  DevGuard g(device);
+  return run_verify_dev(*d, pub, publen, msg, sig, n, ok_out, stream ? (hipStream_t)stream : d->stream);
+}
+
+int eges_synth_sign_dev(int device, uint64_t first_index, size_t n, uint8_t* msg, uint8_t* sig, uint8_t* addr_expected,
+                        void* stream) {
+  if (n == 0) return EGES_SUCCESS;
+  if (!msg || !sig || !addr_expected) return set_err(EGES_E_NULLPTR, "NULL argument");
+  int rc = ensure_init();
+  if (rc) return rc;
+  Dev* d = dev_by_id(device);
+  if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
+  std::lock_guard<std::mutex> lk(d->mu);
+  DevGuard g(device);
+  hipStream_t st = stream ? (hipStream_t)stream : d->stream;
+  Serial ser(*d, st);
+  for (size_t off = 0; off < n; off += CHUNK) {
+    const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
+    SynthParams p{first_index + off, m, msg + off * 32, sig + off * 65, addr_expected + off * 20, d->gtab, d->ws};
+    HIPCHK(launch_synth(p, d->mb_synth, st));
+  }
+  return EGES_SUCCESS;
+}
+
+void eges_keccak256(const uint8_t* data, size_t len, uint8_t* out32) {
+  uint64_t st[25] = {0};
+  const size_t rate = 136;
+  while (len >= rate) {
+    for (size_t i = 0; i < rate / 8; ++i) {
+      uint64_t w = 0;
+      for (int b = 0; b < 8; ++b) w |= (uint64_t)data[8 * i + b] << (8 * b);
+      st[i] ^= w;
+    }
+    keccakf_host(st);
+    data += rate;
+    len -= rate;
+  }
+  uint8_t blk[136] = {0};
+  if (len) std::memcpy(blk, data, len);
+  blk[len] ^= 0x01;
+  blk[rate - 1] ^= 0x80;
+  for (size_t i = 0; i < rate / 8; ++i) {
+    uint64_t w = 0;
+    for (int b = 0; b < 8; ++b) w |= (uint64_t)blk[8 * i + b] << (8 * b);
+    st[i] ^= w;
+  }
+  keccakf_host(st);
+  for (int i = 0; i < 32; ++i) out32[i] = (uint8_t)(st[i / 8] >> (8 * (i % 8)));
+}
+
+}  // extern "C"

@@ -1,0 +1,363 @@
+#pragma once
+// Shared device core of the secp256k1 sender-recovery kernels (gfx950).
+//
+// Hot path: for every signature record
+//   parse (r, s, recid) ........... recovery/main_impl.h:38-58 (overflow => failure)
+//   x = r (+ n if recid & 2) ...... main_impl.h:101-109
+//   R = lift_x(x, recid & 1) ...... group_impl.h:216-237 via (p+1)/4 sqrt, field_impl.h:38-134
+//   r^-1 mod n .................... scalar_impl.h:262-281 -> workgroup Montgomery batch inversion
+//   u1 = -z/r, u2 = s/r ........... main_impl.h:114-117 (z = msg mod n, :183)
+//   Q = u2*R + u1*G ............... ecmult_impl.h:286-404 -> GLV + Strauss, fixed 4-bit signed
+//                                   windows for R / lambda*R (per-lane 8-entry affine table) and
+//                                   12-bit signed windows for G / lambda*G (2 x 2048-entry tables)
+//   Q == infinity => failure ...... main_impl.h:120
+//   affine (batch inversion), serialize 04||X||Y (eckey_impl.h:36-52), Keccak-256 address
+//                                   (crypto.go:194-197, transaction_signing.go:245)
+//
+// Execution model: 256-thread workgroups (4 waves), one signature per lane, persistent
+// grid-stride over 256-signature tiles. Three workgroup-level Montgomery batch inversions
+// per tile (r mod n, the R-table Z's mod p, the final Z mod p) amortise each exponentiation
+// over 256 signatures. All control flow that depends on data is either per-lane selects or
+// wave-uniform (ballot) branches for the rare exceptional additions.
+#include "fe.cuh"
+#include "sc.cuh"
+#include "ge.cuh"
+#include "keccak.cuh"
+#include "launch.h"
+
+namespace eges {
+
+constexpr int WG = 256;
+constexpr int NWAVES = WG / 64;
+constexpr int RWIN = 33;    // 4-bit signed windows over |k| < 2^129 (132 bits)
+constexpr int GWIN = 11;    // 12-bit signed windows (132 bits)
+constexpr int GTAB = 2048;  // {1..2048}*G and {1..2048}*lambda*G
+constexpr int PTAB = 8;     // {1..8}*R per lane
+
+enum : uint32_t {
+  ST_OK = 0, ST_INVALID_CHAIN_ID = 1, ST_INVALID_SIG = 2, ST_INVALID_RECOVERY_ID = 5, ST_RECOVER_FAILED = 6
+};
+
+__constant__ const uint32_t FE_BETA[8] = {0x719501EEu, 0xC1396C28u, 0x12F58995u, 0x9CF04975u,
+                                          0xAC3434E9u, 0x6E64479Eu, 0x657C0710u, 0x7AE96A2Bu};
+__constant__ const uint32_t GEN_X[8] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu,
+                                        0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu};
+__constant__ const uint32_t GEN_Y[8] = {0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u,
+                                        0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
+// p - n  (recovery/main_impl.h:104, ecdsa_impl.h:45-47)
+__constant__ const uint32_t P_MINUS_N[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75FC4u, 0x45512319u,
+                                            0x00000001u, 0u, 0u, 0u};
+
+DEV fe fe_const(const uint32_t* c) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = c[i];
+  return r;
+}
+DEV ge gen_point() {
+  ge g;
+  g.x = fe_const(GEN_X);
+  g.y = fe_const(GEN_Y);
+  return g;
+}
+
+// ------------------------------------------------------------------ cross-lane helpers
+template <class T>
+DEV T shfl_up_t(const T& x, int d) {
+  T r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = (uint32_t)__shfl_up((int)x.v[i], d, 64);
+  return r;
+}
+template <class T>
+DEV T shfl_down_t(const T& x, int d) {
+  T r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = (uint32_t)__shfl_down((int)x.v[i], d, 64);
+  return r;
+}
+
+struct FieldOps {
+  using T = fe;
+  static DEV T one() { return fe_one(); }
+  static DEV T mul(const T& a, const T& b) { return fe_mul(a, b); }
+  static DEV T inv(const T& a) { return fe_inv(a); }
+  static DEV T sel(bool c, const T& a, const T& b) { return fe_select(c, a, b); }
+};
+struct ScalarOps {
+  using T = sc;
+  static DEV T one() { return sc_one(); }
+  static DEV T mul(const T& a, const T& b) { return sc_mul(a, b); }
+  static DEV T inv(const T& a) { return sc_inv(a); }
+  static DEV T sel(bool c, const T& a, const T& b) { return sc_select(c, a, b); }
+};
+
+// Workgroup Montgomery batch inversion: returns a^-1 for valid lanes (garbage otherwise).
+// Invalid lanes contribute 1 to the products so they cannot poison the batch.
+// lds: at least 2 * NWAVES * 8 words. Every thread of the workgroup must call this.
+template <class Ops>
+DEV typename Ops::T wg_batch_inv(const typename Ops::T& a, bool valid, uint32_t* lds) {
+  using T = typename Ops::T;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  T x = Ops::sel(valid, a, Ops::one());
+  T P = x;  // inclusive prefix product within the wave
+#pragma unroll 1
+  for (int d = 1; d < 64; d <<= 1) {
+    T y = shfl_up_t(P, d);
+    T m = Ops::mul(P, y);
+    P = Ops::sel(lane >= d, m, P);
+  }
+  T Q = x;  // inclusive suffix product
+#pragma unroll 1
+  for (int d = 1; d < 64; d <<= 1) {
+    T y = shfl_down_t(Q, d);
+    T m = Ops::mul(Q, y);
+    Q = Ops::sel(lane + d < 64, m, Q);
+  }
+  T pex = Ops::sel(lane == 0, Ops::one(), shfl_up_t(P, 1));
+  T sex = Ops::sel(lane == 63, Ops::one(), shfl_down_t(Q, 1));
+  if (lane == 63) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) lds[wave * 8 + i] = P.v[i];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    T t[NWAVES];
+#pragma unroll
+    for (int w = 0; w < NWAVES; ++w)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t[w].v[i] = lds[w * 8 + i];
+    T tot = t[0];
+#pragma unroll
+    for (int w = 1; w < NWAVES; ++w) tot = Ops::mul(tot, t[w]);
+    T inv = Ops::inv(tot);
+    const int me = lane & (NWAVES - 1);
+#pragma unroll
+    for (int w = 0; w < NWAVES; ++w) inv = Ops::mul(inv, Ops::sel(w == me, Ops::one(), t[w]));
+    if (lane < NWAVES) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) lds[NWAVES * 8 + lane * 8 + i] = inv.v[i];
+    }
+  }
+  __syncthreads();
+  T winv;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) winv.v[i] = lds[NWAVES * 8 + wave * 8 + i];
+  __syncthreads();  // lds is reused by the next call
+  return Ops::mul(Ops::mul(winv, pex), sex);
+}
+
+// ------------------------------------------------------------------ digit recoding
+// Signed fixed-window recoding of a GLV half (|k| < 2^129) into NW digits of W bits,
+// digits in [-2^(W-1), 2^(W-1)], the half's sign folded in. Written to LDS [w][WG].
+template <int W, int NW, class D>
+DEV void recode(const glv_half& h, D* out /* [NW][WG] */) {
+  uint32_t m[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) m[i] = h.mag[i];
+  int carry = 0;
+  const int tid = threadIdx.x;
+#pragma unroll 1
+  for (int w = 0; w < NW; ++w) {
+    int v = (int)(m[0] & ((1u << W) - 1)) + carry;
+    carry = v >= (1 << (W - 1)) ? 1 : 0;
+    v -= carry << W;
+    out[w * WG + tid] = (D)(h.neg ? -v : v);
+    // m >>= W
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m[i] = (m[i] >> W) | (m[i + 1] << (32 - W));
+    m[4] >>= W;
+  }
+}
+
+// ------------------------------------------------------------------ tables
+DEV void store_pt(uint32_t* dst, const ge& p) {
+  fe x = fe_normalize(p.x), y = fe_normalize(p.y);
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  d[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+  d[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+  d[2] = make_uint4(y.v[0], y.v[1], y.v[2], y.v[3]);
+  d[3] = make_uint4(y.v[4], y.v[5], y.v[6], y.v[7]);
+}
+DEV ge load_pt(const uint32_t* src) {
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  uint4 a = s[0], b = s[1], c = s[2], d = s[3];
+  ge p;
+  p.x.v[0] = a.x; p.x.v[1] = a.y; p.x.v[2] = a.z; p.x.v[3] = a.w;
+  p.x.v[4] = b.x; p.x.v[5] = b.y; p.x.v[6] = b.z; p.x.v[7] = b.w;
+  p.y.v[0] = c.x; p.y.v[1] = c.y; p.y.v[2] = c.z; p.y.v[3] = c.w;
+  p.y.v[4] = d.x; p.y.v[5] = d.y; p.y.v[6] = d.z; p.y.v[7] = d.w;
+  return p;
+}
+
+// ------------------------------------------------------------------ Strauss step
+// acc += p when `use`; acc_inf tracks the point at infinity. Exceptional sums (acc == +-p)
+// are resolved exactly on a wave-uniform slow path.
+DEV void add_step(gej& acc, bool& inf, const ge& p, bool use) {
+  bool hz, rz;
+  gej s = gej_add_ge(acc, p, hz, rz);
+  const bool exc = use && !inf && hz;
+  if (__any(exc)) {
+    gej d = gej_double(acc);
+    s = gej_select(exc && rz, d, s);
+  }
+  const bool to_inf = exc && !rz;
+  gej pj = gej_from_ge(p);
+  gej nacc = gej_select(inf, pj, s);
+  acc = gej_select(use, nacc, acc);
+  inf = use ? (inf ? false : to_inf) : inf;
+}
+
+DEV ge neg_if(const ge& p, bool neg) {
+  ge r;
+  r.x = p.x;
+  r.y = fe_select(neg, fe_neg(p.y), p.y);
+  return r;
+}
+
+struct CoreLds {
+  int8_t rdig[2][RWIN][WG];    // R / lambda R digits
+  int16_t gdig[2][GWIN][WG];   // G / lambda G digits
+  uint32_t inv_scratch[2 * NWAVES * 8];
+};
+
+// Per-block workspace (global memory, this block's lanes only):
+//   [0, PTAB*WG*16)            affine table {1..8}*P, entry-major then lane, 16 words/entry
+//   [PTAB*WG*16, +(PTAB-1)*WG*16)  Z_i and prefix products while the table is built
+constexpr size_t WS_WORDS = (size_t)(2 * PTAB - 1) * WG * 16;
+
+DEV void store_fe2(uint32_t* dst, const fe& a, const fe& b) {
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  d[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+  d[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+  d[2] = make_uint4(b.v[0], b.v[1], b.v[2], b.v[3]);
+  d[3] = make_uint4(b.v[4], b.v[5], b.v[6], b.v[7]);
+}
+
+// Q = u_r * P + u_g * G for the workgroup's 256 lanes. P given affine (a valid curve point,
+// possibly a dummy for failed lanes). Returns Jacobian Q and its infinity flag.
+DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& u_g, const uint32_t* gtab,
+                     uint32_t* ws, CoreLds& L) {
+  const int tid = threadIdx.x;
+  uint32_t* const base = ws + (size_t)blockIdx.x * WS_WORDS;
+  uint32_t* const zp = base + (size_t)PTAB * WG * 16;
+  // --- digits
+  {
+    glv_half h1, h2;
+    glv_split(h1, h2, u_r);
+    recode<4, RWIN, int8_t>(h1, &L.rdig[0][0][0]);
+    recode<4, RWIN, int8_t>(h2, &L.rdig[1][0][0]);
+    glv_split(h1, h2, u_g);
+    recode<12, GWIN, int16_t>(h1, &L.gdig[0][0][0]);
+    recode<12, GWIN, int16_t>(h2, &L.gdig[1][0][0]);
+  }
+  // --- per-lane table {1..8} * P: Jacobian T_{i+1} = T_i + P streamed to the workspace,
+  //     then one workgroup batch inversion of prod Z_i and a backward Montgomery pass.
+  {
+    store_pt(base + (size_t)tid * 16, P);
+    gej T;
+    T.x = P.x;
+    T.y = P.y;
+    T.z = fe_one();
+    T = gej_double(T);
+    fe pre = T.z;
+    store_fe2(base + (size_t)(1 * WG + tid) * 16, T.x, T.y);
+    store_fe2(zp + (size_t)(0 * WG + tid) * 16, T.z, pre);
+#pragma unroll 1
+    for (int i = 2; i < PTAB; ++i) {
+      bool hz, rz;
+      T = gej_add_ge(T, P, hz, rz);  // i*P + P, never exceptional for i < 8 < n
+      pre = fe_mul(pre, T.z);
+      store_fe2(base + (size_t)(i * WG + tid) * 16, T.x, T.y);
+      store_fe2(zp + (size_t)((i - 1) * WG + tid) * 16, T.z, pre);
+    }
+    fe inv = wg_batch_inv<FieldOps>(pre, true, L.inv_scratch);  // 1 / (Z_1 ... Z_7)
+#pragma unroll 1
+    for (int i = PTAB - 1; i >= 1; --i) {
+      const ge zz = load_pt(zp + (size_t)((i - 1) * WG + tid) * 16);  // .x = Z_i
+      fe zi = inv;
+      if (i > 1) {
+        const ge pp = load_pt(zp + (size_t)((i - 2) * WG + tid) * 16);  // .y = pre_{i-1}
+        zi = fe_mul(inv, pp.y);
+        inv = fe_mul(inv, zz.x);
+      }
+      const ge J = load_pt(base + (size_t)(i * WG + tid) * 16);
+      const fe zi2 = fe_sqr(zi);
+      ge a;
+      a.x = fe_mul(J.x, zi2);
+      a.y = fe_mul(J.y, fe_mul(zi2, zi));
+      store_pt(base + (size_t)(i * WG + tid) * 16, a);
+    }
+  }
+  // --- Strauss-Shamir: 33 windows of 4 bits (R, lambda R) interleaved with 11 windows of
+  //     12 bits (G, lambda G) every third window.
+  inf = true;
+  acc.x = fe_zero();
+  acc.y = fe_zero();
+  acc.z = fe_zero();
+#pragma unroll 1
+  for (int w = RWIN - 1; w >= 0; --w) {
+    if (w != RWIN - 1) {
+#pragma unroll 1
+      for (int k = 0; k < 4; ++k) acc = gej_double(acc);
+    }
+    const int nadd = (w % 3) == 0 ? 4 : 2;
+#pragma unroll 1
+    for (int j = 0; j < nadd; ++j) {
+      int d;
+      if (j < 2) d = L.rdig[j][w][tid];
+      else d = L.gdig[j - 2][w / 3][tid];
+      const int a = d < 0 ? -d : d;
+      const int e = a > 0 ? a - 1 : 0;
+      ge p;
+      if (j < 2) p = load_pt(base + (size_t)(e * WG + tid) * 16);
+      else p = load_pt(gtab + ((size_t)(j - 2) * GTAB + e) * 16);
+      if (j == 1) p.x = fe_mul(p.x, fe_const(FE_BETA));
+      add_step(acc, inf, neg_if(p, d < 0), d != 0);
+    }
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------ byte helpers
+DEV void limbs_from_be32(uint32_t out[8], const uint8_t* b) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint8_t* q = b + 28 - 4 * i;
+    out[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+}
+DEV void write_be32(uint8_t* dst, const fe& x) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint32_t w = x.v[7 - i];
+    dst[4 * i + 0] = (uint8_t)(w >> 24);
+    dst[4 * i + 1] = (uint8_t)(w >> 16);
+    dst[4 * i + 2] = (uint8_t)(w >> 8);
+    dst[4 * i + 3] = (uint8_t)w;
+  }
+}
+DEV uint64_t be_word(const fe& x, int k) {  // little-endian 64-bit word k of the BE encoding
+  return (uint64_t)__builtin_bswap32(x.v[7 - 2 * k]) | ((uint64_t)__builtin_bswap32(x.v[6 - 2 * k]) << 32);
+}
+
+// Keccak-256(X || Y)[12:32] as 5 little-endian words.
+DEV void pub_address(uint32_t a[5], const fe& X, const fe& Y) {
+  uint64_t w[17];
+#pragma unroll
+  for (int k = 0; k < 17; ++k) w[k] = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    w[k] = be_word(X, k);
+    w[4 + k] = be_word(Y, k);
+  }
+  uint64_t h[4];
+  keccak256_1block<64>(w, h);
+  a[0] = (uint32_t)(h[1] >> 32);
+  a[1] = (uint32_t)h[2];
+  a[2] = (uint32_t)(h[2] >> 32);
+  a[3] = (uint32_t)h[3];
+  a[4] = (uint32_t)(h[3] >> 32);
+}
+
+}  // namespace eges

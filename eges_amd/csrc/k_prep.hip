@@ -1,0 +1,190 @@
+// Table-initialisation and record-preparation kernels (gfx950).
+#include "core.cuh"
+
+namespace eges {
+
+// Fixed-base tables: gtab[t][e] = (e+1) * (t ? lambda*G : G), affine, 16 words per entry.
+// One thread per entry; simple double-and-add + Fermat inversion (runs once per device).
+__global__ void __launch_bounds__(256) init_gtab_kernel(uint32_t* gtab) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= GTAB) return;
+  const uint32_t k = (uint32_t)e + 1;
+  const ge g = gen_point();
+  gej acc = gej_from_ge(g);
+  int top = 31 - __clz(k);
+  for (int b = top - 1; b >= 0; --b) {
+    acc = gej_double(acc);
+    if ((k >> b) & 1u) {
+      bool hz, rz;
+      acc = gej_add_ge(acc, g, hz, rz);  // m*G + G with 2 <= m < n-1: never exceptional
+    }
+  }
+  fe zi = fe_inv(acc.z);
+  fe zi2 = fe_sqr(zi);
+  ge a;
+  a.x = fe_mul(acc.x, zi2);
+  a.y = fe_mul(acc.y, fe_mul(zi2, zi));
+  store_pt(gtab + (size_t)e * 16, a);
+  ge l = a;
+  l.x = fe_mul(a.x, fe_const(FE_BETA));
+  store_pt(gtab + ((size_t)GTAB + e) * 16, l);
+}
+
+// ------------------------------------------------------------------ prep kernels
+// Record layout consumed by the recover kernel (SoA, stride n_pad words):
+//   z[8], r[8], s[8] little-endian limbs of the raw 256-bit values; meta = recid | status << 8
+__global__ void __launch_bounds__(256) prep_ecrecover_kernel(const uint8_t* __restrict__ msg,
+                                                             const uint8_t* __restrict__ sig, uint32_t n,
+                                                             uint32_t n_pad, uint32_t* __restrict__ rec) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t z[8], r[8], s[8];
+  limbs_from_be32(z, msg + (size_t)i * 32);
+  limbs_from_be32(r, sig + (size_t)i * 65);
+  limbs_from_be32(s, sig + (size_t)i * 65 + 32);
+  const uint32_t v = sig[(size_t)i * 65 + 64];
+  // checkSignature (secp256.go:171-179): recid >= 4 => ErrInvalidRecoveryID
+  const uint32_t meta = v >= 4 ? (ST_INVALID_RECOVERY_ID << 8) : v;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    rec[(size_t)k * n_pad + i] = z[k];
+    rec[(size_t)(8 + k) * n_pad + i] = r[k];
+    rec[(size_t)(16 + k) * n_pad + i] = s[k];
+  }
+  rec[(size_t)24 * n_pad + i] = meta;
+}
+
+DEV int bitlen_limbs(const uint32_t x[8]) {
+  int bl = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (x[i]) bl = 32 * i + (32 - __clz(x[i]));
+  return bl;
+}
+
+// types.Sender classification (transaction_signing.go:127-137,182-184,218-247, crypto.go:181-192,
+// transaction.go:142-149, deriveChainId :250-260). Items that fail before the C call get their
+// Go error as status; the rest become ecrecover records with recid = v.
+__global__ void __launch_bounds__(256) prep_sender_kernel(const uint8_t* __restrict__ sighash,
+                                                          const uint8_t* __restrict__ rb,
+                                                          const uint8_t* __restrict__ sb,
+                                                          const uint8_t* __restrict__ vb,
+                                                          const uint8_t* __restrict__ vflags, uint32_t n,
+                                                          uint32_t n_pad, int signer, uint64_t chain_id,
+                                                          uint32_t* __restrict__ rec) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t z[8], r[8], s[8], v[8];
+  limbs_from_be32(z, sighash + (size_t)i * 32);
+  limbs_from_be32(r, rb + (size_t)i * 32);
+  limbs_from_be32(s, sb + (size_t)i * 32);
+  limbs_from_be32(v, vb + (size_t)i * 32);
+  const uint32_t f = vflags ? vflags[i] : 0u;
+  const bool v_wide = f & 1u, r_wide = f & 2u, s_wide = f & 4u;
+  uint32_t status = ST_OK;
+  bool homestead = signer != 0;
+  // Vb: the V handed to recoverPlain
+  uint32_t vb8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) vb8[k] = v[k];
+  bool vb_wide = v_wide;
+  if (signer == 2) {
+    const int bl = v_wide ? 1000 : bitlen_limbs(v);
+    const bool prot = bl <= 8 ? !(v[0] == 27u || v[0] == 28u) : true;
+    if (prot) {
+      bool match;
+      if (bl <= 64) {
+        const uint64_t vv = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+        const uint64_t cid = (vv == 27 || vv == 28) ? 0 : (vv - 35) / 2;  // uint64 wrap as Go
+        match = cid == chain_id;
+      } else if (v_wide) {
+        match = false;
+      } else {
+        // (V - 35) >> 1 == chain_id, V >= 2^64 so no underflow
+        uint32_t t[8];
+        uint64_t br = 35;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint64_t d = (uint64_t)v[k] - br;
+          t[k] = (uint32_t)d;
+          br = (d >> 63) & 1;
+        }
+        bool hi0 = (t[2] >> 1) == 0;
+#pragma unroll
+        for (int k = 3; k < 8; ++k) hi0 = hi0 && t[k] == 0;
+        const uint64_t sh = ((uint64_t)t[0] >> 1) | ((uint64_t)t[1] << 31) | ((uint64_t)(t[2] & 1u) << 63);
+        match = hi0 && sh == chain_id;
+      }
+      if (!match) {
+        status = ST_INVALID_CHAIN_ID;
+      } else {
+        // V' = V - 2*chainId - 8 (big.Int, no wrap)
+        const uint64_t lo = chain_id * 2 + 8;
+        const uint32_t hi = (uint32_t)((chain_id >> 63) & 1u) + (uint32_t)(chain_id * 2 + 8 < 8 ? 1 : 0);
+        uint32_t sub[8] = {(uint32_t)lo, (uint32_t)(lo >> 32), hi, 0, 0, 0, 0, 0};
+        uint64_t br = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint64_t d = (uint64_t)v[k] - sub[k] - br;
+          vb8[k] = (uint32_t)d;
+          br = (d >> 63) & 1;
+        }
+        vb_wide = false;
+      }
+    }
+    homestead = true;
+  }
+  uint32_t recid = 0;
+  if (status == ST_OK) {
+    // recoverPlain :223-229
+    if (vb_wide || bitlen_limbs(vb8) > 8) {
+      status = ST_INVALID_SIG;
+    } else {
+      const uint32_t vv = (vb8[0] - 27u) & 0xffu;
+      // ValidateSignatureValues (crypto.go:181-192)
+      bool r_zero = true, s_zero = true;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { r_zero = r_zero && r[k] == 0; s_zero = s_zero && s[k] == 0; }
+      const bool r_lt_1 = !r_wide && r_zero, s_lt_1 = !s_wide && s_zero;
+      const bool s_high = s_wide || !u256_ge(SC_HALF, s);
+      const bool r_ge_n = r_wide || u256_ge(r, SC_N), s_ge_n = s_wide || u256_ge(s, SC_N);
+      if (r_lt_1 || s_lt_1 || (homestead && s_high) || r_ge_n || s_ge_n || !(vv == 0 || vv == 1))
+        status = ST_INVALID_SIG;
+      else
+        recid = vv;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    rec[(size_t)k * n_pad + i] = z[k];
+    rec[(size_t)(8 + k) * n_pad + i] = r[k];
+    rec[(size_t)(16 + k) * n_pad + i] = s[k];
+  }
+  rec[(size_t)24 * n_pad + i] = recid | (status << 8);
+}
+
+// ------------------------------------------------------------------ launchers
+hipError_t launch_init_gtab(uint32_t* gtab, hipStream_t st) {
+  hipLaunchKernelGGL(init_gtab_kernel, dim3((GTAB + 255) / 256), dim3(256), 0, st, gtab);
+  return hipGetLastError();
+}
+
+hipError_t launch_prep_ecrecover(const uint8_t* msg, const uint8_t* sig, uint32_t n, uint32_t n_pad, uint32_t* rec,
+                                 hipStream_t st) {
+  hipLaunchKernelGGL(prep_ecrecover_kernel, dim3((n + 255) / 256), dim3(256), 0, st, msg, sig, n, n_pad, rec);
+  return hipGetLastError();
+}
+
+hipError_t launch_prep_sender(const uint8_t* sighash, const uint8_t* r, const uint8_t* s, const uint8_t* v,
+                              const uint8_t* vflags, uint32_t n, uint32_t n_pad, int signer, uint64_t chain_id,
+                              uint32_t* rec, hipStream_t st) {
+  hipLaunchKernelGGL(prep_sender_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sighash, r, s, v, vflags, n, n_pad,
+                     signer, chain_id, rec);
+  return hipGetLastError();
+}
+
+size_t ws_bytes_per_block() { return WS_WORDS * sizeof(uint32_t); }
+size_t gtab_bytes() { return (size_t)2 * GTAB * 16 * sizeof(uint32_t); }
+int threads_per_block() { return WG; }
+
+}  // namespace eges

@@ -1,0 +1,60 @@
+// Internal interface between the C-ABI layer (capi.hip) and the kernels (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace eges {
+
+// Record layout produced by the prep kernels: 25 SoA rows of n_pad words
+// (z[8], r[8], s[8], meta) — see kernels.hip.
+constexpr int REC_ROWS = 25;
+
+struct RecoverParams {
+  const uint32_t* rec;
+  uint32_t n, n_pad;
+  uint8_t* status;
+  uint8_t* addr;  // nullable, n*20
+  uint8_t* pub;   // nullable, n*65
+  const uint32_t* gtab;
+  uint32_t* ws;
+};
+
+struct VerifyParams {
+  const uint8_t* pub;
+  const uint8_t* publen;
+  const uint8_t* msg;
+  const uint8_t* sig;
+  uint32_t n;
+  uint8_t* ok;
+  const uint32_t* gtab;
+  uint32_t* ws;
+};
+
+struct SynthParams {
+  uint64_t first;
+  uint32_t n;
+  uint8_t* msg;
+  uint8_t* sig;
+  uint8_t* addr;
+  const uint32_t* gtab;
+  uint32_t* ws;
+};
+
+hipError_t launch_init_gtab(uint32_t* gtab, hipStream_t st);
+hipError_t launch_prep_ecrecover(const uint8_t* msg, const uint8_t* sig, uint32_t n, uint32_t n_pad, uint32_t* rec,
+                                 hipStream_t st);
+hipError_t launch_prep_sender(const uint8_t* sighash, const uint8_t* r, const uint8_t* s, const uint8_t* v,
+                              const uint8_t* vflags, uint32_t n, uint32_t n_pad, int signer, uint64_t chain_id,
+                              uint32_t* rec, hipStream_t st);
+hipError_t launch_recover(const RecoverParams& p, int max_blocks, hipStream_t st);
+hipError_t launch_verify(const VerifyParams& p, int max_blocks, hipStream_t st);
+hipError_t launch_synth(const SynthParams& p, int max_blocks, hipStream_t st);
+int occupancy_recover();
+int occupancy_verify();
+int occupancy_synth();
+size_t ws_bytes_per_block();
+size_t gtab_bytes();
+int threads_per_block();
+
+}  // namespace eges

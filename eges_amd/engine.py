@@ -1,0 +1,119 @@
+"""Batch entry points over numpy host buffers and torch device tensors.
+
+Thin, allocation-only wrappers around libeges.so; all arithmetic happens in the HIP kernels.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+
+def _u8(a, shape_tail, name):
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    if a.ndim != 1 + len(shape_tail) or tuple(a.shape[1:]) != tuple(shape_tail):
+        raise ValueError(f"{name}: expected shape (n, {', '.join(map(str, shape_tail))}), got {a.shape}")
+    return a
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def init(device_mask=0):
+    check(lib.eges_init(device_mask, 0))
+    return lib.eges_device_count()
+
+
+def device_count():
+    return lib.eges_device_count()
+
+
+def ecrecover_batch(msg, sig, want_pub=True, want_addr=True):
+    """crypto.Ecrecover over n items: msg (n,32), sig (n,65) -> (pub (n,65)|None, addr (n,20)|None, status (n,))."""
+    msg = _u8(msg, (32,), "msg")
+    sig = _u8(sig, (65,), "sig")
+    n = msg.shape[0]
+    if sig.shape[0] != n:
+        raise ValueError("msg/sig length mismatch")
+    pub = np.zeros((n, 65), np.uint8) if want_pub else None
+    addr = np.zeros((n, 20), np.uint8) if want_addr else None
+    status = np.zeros(n, np.uint8)
+    if n:
+        check(lib.eges_ecrecover_batch(_p(msg), _p(sig), n, _p(pub), _p(addr), _p(status)))
+    return pub, addr, status
+
+
+def sender_batch(sighash, r, s, v, vflags, signer, chain_id):
+    """types.Sender over n items (big-endian 32-byte r/s/v + EGES_VF_* flags) -> (addr (n,20), status (n,))."""
+    sighash = _u8(sighash, (32,), "sighash")
+    r = _u8(r, (32,), "r")
+    s = _u8(s, (32,), "s")
+    v = _u8(v, (32,), "v")
+    n = sighash.shape[0]
+    vflags = np.zeros(n, np.uint8) if vflags is None else np.ascontiguousarray(vflags, dtype=np.uint8)
+    addr = np.zeros((n, 20), np.uint8)
+    status = np.zeros(n, np.uint8)
+    if n:
+        check(lib.eges_sender_batch(_p(sighash), _p(r), _p(s), _p(v), _p(vflags), n, int(signer), int(chain_id),
+                                    _p(addr), _p(status)))
+    return addr, status
+
+
+def verify_batch(pub, publen, msg, sig):
+    """crypto.VerifySignature over n items: pub (n,65) left-aligned, publen (n,), msg (n,32), sig (n,64) -> ok (n,)."""
+    pub = _u8(pub, (65,), "pub")
+    msg = _u8(msg, (32,), "msg")
+    sig = _u8(sig, (64,), "sig")
+    publen = np.ascontiguousarray(publen, dtype=np.uint8)
+    n = pub.shape[0]
+    ok = np.zeros(n, np.uint8)
+    if n:
+        check(lib.eges_verify_batch(_p(pub), _p(publen), _p(msg), _p(sig), n, _p(ok)))
+    return ok
+
+
+def keccak256(data):
+    data = bytes(data)
+    a = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
+    out = np.zeros(32, np.uint8)
+    lib.eges_keccak256(_p(a), len(data), _p(out))
+    return out.tobytes()
+
+
+# ------------------------------------------------------------------ torch device tensors
+def _tp(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream_of(t):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def ecrecover_batch_dev(msg, sig, pub=None, addr=None, status=None, stream=None):
+    """Device-resident batch: uint8 CUDA(HIP) tensors msg (n,32), sig (n,65); outputs allocated if None.
+    Enqueued on `stream` (default: torch's current stream of the tensors' device); asynchronous."""
+    import torch
+    n = msg.shape[0]
+    dev = msg.device
+    if addr is None:
+        addr = torch.empty((n, 20), dtype=torch.uint8, device=dev)
+    if status is None:
+        status = torch.empty((n,), dtype=torch.uint8, device=dev)
+    st = ctypes.c_void_p(stream) if stream is not None else _stream_of(msg)
+    check(lib.eges_ecrecover_batch_dev(dev.index, _tp(msg), _tp(sig), n, _tp(pub), _tp(addr), _tp(status), st))
+    return pub, addr, status
+
+
+def synth_sign_dev(first_index, n, device, stream=None):
+    """Deterministic synthetic signed batch on `device` -> (msg (n,32), sig (n,65), expected addr (n,20))."""
+    import torch
+    dev = torch.device("cuda", device) if isinstance(device, int) else device
+    msg = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    sig = torch.empty((n, 65), dtype=torch.uint8, device=dev)
+    addr = torch.empty((n, 20), dtype=torch.uint8, device=dev)
+    st = ctypes.c_void_p(stream) if stream is not None else _stream_of(msg)
+    check(lib.eges_synth_sign_dev(dev.index, int(first_index), n, _tp(msg), _tp(sig), _tp(addr), st))
+    return msg, sig, addr

@@ -1,0 +1,148 @@
+/*
+ * eges.h — C-ABI of the MI355X-native secp256k1 sender-recovery engine (libeges.so).
+ *
+ * Drop-in boundary for the reference's cgo seam in crypto/secp256k1 (secp256.go:20-37,
+ * ext.h:18-142): plain pointers and sizes, no torch / HIP types in any signature. A Go
+ * binding is a one-line cgo call per entry.
+ *
+ * Conventions (mirroring the reference seam):
+ *   - Single-item entries return exactly what the replaced C function returns (1 / 0).
+ *   - Batch entries return an eges_rc call code (0 = success) and write one eges_status
+ *     byte per item; item statuses are a 1:1 image of the Go errors the reference path
+ *     returns for that item.
+ *   - The caller owns every buffer; nothing is retained after return. Host-pointer entries
+ *     are synchronous. *_dev entries take device pointers and a hipStream_t (as void*) and
+ *     are asynchronous on that stream.
+ *   - n == 0 is valid and a no-op. A NULL pointer where n > 0 needs it returns
+ *     EGES_E_NULLPTR (never crashes).
+ *   - Thread-safe: concurrent callers are serialised per device.
+ *   - There is no CPU fallback: without a usable gfx950 device every compute entry fails
+ *     with EGES_E_NODEVICE.
+ */
+#ifndef EGES_H
+#define EGES_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EGES_ABI_VERSION 1
+
+/* Per-item status: 1:1 image of the reference errors. */
+typedef enum eges_status {
+    EGES_OK = 0,
+    EGES_INVALID_CHAIN_ID = 1,    /* types.ErrInvalidChainId  core/types/transaction_signing.go:30 */
+    EGES_INVALID_SIG = 2,         /* types.ErrInvalidSig      core/types/transaction.go:36 (recoverPlain :223-229) */
+    EGES_INVALID_MSG_LEN = 3,     /* secp256k1.ErrInvalidMsgLen        crypto/secp256k1/secp256.go:55 */
+    EGES_INVALID_SIG_LEN = 4,     /* secp256k1.ErrInvalidSignatureLen  secp256.go:56 */
+    EGES_INVALID_RECOVERY_ID = 5, /* secp256k1.ErrInvalidRecoveryID    secp256.go:57 */
+    EGES_RECOVER_FAILED = 6       /* secp256k1.ErrRecoverFailed        secp256.go:61 */
+} eges_status;
+
+/* Call-level return codes. */
+typedef enum eges_rc {
+    EGES_SUCCESS = 0,
+    EGES_E_NULLPTR = -1,
+    EGES_E_NODEVICE = -2,
+    EGES_E_HIP = -3,
+    EGES_E_INVALID_ARG = -4,
+    EGES_E_NOMEM = -5
+} eges_rc;
+
+/* Signer kinds for eges_sender_batch (core/types/transaction_signing.go). */
+typedef enum eges_signer {
+    EGES_SIGNER_FRONTIER = 0,  /* FrontierSigner  :218-220 (homestead = false) */
+    EGES_SIGNER_HOMESTEAD = 1, /* HomesteadSigner :182-184 (low-s enforced)     */
+    EGES_SIGNER_EIP155 = 2     /* EIP155Signer    :127-137                      */
+} eges_signer;
+
+/* Per-item flags for eges_sender_batch: the big.Int did not fit in 256 bits. */
+#define EGES_VF_V_WIDE 0x1u
+#define EGES_VF_R_WIDE 0x2u
+#define EGES_VF_S_WIDE 0x4u
+
+/* ---------------------------------------------------------------- lifecycle */
+
+/* Replaces the package init() that builds the context (secp256.go:45-52, ext.h:18-20):
+ * selects devices (bit i of device_mask = HIP device i; 0 = all visible), uploads the
+ * fixed-base tables and allocates staging. Idempotent. flags: reserved, pass 0. */
+int eges_init(uint32_t device_mask, uint32_t flags);
+void eges_shutdown(void);
+/* Number of devices the engine is using (0 before eges_init / without a GPU). */
+int eges_device_count(void);
+/* Human-readable description of the last error on this thread. */
+const char *eges_last_error(void);
+int eges_abi_version(void);
+
+/* ---------------------------------------------------------------- single item */
+
+/* Replaces secp256k1_ext_ecdsa_recover (crypto/secp256k1/ext.h:30-47).
+ * sig65 = R || S || recid, msg32 = hash. Returns 1 and writes the 65-byte uncompressed
+ * public key on success, 0 on failure (including recid >= 4, which the reference's
+ * parse_compact ARG_CHECK would reject). */
+int eges_ecdsa_recover(unsigned char *pubkey_out65, const unsigned char *sigdata65,
+                       const unsigned char *msgdata32);
+
+/* Replaces secp256k1_ext_ecdsa_verify (crypto/secp256k1/ext.h:58-75).
+ * sig64 = R || S. Returns 1 if valid, 0 otherwise (low-s enforced). */
+int eges_ecdsa_verify(const unsigned char *sigdata64, const unsigned char *msgdata32,
+                      const unsigned char *pubkeydata, size_t pubkeylen);
+
+/* ---------------------------------------------------------------- batch, host buffers */
+
+/* crypto.Ecrecover over a batch (crypto/signature_cgo.go:31 -> secp256.go:105-122).
+ * msg: n*32, sig: n*65. Outputs (each may be NULL): pub_out n*65 (zeros on failure),
+ * addr_out n*20 = Keccak256(pub[1:])[12:] (crypto.go:194-197), status n bytes:
+ * EGES_OK / EGES_INVALID_RECOVERY_ID / EGES_RECOVER_FAILED. */
+int eges_ecrecover_batch(const uint8_t *msg, const uint8_t *sig, size_t n, uint8_t *pub_out,
+                         uint8_t *addr_out, uint8_t *status);
+
+/* types.Sender over a batch (transaction_signing.go:72-89,127-137,182-184,218-247).
+ * sighash n*32 = signer.Hash(tx) (the caller passes the Frontier hash for unprotected
+ * txs under an EIP155 signer, as HomesteadSigner.Sender would use). r, s, v: n*32 each,
+ * big-endian, left-padded; vflags n bytes of EGES_VF_*. chain_id: the EIP155 signer's
+ * chain id (ignored for the other signers). Outputs: addr_out n*20, status n. */
+int eges_sender_batch(const uint8_t *sighash, const uint8_t *r, const uint8_t *s, const uint8_t *v,
+                      const uint8_t *vflags, size_t n, int signer, uint64_t chain_id, uint8_t *addr_out,
+                      uint8_t *status);
+
+/* crypto.VerifySignature over a batch (signature_cgo.go:66 -> secp256.go:126-134).
+ * pub: n*65 (each key left-aligned, publen[i] bytes valid: 33 or 65; 0 => false),
+ * msg n*32, sig n*64. ok_out n bytes of 0/1. */
+int eges_verify_batch(const uint8_t *pub, const uint8_t *publen, const uint8_t *msg, const uint8_t *sig,
+                      size_t n, uint8_t *ok_out);
+
+/* ---------------------------------------------------------------- batch, device buffers */
+/* Same semantics; all pointers are device pointers on `device`, work is enqueued on
+ * `stream` (a hipStream_t, NULL = the engine's stream for that device) and the call
+ * returns without synchronising. */
+int eges_ecrecover_batch_dev(int device, const uint8_t *msg, const uint8_t *sig, size_t n, uint8_t *pub_out,
+                             uint8_t *addr_out, uint8_t *status, void *stream);
+int eges_sender_batch_dev(int device, const uint8_t *sighash, const uint8_t *r, const uint8_t *s,
+                          const uint8_t *v, const uint8_t *vflags, size_t n, int signer, uint64_t chain_id,
+                          uint8_t *addr_out, uint8_t *status, void *stream);
+int eges_verify_batch_dev(int device, const uint8_t *pub, const uint8_t *publen, const uint8_t *msg,
+                          const uint8_t *sig, size_t n, uint8_t *ok_out, void *stream);
+
+/* ---------------------------------------------------------------- utilities */
+
+/* Keccak-256 (crypto.Keccak256, crypto/crypto.go:43-49), host implementation. */
+void eges_keccak256(const uint8_t *data, size_t len, uint8_t *out32);
+
+/* Synthetic workload generator (not on the hot path): on `device`, signs n messages with
+ * deterministic keys. Item i (global index first_index + i):
+ *   key_i = Keccak256("eges-key" || le64(i)) mod n (0 -> 1), msg_i = Keccak256("eges-msg" || le64(i)),
+ *   nonce_i = Keccak256("eges-nonce" || le64(i)) mod n (0 -> 1), low-s normalised.
+ * Writes msg n*32, sig n*65 (R||S||recid) and the expected address n*20 (from key_i*G).
+ * Device pointers, asynchronous on stream. */
+int eges_synth_sign_dev(int device, uint64_t first_index, size_t n, uint8_t *msg, uint8_t *sig,
+                        uint8_t *addr_expected, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EGES_H */

@@ -1,0 +1,117 @@
+"""ctypes wrappers of the oracle libraries (TEST INFRASTRUCTURE ONLY, see oracle/__init__.py)."""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libeges_ref.so")
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def have_ref():
+    return os.path.exists(REF_SO)
+
+
+class Oracle:
+    """This repo's CPU restatement (oracle/oracle.c)."""
+
+    def __init__(self):
+        if not os.path.exists(ORACLE_SO):
+            raise FileNotFoundError(f"{ORACLE_SO} missing: run `make -C oracle`")
+        L = ctypes.CDLL(ORACLE_SO)
+        P, SZ, I, U64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+        L.oracle_keccak256.argtypes = [P, SZ, P]
+        L.oracle_sponge.argtypes = [P, SZ, P, SZ, I, ctypes.c_ubyte]
+        L.oracle_ext_ecdsa_recover.argtypes = [P, P, P]
+        L.oracle_recover_pubkey.argtypes = [P, P, P]
+        L.oracle_ext_ecdsa_verify.argtypes = [P, P, P, SZ]
+        L.oracle_verify_signature.argtypes = [P, SZ, P, SZ, P, SZ]
+        L.oracle_sender.argtypes = [P, I, U64, P, P, P, P, I]
+        L.oracle_pub_to_addr.argtypes = [P, P]
+        L.oracle_recover_batch.argtypes = [SZ, P, P, P, P, P]
+        self.L = L
+
+    def keccak256(self, data: bytes) -> bytes:
+        a = np.frombuffer(bytes(data) or b"\0", np.uint8)
+        out = np.zeros(32, np.uint8)
+        self.L.oracle_keccak256(_p(a), len(data), _p(out))
+        return out.tobytes()
+
+    def sponge(self, data: bytes, outlen: int, rate: int, ds: int) -> bytes:
+        a = np.frombuffer(bytes(data) or b"\0", np.uint8)
+        out = np.zeros(outlen, np.uint8)
+        self.L.oracle_sponge(_p(a), len(data), _p(out), outlen, rate, ds)
+        return out.tobytes()
+
+    def recover_pubkey(self, msg: bytes, sig: bytes):
+        """secp256k1.RecoverPubkey -> (status, pub65)."""
+        m = np.frombuffer(bytes(msg), np.uint8)
+        s = np.frombuffer(bytes(sig), np.uint8)
+        pub = np.zeros(65, np.uint8)
+        st = self.L.oracle_recover_pubkey(_p(pub), _p(s), _p(m))
+        return st, pub.tobytes()
+
+    def recover_batch(self, msg, sig):
+        msg = np.ascontiguousarray(msg, np.uint8)
+        sig = np.ascontiguousarray(sig, np.uint8)
+        n = msg.shape[0]
+        pub = np.zeros((n, 65), np.uint8)
+        addr = np.zeros((n, 20), np.uint8)
+        st = np.zeros(n, np.uint8)
+        self.L.oracle_recover_batch(n, _p(msg), _p(sig), _p(pub), _p(addr), _p(st))
+        return pub, addr, st
+
+    def verify(self, pub: bytes, msg: bytes, sig: bytes) -> int:
+        p = np.frombuffer(bytes(pub) or b"\0", np.uint8)
+        m = np.frombuffer(bytes(msg) or b"\0", np.uint8)
+        s = np.frombuffer(bytes(sig) or b"\0", np.uint8)
+        return self.L.oracle_verify_signature(_p(p), len(pub), _p(m), len(msg), _p(s), len(sig))
+
+    def sender(self, signer, chain_id, sighash, r32, s32, v32, vflags):
+        out = np.zeros(20, np.uint8)
+        args = [np.frombuffer(bytes(x), np.uint8) for x in (sighash, r32, s32, v32)]
+        st = self.L.oracle_sender(_p(out), int(signer), int(chain_id), *[_p(a) for a in args], int(vflags))
+        return st, out.tobytes()
+
+    def pub_to_addr(self, pub65: bytes) -> bytes:
+        p = np.frombuffer(bytes(pub65), np.uint8)
+        out = np.zeros(20, np.uint8)
+        self.L.oracle_pub_to_addr(_p(out), _p(p))
+        return out.tobytes()
+
+
+class RefLib:
+    """The reference libsecp256k1 compiled in place (oracle/_ref)."""
+
+    def __init__(self):
+        if not have_ref():
+            raise FileNotFoundError(f"{REF_SO} missing")
+        L = ctypes.CDLL(REF_SO)
+        P, SZ, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        L.eref_ecrecover.argtypes = [P, P, P]
+        L.eref_verify.argtypes = [P, P, P, SZ]
+        L.eref_sign.argtypes = [P, P, P]
+        L.eref_pubkey.argtypes = [P, P]
+        L.eref_ecrecover_batch_mt.argtypes = [SZ, P, P, P, P, I]
+        self.L = L
+
+    def ecrecover(self, msg: bytes, sig: bytes):
+        m = np.frombuffer(bytes(msg), np.uint8)
+        s = np.frombuffer(bytes(sig), np.uint8)
+        pub = np.zeros(65, np.uint8)
+        r = self.L.eref_ecrecover(_p(pub), _p(s), _p(m))
+        return r, pub.tobytes()
+
+    def ecrecover_batch_mt(self, msg, sig, nthreads):
+        msg = np.ascontiguousarray(msg, np.uint8)
+        sig = np.ascontiguousarray(sig, np.uint8)
+        n = msg.shape[0]
+        pub = np.zeros((n, 65), np.uint8)
+        ret = np.zeros(n, np.int8)
+        self.L.eref_ecrecover_batch_mt(n, _p(msg), _p(sig), _p(pub), _p(ret), int(nthreads))
+        return pub, ret

@@ -1,0 +1,70 @@
+"""CPU tests of the C-ABI library: it loads, exports every symbol include/eges.h declares, and
+fails loudly (no CPU fallback) when no GPU is present. No compute calls are made here."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "eges.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(eges_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_entries():
+    syms = declared_symbols()
+    for must in ("eges_init", "eges_ecdsa_recover", "eges_ecdsa_verify", "eges_ecrecover_batch",
+                 "eges_sender_batch", "eges_verify_batch", "eges_ecrecover_batch_dev"):
+        assert must in syms
+
+
+def test_library_exports_all_declared_symbols():
+    from eges_amd import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+    # the Python binding covers the same set
+    assert set(_lib.SIGNATURES) == set(declared_symbols())
+
+
+def test_host_keccak_matches_kat():
+    import eges_amd
+    assert eges_amd.keccak256(b"abc").hex() == "4e03657aea45a94fc7d47ba826c8d667c0d1e6e33a64a036ec44f58fa12d6c45"
+    assert eges_amd.keccak256(b"").hex() == "c5d2460186f7233c927e7db2dcc703c0e500b653ca82273b7bfad8045d85a470"
+    # multi-block (> 136 bytes) against the oracle restatement
+    from oracle import Oracle
+    o = Oracle()
+    for n in (135, 136, 137, 300, 1000):
+        data = bytes((i * 7 + 3) & 0xFF for i in range(n))
+        assert eges_amd.keccak256(data) == o.keccak256(data)
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import numpy as np
+
+    import eges_amd
+    from eges_amd._lib import EGES_E_NODEVICE, EgesError
+    with pytest.raises(EgesError) as ei:
+        eges_amd.ecrecover_batch(np.zeros((1, 32), np.uint8), np.zeros((1, 65), np.uint8))
+    assert ei.value.rc == EGES_E_NODEVICE
+    # single-item entry returns 0 (failure), exactly like the replaced C function would on error
+    from eges_amd._lib import lib
+    pub = (ctypes.c_ubyte * 65)()
+    sig = (ctypes.c_ubyte * 65)()
+    msg = (ctypes.c_ubyte * 32)()
+    assert lib.eges_ecdsa_recover(pub, sig, msg) == 0
+
+
+def test_null_and_empty_inputs():
+    from eges_amd._lib import EGES_E_NULLPTR, EGES_SUCCESS, lib
+    assert lib.eges_ecrecover_batch(None, None, 0, None, None, None) == EGES_SUCCESS  # n == 0 is a no-op
+    assert lib.eges_ecrecover_batch(None, None, 5, None, None, None) == EGES_E_NULLPTR
+    assert lib.eges_verify_batch(None, None, None, None, 3, None) == EGES_E_NULLPTR
+    assert lib.eges_abi_version() == 1
