@@ -65,7 +65,23 @@ class EgesError(RuntimeError):
         self.rc = rc
 
 
+def _bind_process_hip_runtime():
+    """Make libeges.so share the process's HIP runtime with PyTorch.
+
+    torch's wheel ships its own libamdhip64 (SONAME libamdhip64.so.7, loaded as "libamdhip64.so"
+    from torch/lib). If libeges.so were loaded first, its NEEDED libamdhip64.so.7 would pull the
+    /opt/rocm copy and torch would later load a second runtime that cannot open the GPU. Loading
+    torch first lets the dynamic loader satisfy libeges.so's NEEDED entry with torch's copy, so
+    device pointers and streams are shared between the two.
+    """
+    try:
+        import torch  # noqa: F401
+    except Exception:  # torch is optional for the host-buffer API
+        pass
+
+
 def _load():
+    _bind_process_hip_runtime()
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                           "(there is no CPU fallback)")
