@@ -469,7 +469,7 @@ int eges_ecrecover_batch_dev(int device, const uint8_t* msg, const uint8_t* sig,
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
-  return run_recover_dev(*d, msg, sig, n, pub_out, addr_out, status, stream ? (hipStream_t)stream : d->stream);
+  return run_recover_dev(*d, msg, sig, n, pub_out, addr_out, status, (hipStream_t)stream);
 }
 
 int eges_sender_batch_dev(int device, const uint8_t* sighash, const uint8_t* r, const uint8_t* s, const uint8_t* v,
@@ -485,7 +485,7 @@ int eges_sender_batch_dev(int device, const uint8_t* sighash, const uint8_t* r, 
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
   return run_sender_dev(*d, sighash, r, s, v, vflags, n, signer, chain_id, addr_out, status,
-                        stream ? (hipStream_t)stream : d->stream);
+                        (hipStream_t)stream);
 }
 
 int eges_verify_batch_dev(int device, const uint8_t* pub, const uint8_t* publen, const uint8_t* msg, const uint8_t* sig,
@@ -498,7 +498,7 @@ int eges_verify_batch_dev(int device, const uint8_t* pub, const uint8_t* publen,
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
-  return run_verify_dev(*d, pub, publen, msg, sig, n, ok_out, stream ? (hipStream_t)stream : d->stream);
+  return run_verify_dev(*d, pub, publen, msg, sig, n, ok_out, (hipStream_t)stream);
 }
 
 int eges_synth_sign_dev(int device, uint64_t first_index, size_t n, uint8_t* msg, uint8_t* sig, uint8_t* addr_expected,
@@ -511,7 +511,7 @@ int eges_synth_sign_dev(int device, uint64_t first_index, size_t n, uint8_t* msg
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
-  hipStream_t st = stream ? (hipStream_t)stream : d->stream;
+  hipStream_t st = (hipStream_t)stream;
   Serial ser(*d, st);
   for (size_t off = 0; off < n; off += CHUNK) {
     const uint32_t m = (uint32_t)std::min(CHUNK, n - off);

@@ -11,8 +11,8 @@
  *     byte per item; item statuses are a 1:1 image of the Go errors the reference path
  *     returns for that item.
  *   - The caller owns every buffer; nothing is retained after return. Host-pointer entries
- *     are synchronous. *_dev entries take device pointers and a hipStream_t (as void*) and
- *     are asynchronous on that stream.
+ *     are synchronous. *_dev entries take device pointers and a hipStream_t (as void*, NULL
+ *     meaning the HIP null stream) and are asynchronous on that stream.
  *   - n == 0 is valid and a no-op. A NULL pointer where n > 0 needs it returns
  *     EGES_E_NULLPTR (never crashes).
  *   - Thread-safe: concurrent callers are serialised per device.
@@ -117,8 +117,8 @@ int eges_verify_batch(const uint8_t *pub, const uint8_t *publen, const uint8_t *
 
 /* ---------------------------------------------------------------- batch, device buffers */
 /* Same semantics; all pointers are device pointers on `device`, work is enqueued on
- * `stream` (a hipStream_t, NULL = the engine's stream for that device) and the call
- * returns without synchronising. */
+ * `stream` (a hipStream_t; NULL = the HIP null stream, exactly as in HIP) and the call
+ * returns without synchronising. Engine work is serialised across streams on a device. */
 int eges_ecrecover_batch_dev(int device, const uint8_t *msg, const uint8_t *sig, size_t n, uint8_t *pub_out,
                              uint8_t *addr_out, uint8_t *status, void *stream);
 int eges_sender_batch_dev(int device, const uint8_t *sighash, const uint8_t *r, const uint8_t *s,

@@ -97,7 +97,7 @@ class RefLib:
         L.eref_verify.argtypes = [P, P, P, SZ]
         L.eref_sign.argtypes = [P, P, P]
         L.eref_pubkey.argtypes = [P, P]
-        L.eref_ecrecover_batch_mt.argtypes = [SZ, P, P, P, P, I]
+        L.eref_ecrecover_batch_mt.argtypes = [SZ, P, P, P, P, P, I]
         self.L = L
 
     def ecrecover(self, msg: bytes, sig: bytes):
@@ -112,6 +112,7 @@ class RefLib:
         sig = np.ascontiguousarray(sig, np.uint8)
         n = msg.shape[0]
         pub = np.zeros((n, 65), np.uint8)
+        addr = np.zeros((n, 20), np.uint8)
         ret = np.zeros(n, np.int8)
-        self.L.eref_ecrecover_batch_mt(n, _p(msg), _p(sig), _p(pub), _p(ret), int(nthreads))
-        return pub, ret
+        self.L.eref_ecrecover_batch_mt(n, _p(msg), _p(sig), _p(pub), _p(addr), _p(ret), int(nthreads))
+        return pub, addr, ret

@@ -96,25 +96,41 @@ int eref_reencode(unsigned char *out, size_t outlen, const unsigned char *pub, s
     return r;
 }
 
-/* ---- pthread batch harness: the CPU baseline (one worker per core) ---- */
+/* ---- pthread batch harness: the CPU baseline (one worker per core) ----
+ * Per item: crypto.Ecrecover (reference C, exactly as cgo compiles it) then the address
+ * Keccak256(pub[1:])[12:] (transaction_signing.go:245). The reference's Keccak is Go/asm and
+ * cannot be built here; the oracle's C restatement of it (oracle.c, linked into this .so by
+ * oracle/Makefile) stands in for it. */
+void oracle_keccak256(const unsigned char *in, size_t len, unsigned char out[32]);
+
 typedef struct {
     size_t lo, hi;
     const unsigned char *msg, *sig;
-    unsigned char *pub;
+    unsigned char *pub, *addr;
     signed char *ret;
 } eref_job;
 
 static void *eref_worker(void *p) {
     eref_job *j = (eref_job *)p;
-    for (size_t i = j->lo; i < j->hi; ++i)
+    unsigned char h[32];
+    for (size_t i = j->lo; i < j->hi; ++i) {
         j->ret[i] = (signed char)eref_ecrecover(j->pub + 65 * i, j->sig + 65 * i, j->msg + 32 * i);
+        if (j->addr) {
+            if (j->ret[i] == 1) {
+                oracle_keccak256(j->pub + 65 * i + 1, 64, h);
+                memcpy(j->addr + 20 * i, h + 12, 20);
+            } else {
+                memset(j->addr + 20 * i, 0, 20);
+            }
+        }
+    }
     return NULL;
 }
 
 /* Recover n signatures (msg n*32, sig n*65) with nthreads workers.
- * pub_out n*65, ret_out n (codes as eref_ecrecover). */
+ * pub_out n*65, addr_out n*20 (may be NULL), ret_out n (codes as eref_ecrecover). */
 void eref_ecrecover_batch_mt(size_t n, const unsigned char *msg, const unsigned char *sig, unsigned char *pub_out,
-                             signed char *ret_out, int nthreads) {
+                             unsigned char *addr_out, signed char *ret_out, int nthreads) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 1024) nthreads = 1024;
     ctx_get();
@@ -127,7 +143,7 @@ void eref_ecrecover_batch_mt(size_t n, const unsigned char *msg, const unsigned 
         if (lo > n) lo = n;
         if (hi > n) hi = n;
         jobs[t].lo = lo; jobs[t].hi = hi; jobs[t].msg = msg; jobs[t].sig = sig;
-        jobs[t].pub = pub_out; jobs[t].ret = ret_out;
+        jobs[t].pub = pub_out; jobs[t].addr = addr_out; jobs[t].ret = ret_out;
         pthread_create(&th[t], NULL, eref_worker, &jobs[t]);
     }
     for (t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
