@@ -44,16 +44,17 @@ __constant__ const uint32_t GEN_X[8] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0
                                         0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu};
 __constant__ const uint32_t GEN_Y[8] = {0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u,
                                         0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
+// p, little-endian 32-bit limbs (field_10x26_impl.h set_b32 rejects >= p)
+__constant__ const uint32_t FE_P[8] = {0xFFFFFC2Fu, 0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu,
+                                       0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
 // p - n  (recovery/main_impl.h:104, ecdsa_impl.h:45-47)
 __constant__ const uint32_t P_MINUS_N[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75FC4u, 0x45512319u,
                                             0x00000001u, 0u, 0u, 0u};
 
-DEV fe fe_const(const uint32_t* c) {
-  fe r;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[i] = c[i];
-  return r;
-}
+DEV fe fe_const(const uint32_t* c) { return fe_from_u256(c); }
+
+template <class T>
+constexpr int NL = sizeof(T) / sizeof(uint32_t);  // limbs of fe (10) / sc (8)
 DEV ge gen_point() {
   ge g;
   g.x = fe_const(GEN_X);
@@ -66,14 +67,14 @@ template <class T>
 DEV T shfl_up_t(const T& x, int d) {
   T r;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[i] = (uint32_t)__shfl_up((int)x.v[i], d, 64);
+  for (int i = 0; i < NL<T>; ++i) r.v[i] = (uint32_t)__shfl_up((int)x.v[i], d, 64);
   return r;
 }
 template <class T>
 DEV T shfl_down_t(const T& x, int d) {
   T r;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[i] = (uint32_t)__shfl_down((int)x.v[i], d, 64);
+  for (int i = 0; i < NL<T>; ++i) r.v[i] = (uint32_t)__shfl_down((int)x.v[i], d, 64);
   return r;
 }
 
@@ -94,7 +95,7 @@ struct ScalarOps {
 
 // Workgroup Montgomery batch inversion: returns a^-1 for valid lanes (garbage otherwise).
 // Invalid lanes contribute 1 to the products so they cannot poison the batch.
-// lds: at least 2 * NWAVES * 8 words. Every thread of the workgroup must call this.
+// lds: at least 2 * NWAVES * 10 words. Every thread of the workgroup must call this.
 template <class Ops>
 DEV typename Ops::T wg_batch_inv(const typename Ops::T& a, bool valid, uint32_t* lds) {
   using T = typename Ops::T;
@@ -118,7 +119,7 @@ DEV typename Ops::T wg_batch_inv(const typename Ops::T& a, bool valid, uint32_t*
   T sex = Ops::sel(lane == 63, Ops::one(), shfl_down_t(Q, 1));
   if (lane == 63) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) lds[wave * 8 + i] = P.v[i];
+    for (int i = 0; i < NL<T>; ++i) lds[wave * 10 + i] = P.v[i];
   }
   __syncthreads();
   if (wave == 0) {
@@ -126,7 +127,7 @@ DEV typename Ops::T wg_batch_inv(const typename Ops::T& a, bool valid, uint32_t*
 #pragma unroll
     for (int w = 0; w < NWAVES; ++w)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) t[w].v[i] = lds[w * 8 + i];
+      for (int i = 0; i < NL<T>; ++i) t[w].v[i] = lds[w * 10 + i];
     T tot = t[0];
 #pragma unroll
     for (int w = 1; w < NWAVES; ++w) tot = Ops::mul(tot, t[w]);
@@ -136,13 +137,13 @@ DEV typename Ops::T wg_batch_inv(const typename Ops::T& a, bool valid, uint32_t*
     for (int w = 0; w < NWAVES; ++w) inv = Ops::mul(inv, Ops::sel(w == me, Ops::one(), t[w]));
     if (lane < NWAVES) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) lds[NWAVES * 8 + lane * 8 + i] = inv.v[i];
+      for (int i = 0; i < NL<T>; ++i) lds[NWAVES * 10 + lane * 10 + i] = inv.v[i];
     }
   }
   __syncthreads();
   T winv;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) winv.v[i] = lds[NWAVES * 8 + wave * 8 + i];
+  for (int i = 0; i < NL<T>; ++i) winv.v[i] = lds[NWAVES * 10 + wave * 10 + i];
   __syncthreads();  // lds is reused by the next call
   return Ops::mul(Ops::mul(winv, pex), sex);
 }
@@ -171,22 +172,26 @@ DEV void recode(const glv_half& h, D* out /* [NW][WG] */) {
 }
 
 // ------------------------------------------------------------------ tables
-DEV void store_pt(uint32_t* dst, const ge& p) {
-  fe x = fe_normalize(p.x), y = fe_normalize(p.y);
+// Affine point record: x then y, 10 radix-2^26 limbs each (80 bytes, 16-byte aligned).
+constexpr int PT_WORDS = 20;
+
+DEV void store_pt(uint32_t* dst, const ge& p) {  // coordinates must have magnitude <= 1
   uint4* d = reinterpret_cast<uint4*>(dst);
-  d[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
-  d[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
-  d[2] = make_uint4(y.v[0], y.v[1], y.v[2], y.v[3]);
-  d[3] = make_uint4(y.v[4], y.v[5], y.v[6], y.v[7]);
+  d[0] = make_uint4(p.x.v[0], p.x.v[1], p.x.v[2], p.x.v[3]);
+  d[1] = make_uint4(p.x.v[4], p.x.v[5], p.x.v[6], p.x.v[7]);
+  d[2] = make_uint4(p.x.v[8], p.x.v[9], p.y.v[0], p.y.v[1]);
+  d[3] = make_uint4(p.y.v[2], p.y.v[3], p.y.v[4], p.y.v[5]);
+  d[4] = make_uint4(p.y.v[6], p.y.v[7], p.y.v[8], p.y.v[9]);
 }
 DEV ge load_pt(const uint32_t* src) {
   const uint4* s = reinterpret_cast<const uint4*>(src);
-  uint4 a = s[0], b = s[1], c = s[2], d = s[3];
+  const uint4 a = s[0], b = s[1], c = s[2], d = s[3], e = s[4];
   ge p;
   p.x.v[0] = a.x; p.x.v[1] = a.y; p.x.v[2] = a.z; p.x.v[3] = a.w;
   p.x.v[4] = b.x; p.x.v[5] = b.y; p.x.v[6] = b.z; p.x.v[7] = b.w;
-  p.y.v[0] = c.x; p.y.v[1] = c.y; p.y.v[2] = c.z; p.y.v[3] = c.w;
-  p.y.v[4] = d.x; p.y.v[5] = d.y; p.y.v[6] = d.z; p.y.v[7] = d.w;
+  p.x.v[8] = c.x; p.x.v[9] = c.y; p.y.v[0] = c.z; p.y.v[1] = c.w;
+  p.y.v[2] = d.x; p.y.v[3] = d.y; p.y.v[4] = d.z; p.y.v[5] = d.w;
+  p.y.v[6] = e.x; p.y.v[7] = e.y; p.y.v[8] = e.z; p.y.v[9] = e.w;
   return p;
 }
 
@@ -208,30 +213,29 @@ DEV void add_step(gej& acc, bool& inf, const ge& p, bool use) {
   inf = use ? (inf ? false : to_inf) : inf;
 }
 
-DEV ge neg_if(const ge& p, bool neg) {
+DEV ge neg_if(const ge& p, bool neg) {  // y magnitude <= 2 afterwards
   ge r;
   r.x = p.x;
-  r.y = fe_select(neg, fe_neg(p.y), p.y);
+  r.y = fe_select(neg, fe_neg<1>(p.y), p.y);
   return r;
 }
 
 struct CoreLds {
   int8_t rdig[2][RWIN][WG];    // R / lambda R digits
   int16_t gdig[2][GWIN][WG];   // G / lambda G digits
-  uint32_t inv_scratch[2 * NWAVES * 8];
+  uint32_t inv_scratch[2 * NWAVES * 10];
 };
 
 // Per-block workspace (global memory, this block's lanes only):
 //   [0, PTAB*WG*16)            affine table {1..8}*P, entry-major then lane, 16 words/entry
 //   [PTAB*WG*16, +(PTAB-1)*WG*16)  Z_i and prefix products while the table is built
-constexpr size_t WS_WORDS = (size_t)(2 * PTAB - 1) * WG * 16;
+constexpr size_t WS_WORDS = (size_t)(2 * PTAB - 1) * WG * PT_WORDS;
 
 DEV void store_fe2(uint32_t* dst, const fe& a, const fe& b) {
-  uint4* d = reinterpret_cast<uint4*>(dst);
-  d[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
-  d[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
-  d[2] = make_uint4(b.v[0], b.v[1], b.v[2], b.v[3]);
-  d[3] = make_uint4(b.v[4], b.v[5], b.v[6], b.v[7]);
+  ge p;
+  p.x = a;
+  p.y = b;
+  store_pt(dst, p);
 }
 
 // Q = u_r * P + u_g * G for the workgroup's 256 lanes. P given affine (a valid curve point,
@@ -240,7 +244,7 @@ DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& 
                      uint32_t* ws, CoreLds& L) {
   const int tid = threadIdx.x;
   uint32_t* const base = ws + (size_t)blockIdx.x * WS_WORDS;
-  uint32_t* const zp = base + (size_t)PTAB * WG * 16;
+  uint32_t* const zp = base + (size_t)PTAB * WG * PT_WORDS;
   // --- digits
   {
     glv_half h1, h2;
@@ -254,39 +258,39 @@ DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& 
   // --- per-lane table {1..8} * P: Jacobian T_{i+1} = T_i + P streamed to the workspace,
   //     then one workgroup batch inversion of prod Z_i and a backward Montgomery pass.
   {
-    store_pt(base + (size_t)tid * 16, P);
+    store_pt(base + (size_t)tid * PT_WORDS, P);
     gej T;
     T.x = P.x;
     T.y = P.y;
     T.z = fe_one();
     T = gej_double(T);
     fe pre = T.z;
-    store_fe2(base + (size_t)(1 * WG + tid) * 16, T.x, T.y);
-    store_fe2(zp + (size_t)(0 * WG + tid) * 16, T.z, pre);
+    store_fe2(base + (size_t)(1 * WG + tid) * PT_WORDS, T.x, T.y);
+    store_fe2(zp + (size_t)(0 * WG + tid) * PT_WORDS, T.z, pre);
 #pragma unroll 1
     for (int i = 2; i < PTAB; ++i) {
       bool hz, rz;
       T = gej_add_ge(T, P, hz, rz);  // i*P + P, never exceptional for i < 8 < n
       pre = fe_mul(pre, T.z);
-      store_fe2(base + (size_t)(i * WG + tid) * 16, T.x, T.y);
-      store_fe2(zp + (size_t)((i - 1) * WG + tid) * 16, T.z, pre);
+      store_fe2(base + (size_t)(i * WG + tid) * PT_WORDS, T.x, T.y);
+      store_fe2(zp + (size_t)((i - 1) * WG + tid) * PT_WORDS, T.z, pre);
     }
     fe inv = wg_batch_inv<FieldOps>(pre, true, L.inv_scratch);  // 1 / (Z_1 ... Z_7)
 #pragma unroll 1
     for (int i = PTAB - 1; i >= 1; --i) {
-      const ge zz = load_pt(zp + (size_t)((i - 1) * WG + tid) * 16);  // .x = Z_i
+      const ge zz = load_pt(zp + (size_t)((i - 1) * WG + tid) * PT_WORDS);  // .x = Z_i
       fe zi = inv;
       if (i > 1) {
-        const ge pp = load_pt(zp + (size_t)((i - 2) * WG + tid) * 16);  // .y = pre_{i-1}
+        const ge pp = load_pt(zp + (size_t)((i - 2) * WG + tid) * PT_WORDS);  // .y = pre_{i-1}
         zi = fe_mul(inv, pp.y);
         inv = fe_mul(inv, zz.x);
       }
-      const ge J = load_pt(base + (size_t)(i * WG + tid) * 16);
+      const ge J = load_pt(base + (size_t)(i * WG + tid) * PT_WORDS);
       const fe zi2 = fe_sqr(zi);
       ge a;
       a.x = fe_mul(J.x, zi2);
       a.y = fe_mul(J.y, fe_mul(zi2, zi));
-      store_pt(base + (size_t)(i * WG + tid) * 16, a);
+      store_pt(base + (size_t)(i * WG + tid) * PT_WORDS, a);
     }
   }
   // --- Strauss-Shamir: 33 windows of 4 bits (R, lambda R) interleaved with 11 windows of
@@ -310,8 +314,8 @@ DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& 
       const int a = d < 0 ? -d : d;
       const int e = a > 0 ? a - 1 : 0;
       ge p;
-      if (j < 2) p = load_pt(base + (size_t)(e * WG + tid) * 16);
-      else p = load_pt(gtab + ((size_t)(j - 2) * GTAB + e) * 16);
+      if (j < 2) p = load_pt(base + (size_t)(e * WG + tid) * PT_WORDS);
+      else p = load_pt(gtab + ((size_t)(j - 2) * GTAB + e) * PT_WORDS);
       if (j == 1) p.x = fe_mul(p.x, fe_const(FE_BETA));
       add_step(acc, inf, neg_if(p, d < 0), d != 0);
     }
@@ -327,22 +331,22 @@ DEV void limbs_from_be32(uint32_t out[8], const uint8_t* b) {
     out[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
   }
 }
-DEV void write_be32(uint8_t* dst, const fe& x) {
+DEV void write_be32(uint8_t* dst, const uint32_t x[8]) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    uint32_t w = x.v[7 - i];
+    uint32_t w = x[7 - i];
     dst[4 * i + 0] = (uint8_t)(w >> 24);
     dst[4 * i + 1] = (uint8_t)(w >> 16);
     dst[4 * i + 2] = (uint8_t)(w >> 8);
     dst[4 * i + 3] = (uint8_t)w;
   }
 }
-DEV uint64_t be_word(const fe& x, int k) {  // little-endian 64-bit word k of the BE encoding
-  return (uint64_t)__builtin_bswap32(x.v[7 - 2 * k]) | ((uint64_t)__builtin_bswap32(x.v[6 - 2 * k]) << 32);
+DEV uint64_t be_word(const uint32_t x[8], int k) {  // little-endian 64-bit word k of the BE encoding
+  return (uint64_t)__builtin_bswap32(x[7 - 2 * k]) | ((uint64_t)__builtin_bswap32(x[6 - 2 * k]) << 32);
 }
 
-// Keccak-256(X || Y)[12:32] as 5 little-endian words.
-DEV void pub_address(uint32_t a[5], const fe& X, const fe& Y) {
+// Keccak-256(X || Y)[12:32] as 5 little-endian words; X, Y canonical 256-bit integers.
+DEV void pub_address(uint32_t a[5], const uint32_t X[8], const uint32_t Y[8]) {
   uint64_t w[17];
 #pragma unroll
   for (int k = 0; k < 17; ++k) w[k] = 0;

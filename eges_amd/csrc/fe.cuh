@@ -1,14 +1,17 @@
-// Field arithmetic mod p = 2^256 - 2^32 - 977 for gfx950.
+// Field arithmetic mod p = 2^256 - 2^32 - 977 for gfx950, radix 2^26 (10 limbs).
 //
 // Same values as libsecp256k1's field (crypto/secp256k1/libsecp256k1/src/field_10x26_impl.h,
-// field_impl.h), different representation: 8 x 32-bit little-endian limbs so that one
-// v_mad_u64_u32 (measured 4.4 cyc/wave-inst, the same issue class as a 32-bit add with
-// carry on gfx950; see tools/ubench_valu.hip) produces a full 32x32->64 partial product
-// plus a 64-bit addend.
+// field_impl.h). The radix is chosen for the MI355X VALU, not copied: every 26x26-bit partial
+// product (up to 28x28 with lazy additions) accumulates IN PLACE into a 64-bit column with one
+// v_mad_u64_u32 (4.4 cyc / wave64 instruction, tools/ubench_valu.hip) — no carry flags, no
+// zero-extension moves — and additions / subtractions are plain 32-bit v_add_u32 (2.5 cyc) on
+// limbs with headroom. A full 32-bit-limb multiply instead needs a carry op per product.
 //
-// Invariant ("weak" form): every fe holds a value < 2^256 that is congruent to the field
-// element; it may be >= p. fe_normalize() maps it to [0, p). Equality / zero tests and
-// serialisation normalise first.
+// Representation: value = sum_k v[k] * 2^(26 k), k = 0..9 (up to 2^260). "Magnitude m": every
+// limb <= m * 2^26 (+ a 2^19 slack on the outputs of mul/sqr/normalize_weak, which are
+// magnitude 1). Inputs of fe_mul / fe_sqr must have magnitude <= 4; fe_sub<M>(a, b) needs
+// magnitude(b) < 2M and returns magnitude(a) + 2M. Values are weak (congruent mod p, possibly
+// >= p) until fe_normalize().
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -18,126 +21,119 @@
 namespace eges {
 
 struct fe {
-  uint32_t v[8];
+  uint32_t v[10];
 };
 
-// 2^256 mod p = 2^32 + 977
-constexpr uint32_t FE_C0 = 977u;
+constexpr uint32_t M26 = 0x3FFFFFFu;
+// 2^260 mod p = 2^36 + 15632  -> fold v * 2^260 as v * 15632 (same limb) + v * 2^10 (next limb)
+constexpr uint32_t FOLD0 = 15632u;
+constexpr uint32_t FOLD1 = 1024u;
+// 2^256 mod p = 2^32 + 977 = 977 + 2^6 * 2^26
+constexpr uint32_t C256_0 = 977u;
+constexpr uint32_t C256_1 = 64u;
 
-DEV fe fe_zero() { fe r; for (int i = 0; i < 8; ++i) r.v[i] = 0; return r; }
-DEV fe fe_one() { fe r = fe_zero(); r.v[0] = 1; return r; }
-DEV fe fe_from_u32(uint32_t x) { fe r = fe_zero(); r.v[0] = x; return r; }
+DEV uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
 
-// Fold a carry word k (value k * 2^256) back in: r += k * (2^32 + 977). k is small
-// (< 2^34 here), so the fold can overflow 2^256 at most once more, by a tiny amount,
-// which a second single-word fold absorbs without further carries.
-DEV void fe_fold(fe& r, uint64_t k) {
-  uint64_t c = (uint64_t)r.v[0] + (k & 0xffffffffull) * FE_C0;
-  r.v[0] = (uint32_t)c;
-  c = (c >> 32) + (uint64_t)r.v[1] + (k >> 32) * FE_C0 + (k & 0xffffffffull);
-  r.v[1] = (uint32_t)c;
-  c = (c >> 32) + (uint64_t)r.v[2] + (k >> 32);
-  r.v[2] = (uint32_t)c;
-  c >>= 32;
-#pragma unroll
-  for (int i = 3; i < 8; ++i) {
-    c += r.v[i];
-    r.v[i] = (uint32_t)c;
-    c >>= 32;
-  }
-  // c is 0 or 1 here; if 1 the value wrapped to something < 2^35 and adding 2^32+977 cannot
-  // carry beyond limb 1.
-  uint64_t d = (uint64_t)r.v[0] + (uint32_t)c * FE_C0;
-  r.v[0] = (uint32_t)d;
-  d = (d >> 32) + (uint64_t)r.v[1] + (uint32_t)c;
-  r.v[1] = (uint32_t)d;
-  r.v[2] += (uint32_t)(d >> 32);
-}
-
-// r = lo + hi * 2^256 reduced to weak form. t[0..15] little-endian.
-DEV fe fe_reduce512(const uint32_t t[16]) {
+DEV fe fe_zero() {
   fe r;
-  // r = lo + hi * 977 + (hi << 32)
-  uint64_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    c += (uint64_t)t[8 + i] * FE_C0 + t[i];
-    if (i > 0) c += t[8 + i - 1];
-    r.v[i] = (uint32_t)c;
-    c >>= 32;
-  }
-  c += t[15];  // top of (hi << 32)
-  fe_fold(r, c);
+  for (int i = 0; i < 10; ++i) r.v[i] = 0;
+  return r;
+}
+DEV fe fe_one() { fe r = fe_zero(); r.v[0] = 1; return r; }
+DEV fe fe_from_u32(uint32_t x) {  // x < 2^26 suffices for the constants used here
+  fe r = fe_zero();
+  r.v[0] = x & M26;
+  r.v[1] = x >> 26;
   return r;
 }
 
-// 256x256 -> 512 schoolbook, row (operand) scanning: each partial product is one
-// v_mad_u64_u32 whose 64-bit addend carries the running limb; the row carry is added
-// as a 32-bit value.
-DEV void mul_256x256(uint32_t t[16], const uint32_t a[8], const uint32_t b[8]) {
-  uint64_t c = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    c = (uint64_t)a[0] * b[j] + (c >> 32);
-    t[j] = (uint32_t)c;
-  }
-  t[8] = (uint32_t)(c >> 32);
-#pragma unroll
-  for (int i = 1; i < 8; ++i) {
-    c = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      c = (uint64_t)a[i] * b[j] + (uint64_t)t[i + j] + (c >> 32);
-      t[i + j] = (uint32_t)c;
-    }
-    t[i + 8] = (uint32_t)(c >> 32);
-  }
+// 256-bit little-endian 32-bit limbs -> radix 2^26 (value unchanged, magnitude 1)
+DEV fe fe_from_u256(const uint32_t x[8]) {
+  fe r;
+  r.v[0] = x[0] & M26;
+  r.v[1] = ((x[0] >> 26) | (x[1] << 6)) & M26;
+  r.v[2] = ((x[1] >> 20) | (x[2] << 12)) & M26;
+  r.v[3] = ((x[2] >> 14) | (x[3] << 18)) & M26;
+  r.v[4] = ((x[3] >> 8) | (x[4] << 24)) & M26;
+  r.v[5] = (x[4] >> 2) & M26;
+  r.v[6] = ((x[4] >> 28) | (x[5] << 4)) & M26;
+  r.v[7] = ((x[5] >> 22) | (x[6] << 10)) & M26;
+  r.v[8] = ((x[6] >> 16) | (x[7] << 16)) & M26;
+  r.v[9] = x[7] >> 10;
+  return r;
 }
 
-// Squaring: off-diagonal products once, doubled, plus the diagonal.
-DEV void sqr_256(uint32_t t[16], const uint32_t a[8]) {
+// Canonical (fully normalised) radix-2^26 -> 256-bit 32-bit limbs.
+DEV void fe_to_u256(uint32_t x[8], const fe& a) {
+  x[0] = a.v[0] | (a.v[1] << 26);
+  x[1] = (a.v[1] >> 6) | (a.v[2] << 20);
+  x[2] = (a.v[2] >> 12) | (a.v[3] << 14);
+  x[3] = (a.v[3] >> 18) | (a.v[4] << 8);
+  x[4] = (a.v[4] >> 24) | (a.v[5] << 2) | (a.v[6] << 28);
+  x[5] = (a.v[6] >> 4) | (a.v[7] << 22);
+  x[6] = (a.v[7] >> 10) | (a.v[8] << 16);
+  x[7] = (a.v[8] >> 16) | (a.v[9] << 10);
+}
+
+// ------------------------------------------------------------------ reduction of 19 columns
+// S[0..18]: column sums (each < 2^59.4). Returns magnitude-1 limbs.
+DEV fe fe_reduce_cols(uint64_t S[19]) {
+  // fold columns 18..10 (descending: column 18 spills into column 10, folded afterwards).
+  // S_k 2^(26k) = (hi 2^32 + lo) 2^(26(k-10)) (2^36 + 15632)
 #pragma unroll
-  for (int i = 0; i < 16; ++i) t[i] = 0;
-#pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    uint64_t c = 0;
-#pragma unroll
-    for (int j = i + 1; j < 8; ++j) {
-      c = (uint64_t)a[i] * a[j] + (uint64_t)t[i + j] + (c >> 32);
-      t[i + j] = (uint32_t)c;
-    }
-    t[i + 8] = (uint32_t)(c >> 32);
+  for (int k = 18; k >= 10; --k) {
+    const uint32_t lo = (uint32_t)S[k];
+    const uint32_t hi = (uint32_t)(S[k] >> 32);
+    S[k - 10] = mad64(lo, FOLD0, S[k - 10]);
+    S[k - 9] = mad64(lo, FOLD1, S[k - 9]);
+    S[k - 9] = mad64(hi, FOLD0 << 6, S[k - 9]);
+    S[k - 8] = mad64(hi, 1u << 16, S[k - 8]);
   }
-  // double
-  uint32_t top = t[15] >> 31;
+  fe r;
 #pragma unroll
-  for (int i = 15; i > 0; --i) t[i] = (t[i] << 1) | (t[i - 1] >> 31);
-  t[0] <<= 1;
-  (void)top;  // off-diagonal sum < 2^511, doubling cannot overflow 512 bits
-  // add diagonal
-  uint64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    uint64_t sq = (uint64_t)a[i] * a[i];
-    c += (uint64_t)t[2 * i] + (uint32_t)sq;
-    t[2 * i] = (uint32_t)c;
-    c >>= 32;
-    c += (uint64_t)t[2 * i + 1] + (uint32_t)(sq >> 32);
-    t[2 * i + 1] = (uint32_t)c;
-    c >>= 32;
+  for (int k = 0; k < 9; ++k) {
+    r.v[k] = (uint32_t)S[k] & M26;
+    S[k + 1] += S[k] >> 26;
   }
+  r.v[9] = (uint32_t)S[9] & M26;
+  const uint64_t c = S[9] >> 26;  // < 2^33.5: multiple of 2^260
+  const uint32_t cl = (uint32_t)c, ch = (uint32_t)(c >> 32);
+  uint64_t t0 = mad64(cl, FOLD0, r.v[0]);
+  uint64_t t1 = mad64(cl, FOLD1, r.v[1]);
+  t1 = mad64(ch, FOLD0 << 6, t1);
+  r.v[0] = (uint32_t)t0 & M26;
+  t1 += t0 >> 26;
+  r.v[1] = (uint32_t)t1 & M26;
+  r.v[2] += (uint32_t)(t1 >> 26) + (ch << 16);
+  return r;
 }
 
 DEV fe fe_mul(const fe& a, const fe& b) {
-  uint32_t t[16];
-  mul_256x256(t, a.v, b.v);
-  return fe_reduce512(t);
+  uint64_t S[19];
+#pragma unroll
+  for (int k = 0; k < 19; ++k) S[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i)
+#pragma unroll
+    for (int j = 0; j < 10; ++j) S[i + j] = mad64(a.v[i], b.v[j], S[i + j]);
+  return fe_reduce_cols(S);
 }
 
 DEV fe fe_sqr(const fe& a) {
-  uint32_t t[16];
-  sqr_256(t, a.v);
-  return fe_reduce512(t);
+  uint32_t d[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) d[i] = a.v[i] << 1;  // < 2^29.1 for magnitude <= 4
+  uint64_t S[19];
+#pragma unroll
+  for (int k = 0; k < 19; ++k) S[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    S[2 * i] = mad64(a.v[i], a.v[i], S[2 * i]);
+#pragma unroll
+    for (int j = i + 1; j < 10; ++j) S[i + j] = mad64(a.v[i], d[j], S[i + j]);
+  }
+  return fe_reduce_cols(S);
 }
 
 DEV fe fe_sqr_n(fe a, int n) {
@@ -146,141 +142,138 @@ DEV fe fe_sqr_n(fe a, int n) {
   return a;
 }
 
+// ------------------------------------------------------------------ linear ops (no carries)
 DEV fe fe_add(const fe& a, const fe& b) {
   fe r;
-  uint64_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    c += (uint64_t)a.v[i] + b.v[i];
-    r.v[i] = (uint32_t)c;
-    c >>= 32;
-  }
-  // value = r + c*2^256 ; fold c (0/1)
-  uint64_t d = (uint64_t)r.v[0] + (uint32_t)c * FE_C0;
-  r.v[0] = (uint32_t)d;
-  d = (d >> 32) + (uint64_t)r.v[1] + (uint32_t)c;
-  r.v[1] = (uint32_t)d;
-  d >>= 32;
-#pragma unroll
-  for (int i = 2; i < 8; ++i) {
-    d += r.v[i];
-    r.v[i] = (uint32_t)d;
-    d >>= 32;
-  }
-  // second wrap only if r was >= 2^256 - 2^32 - 977; then the result is < 2^33 and
-  // the fold below cannot carry past limb 1.
-  uint64_t e = (uint64_t)r.v[0] + (uint32_t)d * FE_C0;
-  r.v[0] = (uint32_t)e;
-  e = (e >> 32) + (uint64_t)r.v[1] + (uint32_t)d;
-  r.v[1] = (uint32_t)e;
-  r.v[2] += (uint32_t)(e >> 32);
+  for (int i = 0; i < 10; ++i) r.v[i] = a.v[i] + b.v[i];
   return r;
 }
 
-// a - b (mod p): on borrow, subtract 2^32+977 (== add p, mod 2^256); a second borrow
-// means the intermediate wrapped below zero again, subtract once more.
+// Limbs of K1 = a multiple of p whose every limb is ~2 * 2^26.
+__constant__ const uint32_t FE_K1[10] = {0x7ff85e0u, 0x7fff7feu, 0x7fffffeu, 0x7fffffeu, 0x7fffffeu,
+                                         0x7fffffeu, 0x7fffffeu, 0x7fffffeu, 0x7fffffeu, 0x7fffffeu};
+
+// a - b for magnitude(b) < 2M; result magnitude(a) + 2M.
+template <int M>
 DEV fe fe_sub(const fe& a, const fe& b) {
+  constexpr uint32_t k0 = 0x7ff85e0u * M, k1 = 0x7fff7feu * M, kk = 0x7fffffeu * M;
   fe r;
-  uint64_t br = 0;
+  r.v[0] = a.v[0] + k0 - b.v[0];
+  r.v[1] = a.v[1] + k1 - b.v[1];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    uint64_t d = (uint64_t)a.v[i] - b.v[i] - br;
-    r.v[i] = (uint32_t)d;
-    br = (d >> 63) & 1;
-  }
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    uint32_t m = (uint32_t)br;  // 1 if we must subtract 2^32 + 977
-    uint64_t d = (uint64_t)r.v[0] - (uint64_t)(m * FE_C0);
-    r.v[0] = (uint32_t)d;
-    uint64_t b2 = (d >> 63) & 1;
-    d = (uint64_t)r.v[1] - m - b2;
-    r.v[1] = (uint32_t)d;
-    b2 = (d >> 63) & 1;
-#pragma unroll
-    for (int i = 2; i < 8; ++i) {
-      d = (uint64_t)r.v[i] - b2;
-      r.v[i] = (uint32_t)d;
-      b2 = (d >> 63) & 1;
-    }
-    br = b2 & m;
-  }
+  for (int i = 2; i < 10; ++i) r.v[i] = a.v[i] + kk - b.v[i];
   return r;
 }
 
-DEV fe fe_neg(const fe& a) { return fe_sub(fe_zero(), a); }
+template <int M>
+DEV fe fe_neg(const fe& a) {
+  return fe_sub<M>(fe_zero(), a);
+}
 
-// r = a * k for a small constant k (< 2^30)
+// limbwise small multiple (magnitude * k)
 DEV fe fe_mul_small(const fe& a, uint32_t k) {
   fe r;
-  uint64_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    c = (uint64_t)a.v[i] * k + (c >> 32);
-    r.v[i] = (uint32_t)c;
-  }
-  fe_fold(r, c >> 32);
+  for (int i = 0; i < 10; ++i) r.v[i] = a.v[i] * k;
   return r;
 }
 
-// Canonical representative in [0, p).
-DEV fe fe_normalize(const fe& a) {
-  // a >= p  <=>  a + (2^32 + 977) >= 2^256
-  fe t;
-  uint64_t c = (uint64_t)a.v[0] + FE_C0;
-  t.v[0] = (uint32_t)c;
-  c = (c >> 32) + (uint64_t)a.v[1] + 1u;
-  t.v[1] = (uint32_t)c;
-  c >>= 32;
-#pragma unroll
-  for (int i = 2; i < 8; ++i) {
-    c += a.v[i];
-    t.v[i] = (uint32_t)c;
-    c >>= 32;
-  }
+// Carry pass: any magnitude (limbs < 2^32) -> magnitude 1 (same value mod p).
+DEV fe fe_normalize_weak(const fe& a) {
   fe r;
-  bool ge = c != 0;
+  uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[i] = ge ? t.v[i] : a.v[i];
+  for (int i = 0; i < 9; ++i) {
+    const uint32_t t = a.v[i] + c;
+    r.v[i] = t & M26;
+    c = t >> 26;
+  }
+  const uint32_t t9 = a.v[9] + c;
+  r.v[9] = t9 & M26;
+  const uint32_t h = t9 >> 26;  // multiple of 2^260, < 2^7
+  const uint32_t u0 = r.v[0] + h * FOLD0;
+  r.v[0] = u0 & M26;
+  r.v[1] += (u0 >> 26) + h * FOLD1;
   return r;
+}
+
+// Canonical representative in [0, p), any magnitude.
+DEV fe fe_normalize(const fe& a) {
+  fe r = fe_normalize_weak(a);  // < 2^260 + small
+  // fold bits >= 2^256 (limb 9 bits 22..25): h * (2^32 + 977)
+  uint32_t h = r.v[9] >> 22;
+  r.v[9] &= 0x3FFFFFu;
+  uint32_t c = h * C256_0;
+  {
+    uint32_t t = r.v[0] + c;
+    r.v[0] = t & M26;
+    t = r.v[1] + (t >> 26) + h * C256_1;
+    r.v[1] = t & M26;
+    c = t >> 26;
+#pragma unroll
+    for (int i = 2; i < 9; ++i) {
+      t = r.v[i] + c;
+      r.v[i] = t & M26;
+      c = t >> 26;
+    }
+    r.v[9] += c;  // value now < 2^256 + 2^32 (r.v[9] <= 2^22)
+  }
+  // one more fold if it reached 2^256, then the value is < 2^33: no further carries past limb 2
+  h = r.v[9] >> 22;
+  r.v[9] &= 0x3FFFFFu;
+  {
+    uint32_t t = r.v[0] + h * C256_0;
+    r.v[0] = t & M26;
+    t = r.v[1] + (t >> 26) + h * C256_1;
+    r.v[1] = t & M26;
+    r.v[2] += t >> 26;
+  }
+  // r < 2^256; subtract p if r >= p  <=>  r + 2^32 + 977 >= 2^256
+  uint32_t s[10];
+  {
+    uint32_t t = r.v[0] + C256_0;
+    s[0] = t & M26;
+    t = r.v[1] + (t >> 26) + C256_1;
+    s[1] = t & M26;
+    uint32_t cc = t >> 26;
+#pragma unroll
+    for (int i = 2; i < 10; ++i) {
+      t = r.v[i] + cc;
+      s[i] = t & M26;
+      cc = t >> 26;
+    }
+    // s[9] bit 22 set <=> r + 2^32 + 977 >= 2^256
+  }
+  const bool ge = (s[9] >> 22) != 0;
+  s[9] &= 0x3FFFFFu;
+  fe o;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) o.v[i] = ge ? s[i] : r.v[i];
+  return o;
 }
 
 DEV bool fe_is_zero(const fe& a) {
-  fe n = fe_normalize(a);
+  const fe n = fe_normalize(a);
   uint32_t o = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) o |= n.v[i];
+  for (int i = 0; i < 10; ++i) o |= n.v[i];
   return o == 0;
 }
 
-DEV bool fe_equal(const fe& a, const fe& b) { return fe_is_zero(fe_sub(a, b)); }
+DEV bool fe_equal(const fe& a, const fe& b) { return fe_is_zero(fe_sub<1>(a, b)); }
 
-DEV bool fe_is_odd(const fe& a) { return fe_normalize(a).v[0] & 1; }
+DEV bool fe_is_odd(const fe& a) { return fe_normalize(a).v[0] & 1u; }
 
 DEV fe fe_select(bool c, const fe& a, const fe& b) {
   fe r;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+  for (int i = 0; i < 10; ++i) r.v[i] = c ? a.v[i] : b.v[i];
   return r;
 }
 
-// Big-endian 32-byte load; returns false if the value is >= p (field_10x26_impl.h:323-345).
-DEV bool fe_set_b32_checked(fe& r, const uint8_t* b) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint8_t* q = b + 28 - 4 * i;
-    r.v[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
-  }
-  fe n = fe_normalize(r);
-  bool ok = true;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) ok = ok && (n.v[i] == r.v[i]);
-  return ok;
-}
-
 // ---- exponentiation chains ------------------------------------------------
-// a^(2^k - 1) ladder shared by sqrt and inverse:
-// x2, x3, x6, x9, x11, x22, x44, x88, x176, x220, x223
+// a^(2^k - 1) ladder shared by sqrt and inverse: x2, x3, x6, x9, x11, x22, x44, x88, x176, x220, x223
 struct fe_chain {
   fe x2, x3, x22, x223;
 };

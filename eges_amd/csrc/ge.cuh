@@ -5,6 +5,9 @@
 // Formulas: doubling dbl-2009-l (2M + 5S), mixed addition madd-2007-bl (7M + 4S). The
 // exceptional cases libsecp256k1 handles with branches (a == infinity, a == b, a == -b) are
 // reported through flags so the kernel can resolve them with wave-uniform control flow.
+//
+// Magnitudes (fe.cuh): every coordinate at rest has magnitude 1; comments give the magnitude
+// of each intermediate; fe_mul / fe_sqr inputs stay <= 4.
 #pragma once
 #include "fe.cuh"
 
@@ -19,46 +22,47 @@ struct ge {
 
 // Jacobian doubling. Input with Z == 0 yields Z == 0 (infinity stays infinity).
 DEV gej gej_double(const gej& a) {
-  fe A = fe_sqr(a.x);
-  fe B = fe_sqr(a.y);
-  fe C = fe_sqr(B);
-  fe t = fe_sqr(fe_add(a.x, B));
-  t = fe_sub(fe_sub(t, A), C);
-  fe D = fe_add(t, t);                     // 4 X Y^2
-  fe E = fe_add(fe_add(A, A), A);          // 3 X^2
-  fe F = fe_sqr(E);
+  const fe A = fe_sqr(a.x);                           // 1
+  const fe B = fe_sqr(a.y);                           // 1
+  const fe C = fe_sqr(B);                             // 1
+  const fe t = fe_sub<2>(fe_sqr(fe_add(a.x, B)), fe_add(A, C));  // (X+B)^2 - A - C: 1 + 4 = 5
+  const fe D = fe_normalize_weak(fe_add(t, t));       // 4 X Y^2, 1
+  const fe E = fe_add(fe_add(A, A), A);               // 3 X^2, 3
+  const fe F = fe_sqr(E);                             // 1
   gej r;
-  r.x = fe_sub(F, fe_add(D, D));           // E^2 - 2D
-  fe C8 = fe_mul_small(C, 8);
-  r.y = fe_sub(fe_mul(E, fe_sub(D, r.x)), C8);
-  fe yz = fe_mul(a.y, a.z);
-  r.z = fe_add(yz, yz);
+  r.x = fe_normalize_weak(fe_sub<2>(F, fe_add(D, D)));               // E^2 - 2D: 1 + 4 -> 1
+  const fe m = fe_mul(E, fe_sub<1>(D, r.x));                         // in 3, 3 -> 1
+  r.y = fe_normalize_weak(fe_sub<8>(m, fe_mul_small(C, 8)));         // 1 + 16 -> 1
+  const fe yz = fe_mul(a.y, a.z);                                    // 1
+  r.z = fe_normalize_weak(fe_add(yz, yz));                           // 2 Y Z, 1
   return r;
 }
 
-// Mixed addition a (Jacobian, not infinity) + b (affine). Sets h_zero when U2 == X1
-// (a == +-b); then r_zero tells doubling (a == b) from infinity (a == -b) and the returned
-// point is meaningless.
+// Mixed addition a (Jacobian, not infinity) + b (affine, x magnitude 1, y magnitude <= 2).
+// Sets h_zero when U2 == X1 (a == +-b); then r_zero tells doubling (a == b) from infinity
+// (a == -b) and the returned point is meaningless.
 DEV gej gej_add_ge(const gej& a, const ge& b, bool& h_zero, bool& r_zero) {
-  fe Z1Z1 = fe_sqr(a.z);
-  fe U2 = fe_mul(b.x, Z1Z1);
-  fe S2 = fe_mul(fe_mul(b.y, a.z), Z1Z1);
-  fe H = fe_sub(U2, a.x);
-  fe rr = fe_sub(S2, a.y);
+  const fe Z1Z1 = fe_sqr(a.z);                                       // 1
+  const fe U2 = fe_mul(b.x, Z1Z1);                                   // 1
+  const fe S2 = fe_mul(fe_mul(b.y, a.z), Z1Z1);                      // 1
+  const fe H = fe_sub<1>(U2, a.x);                                   // 3
+  const fe R = fe_normalize_weak(fe_sub<1>(S2, a.y));                // 1
   h_zero = fe_is_zero(H);
-  r_zero = fe_is_zero(rr);
-  fe HH = fe_sqr(H);
-  fe I = fe_add(HH, HH);
-  I = fe_add(I, I);                         // 4 HH
-  fe J = fe_mul(H, I);
-  rr = fe_add(rr, rr);                      // 2 (S2 - Y1)
-  fe V = fe_mul(a.x, I);
+  r_zero = fe_is_zero(R);
+  const fe HH = fe_sqr(H);                                           // 1
+  const fe HH2 = fe_add(HH, HH);
+  const fe I = fe_add(HH2, HH2);                                     // 4 HH, 4
+  const fe J = fe_mul(H, I);                                         // 1
+  const fe R2 = fe_add(R, R);                                        // 2 (S2 - Y1), 2
+  const fe V = fe_mul(a.x, I);                                       // 1
   gej r;
-  r.x = fe_sub(fe_sub(fe_sqr(rr), J), fe_add(V, V));
-  fe YJ = fe_mul(a.y, J);
-  r.y = fe_sub(fe_mul(rr, fe_sub(V, r.x)), fe_add(YJ, YJ));
-  fe zh = fe_sqr(fe_add(a.z, H));
-  r.z = fe_sub(fe_sub(zh, Z1Z1), HH);       // 2 Z1 H
+  const fe JV = fe_add(J, fe_add(V, V));                             // 3
+  r.x = fe_normalize_weak(fe_sub<2>(fe_sqr(R2), JV));                // R^2 - J - 2V: 1 + 4 -> 1
+  const fe YJ = fe_mul(a.y, J);                                      // 1
+  const fe m = fe_mul(R2, fe_sub<1>(V, r.x));                        // in 2, 3 -> 1
+  r.y = fe_normalize_weak(fe_sub<2>(m, fe_add(YJ, YJ)));             // 1 + 4 -> 1
+  const fe zh = fe_sqr(fe_add(a.z, H));                              // in 4 -> 1
+  r.z = fe_normalize_weak(fe_sub<2>(zh, fe_add(Z1Z1, HH)));          // 2 Z1 H: 1 + 4 -> 1
   return r;
 }
 
@@ -78,24 +82,25 @@ DEV gej gej_select(bool c, const gej& a, const gej& b) {
   return r;
 }
 
-// y from x with the requested parity; false if x^3 + 7 is not a square (ge_set_xo_var).
+// y from x (magnitude 1) with the requested parity; false if x^3 + 7 is not a square
+// (ge_set_xo_var). Returned coordinates are canonical.
 DEV bool ge_set_xo(ge& r, const fe& x, bool odd) {
-  fe c = fe_add(fe_mul(fe_sqr(x), x), fe_from_u32(7));
+  const fe c = fe_add(fe_mul(fe_sqr(x), x), fe_from_u32(7));        // 1 + tiny
   fe y;
-  bool ok = fe_sqrt(y, c);
+  const bool ok = fe_sqrt(y, c);
   y = fe_normalize(y);
-  bool flip = ((y.v[0] & 1u) != 0) != odd;
-  y = fe_select(flip, fe_normalize(fe_neg(y)), y);
-  r.x = x;
+  const bool flip = ((y.v[0] & 1u) != 0) != odd;
+  y = fe_select(flip, fe_normalize(fe_neg<1>(y)), y);
+  r.x = fe_normalize(x);
   r.y = y;
   return ok;
 }
 
-// On-curve check for an affine point with x, y < p (ge_is_valid_var).
+// On-curve check for an affine point (ge_is_valid_var).
 DEV bool ge_is_valid(const ge& a) {
-  fe y2 = fe_sqr(a.y);
-  fe x3 = fe_add(fe_mul(fe_sqr(a.x), a.x), fe_from_u32(7));
-  return fe_equal(y2, x3);
+  const fe y2 = fe_sqr(a.y);
+  const fe x3 = fe_add(fe_mul(fe_sqr(a.x), a.x), fe_from_u32(7));
+  return fe_equal(x3, y2);
 }
 
 }  // namespace eges

@@ -24,10 +24,10 @@ __global__ void __launch_bounds__(256) init_gtab_kernel(uint32_t* gtab) {
   ge a;
   a.x = fe_mul(acc.x, zi2);
   a.y = fe_mul(acc.y, fe_mul(zi2, zi));
-  store_pt(gtab + (size_t)e * 16, a);
+  store_pt(gtab + (size_t)e * PT_WORDS, a);
   ge l = a;
   l.x = fe_mul(a.x, fe_const(FE_BETA));
-  store_pt(gtab + ((size_t)GTAB + e) * 16, l);
+  store_pt(gtab + ((size_t)GTAB + e) * PT_WORDS, l);
 }
 
 // ------------------------------------------------------------------ prep kernels
@@ -184,7 +184,7 @@ hipError_t launch_prep_sender(const uint8_t* sighash, const uint8_t* r, const ui
 }
 
 size_t ws_bytes_per_block() { return WS_WORDS * sizeof(uint32_t); }
-size_t gtab_bytes() { return (size_t)2 * GTAB * 16 * sizeof(uint32_t); }
+size_t gtab_bytes() { return (size_t)2 * GTAB * PT_WORDS * sizeof(uint32_t); }
 int threads_per_block() { return WG; }
 
 }  // namespace eges

@@ -29,19 +29,20 @@ __global__ void __launch_bounds__(WG, 2) recover_kernel(RecoverParams prm) {
     sc Z = sc_from_limbs(zl, ovz);
     ok = ok && !ovr && !ovs && !sc_is_zero(R) && !sc_is_zero(S);
     // x = r (+ n)
-    fe x;
+    uint32_t xr[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) x.v[k] = R.v[k];
+    for (int k = 0; k < 8; ++k) xr[k] = R.v[k];
     if (recid & 2u) {
       ok = ok && !u256_ge(R.v, P_MINUS_N);
       uint64_t c = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        c += (uint64_t)x.v[k] + SC_N[k];
-        x.v[k] = (uint32_t)c;
+        c += (uint64_t)xr[k] + SC_N[k];
+        xr[k] = (uint32_t)c;
         c >>= 32;
       }
     }
+    const fe x = fe_from_u256(xr);
     ge Rp;
     const bool lifted = ge_set_xo(Rp, x, (recid & 1u) != 0);
     ok = ok && lifted;
@@ -62,8 +63,9 @@ __global__ void __launch_bounds__(WG, 2) recover_kernel(RecoverParams prm) {
     // affine: batch-invert Z
     fe zi = wg_batch_inv<FieldOps>(Q.z, ok, L.inv_scratch);
     fe zi2 = fe_sqr(zi);
-    fe X = fe_normalize(fe_mul(Q.x, zi2));
-    fe Y = fe_normalize(fe_mul(Q.y, fe_mul(zi2, zi)));
+    uint32_t X[8], Y[8];
+    fe_to_u256(X, fe_normalize(fe_mul(Q.x, zi2)));
+    fe_to_u256(Y, fe_normalize(fe_mul(Q.y, fe_mul(zi2, zi))));
     if (in) {
       const uint32_t st = pre != ST_OK ? pre : (ok ? ST_OK : ST_RECOVER_FAILED);
       prm.status[idx] = (uint8_t)st;

@@ -55,14 +55,15 @@ __global__ void __launch_bounds__(WG, 2) synth_sign_kernel(SynthParams prm) {
     fe rzi = wg_batch_inv<FieldOps>(Rj.z, true, L.inv_scratch);
     fe pzi = wg_batch_inv<FieldOps>(Pj.z, true, L.inv_scratch);
     fe rzi2 = fe_sqr(rzi), pzi2 = fe_sqr(pzi);
-    fe Rx = fe_normalize(fe_mul(Rj.x, rzi2));
-    fe Ry = fe_normalize(fe_mul(Rj.y, fe_mul(rzi2, rzi)));
-    fe Px = fe_normalize(fe_mul(Pj.x, pzi2));
-    fe Py = fe_normalize(fe_mul(Pj.y, fe_mul(pzi2, pzi)));
+    uint32_t Rx[8], Ry[8], Px[8], Py[8];
+    fe_to_u256(Rx, fe_normalize(fe_mul(Rj.x, rzi2)));
+    fe_to_u256(Ry, fe_normalize(fe_mul(Rj.y, fe_mul(rzi2, rzi))));
+    fe_to_u256(Px, fe_normalize(fe_mul(Pj.x, pzi2)));
+    fe_to_u256(Py, fe_normalize(fe_mul(Pj.y, fe_mul(pzi2, pzi))));
     // r = Rx mod n, recid = odd(Ry) | (Rx >= n) << 1
     bool rov;
-    sc r = sc_from_limbs(Rx.v, rov);
-    uint32_t recid = (Ry.v[0] & 1u) | (rov ? 2u : 0u);
+    sc r = sc_from_limbs(Rx, rov);
+    uint32_t recid = (Ry[0] & 1u) | (rov ? 2u : 0u);
     // s = k^-1 (z + r d)
     sc kinv = wg_batch_inv<ScalarOps>(kn, true, L.inv_scratch);
     sc s = sc_mul(kinv, sc_add(z, sc_mul(r, d)));
@@ -72,16 +73,10 @@ __global__ void __launch_bounds__(WG, 2) synth_sign_kernel(SynthParams prm) {
     }
     if (in) {
       uint8_t* m = prm.msg + (size_t)li * 32;
-      fe zf;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) zf.v[k] = ml[k];
-      write_be32(m, zf);
+      write_be32(m, ml);
       uint8_t* sg = prm.sig + (size_t)li * 65;
-      fe rf, sf;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) { rf.v[k] = r.v[k]; sf.v[k] = s.v[k]; }
-      write_be32(sg, rf);
-      write_be32(sg + 32, sf);
+      write_be32(sg, r.v);
+      write_be32(sg + 32, s.v);
       sg[64] = (uint8_t)recid;
       uint32_t a[5];
       pub_address(a, Px, Py);

@@ -34,14 +34,9 @@ __global__ void __launch_bounds__(WG, 2) verify_kernel(VerifyParams prm) {
     sc S = sc_from_limbs(sl, ovs);
     sc Z = sc_from_limbs(zl, ovz);
     bool ok = in && !ovr && !ovs;
-    // pubkey parse
-    fe X, Y;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { X.v[k] = px[k]; Y.v[k] = py[k]; }
-    const fe Xn = fe_normalize(X), Yn = fe_normalize(Y);
-    bool x_ok = true, y_ok = true;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { x_ok = x_ok && Xn.v[k] == X.v[k]; y_ok = y_ok && Yn.v[k] == Y.v[k]; }
+    // pubkey parse (eckey_impl.h:17-34): coordinates must be < p
+    const bool x_ok = !u256_ge(px, FE_P), y_ok = !u256_ge(py, FE_P);
+    const fe X = fe_from_u256(px), Y = fe_from_u256(py);
     const bool c33 = plen == 33 && (pfx == 2 || pfx == 3);
     const bool c65 = plen == 65 && (pfx == 4 || pfx == 6 || pfx == 7);
     ge P;
@@ -52,7 +47,7 @@ __global__ void __launch_bounds__(WG, 2) verify_kernel(VerifyParams prm) {
       ge full;
       full.x = X;
       full.y = Y;
-      const bool hybrid_bad = (pfx == 6 || pfx == 7) && ((Y.v[0] & 1u) != (pfx == 7 ? 1u : 0u));
+      const bool hybrid_bad = (pfx == 6 || pfx == 7) && ((py[0] & 1u) != (pfx == 7 ? 1u : 0u));
       const bool on = ge_is_valid(full);
       pk_ok = (c33 && x_ok && lo) || (c65 && x_ok && y_ok && !hybrid_bad && on);
       P.x = X;
@@ -74,21 +69,20 @@ __global__ void __launch_bounds__(WG, 2) verify_kernel(VerifyParams prm) {
     ecmult_core(Q, qinf, P, u2, u1, prm.gtab, prm.ws, L);
     ok = ok && !qinf;
     // x(Q) mod n == r  <=>  r*Z^2 == X  or  (r < p - n and (r + n)*Z^2 == X)
-    fe xr;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) xr.v[k] = R.v[k];
-    fe z2 = fe_sqr(Q.z);
-    bool eq = fe_equal(fe_mul(xr, z2), Q.x);
+    const fe xr = fe_from_u256(R.v);
+    const fe z2 = fe_sqr(Q.z);
+    bool eq = fe_equal(Q.x, fe_mul(xr, z2));
     const bool small = !u256_ge(R.v, P_MINUS_N);
-    fe xrn;
+    uint32_t rn[8];
     uint64_t c = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      c += (uint64_t)xr.v[k] + SC_N[k];
-      xrn.v[k] = (uint32_t)c;
+      c += (uint64_t)R.v[k] + SC_N[k];
+      rn[k] = (uint32_t)c;
       c >>= 32;
     }
-    eq = eq || (small && fe_equal(fe_mul(xrn, z2), Q.x));
+    const fe xrn = fe_from_u256(rn);
+    eq = eq || (small && fe_equal(Q.x, fe_mul(xrn, z2)));
     if (in) prm.ok[idx] = (ok && eq) ? 1 : 0;
   }
 }

@@ -11,6 +11,58 @@
 
 namespace eges {
 
+// 256x256 -> 512 schoolbook, row (operand) scanning over 32-bit limbs: each partial product
+// is one v_mad_u64_u32 whose 64-bit addend carries the running limb.
+DEV void mul_256x256(uint32_t t[16], const uint32_t a[8], const uint32_t b[8]) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    c = (uint64_t)a[0] * b[j] + (c >> 32);
+    t[j] = (uint32_t)c;
+  }
+  t[8] = (uint32_t)(c >> 32);
+#pragma unroll
+  for (int i = 1; i < 8; ++i) {
+    c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      c = (uint64_t)a[i] * b[j] + (uint64_t)t[i + j] + (c >> 32);
+      t[i + j] = (uint32_t)c;
+    }
+    t[i + 8] = (uint32_t)(c >> 32);
+  }
+}
+
+// Squaring: off-diagonal products once, doubled, plus the diagonal.
+DEV void sqr_256(uint32_t t[16], const uint32_t a[8]) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = i + 1; j < 8; ++j) {
+      c = (uint64_t)a[i] * a[j] + (uint64_t)t[i + j] + (c >> 32);
+      t[i + j] = (uint32_t)c;
+    }
+    t[i + 8] = (uint32_t)(c >> 32);
+  }
+#pragma unroll
+  for (int i = 15; i > 0; --i) t[i] = (t[i] << 1) | (t[i - 1] >> 31);  // off-diagonal sum < 2^511
+  t[0] <<= 1;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint64_t sq = (uint64_t)a[i] * a[i];
+    c += (uint64_t)t[2 * i] + (uint32_t)sq;
+    t[2 * i] = (uint32_t)c;
+    c >>= 32;
+    c += (uint64_t)t[2 * i + 1] + (uint32_t)(sq >> 32);
+    t[2 * i + 1] = (uint32_t)c;
+    c >>= 32;
+  }
+}
+
 struct sc {
   uint32_t v[8];
 };

@@ -1,0 +1,156 @@
+// Field / group self-test kernels (test harness only: libeges_selftest.so, used by
+// tests/test_gpu_field.py; not part of libeges.so). Inputs and outputs are canonical 256-bit
+// integers as 8 little-endian 32-bit words; the Python side checks against big integers.
+#include <hip/hip_runtime.h>
+
+#include "core.cuh"
+
+namespace eges {
+
+// op codes
+enum : int {
+  OP_MUL = 0,      // a * b
+  OP_SQR = 1,      // a^2
+  OP_ADD = 2,      // a + b
+  OP_SUB = 3,      // a - b
+  OP_INV = 4,      // a^-1
+  OP_SQRT = 5,     // sqrt(a) (out) and is-square flag (flag)
+  OP_LAZY = 6,     // (4a) * (a + 3b) - 2b*(a - b) with maximal lazy magnitudes
+  OP_NEG = 7,      // -a
+  OP_EQZ = 8,      // flag = (a == b mod p) via fe_equal on a raw (non-reduced) input
+  OP_DBL = 9,      // Jacobian doubling of affine (a, b): out affine x, out2 affine y
+  OP_MADD = 10,    // (a,b) + (c,d) affine inputs via Jacobian (Z=1) mixed add; flags h0/r0
+  OP_SCMUL = 11,   // a * b mod n
+  OP_SCINV = 12,   // a^-1 mod n
+  OP_GLV = 13,     // glv split of a: out = |k1|, out2 = |k2| (160-bit), flag = signs
+};
+
+__device__ fe ld(const uint32_t* p, uint32_t i) {
+  uint32_t x[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x[k] = p[(size_t)i * 8 + k];
+  return fe_from_u256(x);
+}
+__device__ void st(uint32_t* p, uint32_t i, const fe& a) {
+  uint32_t x[8];
+  fe_to_u256(x, fe_normalize(a));
+#pragma unroll
+  for (int k = 0; k < 8; ++k) p[(size_t)i * 8 + k] = x[k];
+}
+
+__global__ void selftest_kernel(int op, uint32_t n, const uint32_t* A, const uint32_t* B, const uint32_t* C,
+                                const uint32_t* D, uint32_t* out, uint32_t* out2, uint32_t* flag) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const fe a = ld(A, i), b = ld(B, i);
+  switch (op) {
+    case OP_MUL: st(out, i, fe_mul(a, b)); break;
+    case OP_SQR: st(out, i, fe_sqr(a)); break;
+    case OP_ADD: st(out, i, fe_add(a, b)); break;
+    case OP_SUB: st(out, i, fe_sub<1>(a, b)); break;
+    case OP_INV: st(out, i, fe_inv(a)); break;
+    case OP_SQRT: {
+      fe r;
+      const bool ok = fe_sqrt(r, a);
+      st(out, i, r);
+      flag[i] = ok;
+      break;
+    }
+    case OP_LAZY: {
+      const fe a4 = fe_add(fe_add(a, a), fe_add(a, a));         // 4
+      const fe t = fe_add(a, fe_add(b, fe_add(b, b)));          // 4
+      const fe u = fe_mul(a4, t);                               // 1
+      const fe w = fe_mul(fe_add(b, b), fe_sub<1>(a, b));       // 2 x 3
+      st(out, i, fe_sub<1>(u, w));
+      break;
+    }
+    case OP_NEG: st(out, i, fe_neg<1>(a)); break;
+    case OP_EQZ: {
+      // raw limbs of A taken as a weak value (may be >= p); equality with b
+      flag[i] = fe_equal(a, b) ? 1u : 0u;
+      break;
+    }
+    case OP_DBL: {
+      gej j;
+      j.x = a;
+      j.y = b;
+      j.z = fe_one();
+      gej r = gej_double(gej_double(j));  // 4P, exercises Z != 1
+      const fe zi = fe_inv(r.z);
+      const fe zi2 = fe_sqr(zi);
+      st(out, i, fe_mul(r.x, zi2));
+      st(out2, i, fe_mul(r.y, fe_mul(zi2, zi)));
+      break;
+    }
+    case OP_MADD: {
+      gej j;
+      j.x = a;
+      j.y = b;
+      j.z = fe_one();
+      j = gej_double(j);  // 2P (Z != 1)
+      ge q;
+      q.x = ld(C, i);
+      q.y = ld(D, i);
+      bool hz, rz;
+      gej r = gej_add_ge(j, q, hz, rz);
+      const fe zi = fe_inv(r.z);
+      const fe zi2 = fe_sqr(zi);
+      st(out, i, fe_mul(r.x, zi2));
+      st(out2, i, fe_mul(r.y, fe_mul(zi2, zi)));
+      flag[i] = (hz ? 1u : 0u) | (rz ? 2u : 0u);
+      break;
+    }
+    case OP_SCMUL:
+    case OP_SCINV: {
+      uint32_t x[8], y[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { x[k] = A[(size_t)i * 8 + k]; y[k] = B[(size_t)i * 8 + k]; }
+      bool o1, o2;
+      sc s1 = sc_from_limbs(x, o1), s2 = sc_from_limbs(y, o2);
+      sc r = op == OP_SCMUL ? sc_mul(s1, s2) : sc_inv(s1);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) out[(size_t)i * 8 + k] = r.v[k];
+      break;
+    }
+    case OP_GLV: {
+      uint32_t x[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = A[(size_t)i * 8 + k];
+      bool o;
+      sc s = sc_from_limbs(x, o);
+      glv_half h1, h2;
+      glv_split(h1, h2, s);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        out[(size_t)i * 8 + k] = k < 5 ? h1.mag[k] : 0u;
+        out2[(size_t)i * 8 + k] = k < 5 ? h2.mag[k] : 0u;
+      }
+      flag[i] = (h1.neg ? 1u : 0u) | (h2.neg ? 2u : 0u);
+      break;
+    }
+  }
+}
+
+}  // namespace eges
+
+extern "C" int eges_selftest(int op, uint32_t n, const uint32_t* a, const uint32_t* b, const uint32_t* c,
+                             const uint32_t* d, uint32_t* out, uint32_t* out2, uint32_t* flag) {
+  const size_t B = (size_t)n * 32;
+  uint32_t *da, *db, *dc, *dd, *dout, *dout2, *dflag;
+  if (hipMalloc(&da, B) || hipMalloc(&db, B) || hipMalloc(&dc, B) || hipMalloc(&dd, B) || hipMalloc(&dout, B) ||
+      hipMalloc(&dout2, B) || hipMalloc(&dflag, (size_t)n * 4))
+    return -1;
+  hipMemcpy(da, a, B, hipMemcpyHostToDevice);
+  hipMemcpy(db, b, B, hipMemcpyHostToDevice);
+  hipMemcpy(dc, c, B, hipMemcpyHostToDevice);
+  hipMemcpy(dd, d, B, hipMemcpyHostToDevice);
+  hipMemset(dflag, 0, (size_t)n * 4);
+  hipLaunchKernelGGL(eges::selftest_kernel, dim3((n + 127) / 128), dim3(128), 0, 0, op, n, da, db, dc, dd, dout, dout2,
+                     dflag);
+  hipError_t e = hipDeviceSynchronize();
+  hipMemcpy(out, dout, B, hipMemcpyDeviceToHost);
+  hipMemcpy(out2, dout2, B, hipMemcpyDeviceToHost);
+  hipMemcpy(flag, dflag, (size_t)n * 4, hipMemcpyDeviceToHost);
+  hipFree(da); hipFree(db); hipFree(dc); hipFree(dd); hipFree(dout); hipFree(dout2); hipFree(dflag);
+  return e == hipSuccess ? 0 : -2;
+}
