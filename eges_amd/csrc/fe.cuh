@@ -34,6 +34,14 @@ constexpr uint32_t C256_1 = 64u;
 
 DEV uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
 
+// A wave-uniform constant the optimiser cannot see through: keeps x * 2^k as ONE
+// v_mad_u64_u32 (SGPR operand) instead of the v_mov + v_lshlrev_b64 + v_lshl_add_u64 the
+// shift canonicalisation produces for 64-bit accumulators.
+DEV uint32_t opaque_u32(uint32_t x) {
+  asm volatile("" : "+s"(x));
+  return x;
+}
+
 DEV fe fe_zero() {
   fe r;
 #pragma unroll
@@ -79,6 +87,7 @@ DEV void fe_to_u256(uint32_t x[8], const fe& a) {
 // ------------------------------------------------------------------ reduction of 19 columns
 // S[0..18]: column sums (each < 2^59.4). Returns magnitude-1 limbs.
 DEV fe fe_reduce_cols(uint64_t S[19]) {
+  const uint32_t f1 = opaque_u32(FOLD1), f16 = opaque_u32(1u << 16);
   // fold columns 18..10 (descending: column 18 spills into column 10, folded afterwards).
   // S_k 2^(26k) = (hi 2^32 + lo) 2^(26(k-10)) (2^36 + 15632)
 #pragma unroll
@@ -86,9 +95,9 @@ DEV fe fe_reduce_cols(uint64_t S[19]) {
     const uint32_t lo = (uint32_t)S[k];
     const uint32_t hi = (uint32_t)(S[k] >> 32);
     S[k - 10] = mad64(lo, FOLD0, S[k - 10]);
-    S[k - 9] = mad64(lo, FOLD1, S[k - 9]);
+    S[k - 9] = mad64(lo, f1, S[k - 9]);
     S[k - 9] = mad64(hi, FOLD0 << 6, S[k - 9]);
-    S[k - 8] = mad64(hi, 1u << 16, S[k - 8]);
+    S[k - 8] = mad64(hi, f16, S[k - 8]);
   }
   fe r;
 #pragma unroll
@@ -100,7 +109,7 @@ DEV fe fe_reduce_cols(uint64_t S[19]) {
   const uint64_t c = S[9] >> 26;  // < 2^33.5: multiple of 2^260
   const uint32_t cl = (uint32_t)c, ch = (uint32_t)(c >> 32);
   uint64_t t0 = mad64(cl, FOLD0, r.v[0]);
-  uint64_t t1 = mad64(cl, FOLD1, r.v[1]);
+  uint64_t t1 = mad64(cl, f1, r.v[1]);
   t1 = mad64(ch, FOLD0 << 6, t1);
   r.v[0] = (uint32_t)t0 & M26;
   t1 += t0 >> 26;

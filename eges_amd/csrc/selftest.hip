@@ -140,17 +140,88 @@ extern "C" int eges_selftest(int op, uint32_t n, const uint32_t* a, const uint32
   if (hipMalloc(&da, B) || hipMalloc(&db, B) || hipMalloc(&dc, B) || hipMalloc(&dd, B) || hipMalloc(&dout, B) ||
       hipMalloc(&dout2, B) || hipMalloc(&dflag, (size_t)n * 4))
     return -1;
-  hipMemcpy(da, a, B, hipMemcpyHostToDevice);
-  hipMemcpy(db, b, B, hipMemcpyHostToDevice);
-  hipMemcpy(dc, c, B, hipMemcpyHostToDevice);
-  hipMemcpy(dd, d, B, hipMemcpyHostToDevice);
-  hipMemset(dflag, 0, (size_t)n * 4);
+  (void)hipMemcpy(da, a, B, hipMemcpyHostToDevice);
+  (void)hipMemcpy(db, b, B, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dc, c, B, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dd, d, B, hipMemcpyHostToDevice);
+  (void)hipMemset(dflag, 0, (size_t)n * 4);
   hipLaunchKernelGGL(eges::selftest_kernel, dim3((n + 127) / 128), dim3(128), 0, 0, op, n, da, db, dc, dd, dout, dout2,
                      dflag);
   hipError_t e = hipDeviceSynchronize();
-  hipMemcpy(out, dout, B, hipMemcpyDeviceToHost);
-  hipMemcpy(out2, dout2, B, hipMemcpyDeviceToHost);
-  hipMemcpy(flag, dflag, (size_t)n * 4, hipMemcpyDeviceToHost);
-  hipFree(da); hipFree(db); hipFree(dc); hipFree(dd); hipFree(dout); hipFree(dout2); hipFree(dflag);
+  (void)hipMemcpy(out, dout, B, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(out2, dout2, B, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(flag, dflag, (size_t)n * 4, hipMemcpyDeviceToHost);
+  (void)hipFree(da); (void)hipFree(db); (void)hipFree(dc); (void)hipFree(dd); (void)hipFree(dout); (void)hipFree(dout2); (void)hipFree(dflag);
   return e == hipSuccess ? 0 : -2;
+}
+
+// ---------------------------------------------------------------- op microbenchmarks
+// Each lane runs `reps` iterations of one operation on register-resident data; the host
+// launches 2 blocks of 256 per CU (the recover kernel's occupancy) and reports wall time.
+namespace eges {
+template <int OP>
+__global__ void __launch_bounds__(256, 2) opbench_kernel(uint32_t* sink, int reps) {
+  uint32_t seed = blockIdx.x * 256 + threadIdx.x + 1;
+  uint32_t w[8];
+  for (int k = 0; k < 8; ++k) w[k] = seed * 2654435761u + k * 40503u;
+  fe a = fe_from_u256(w);
+  for (int k = 0; k < 8; ++k) w[k] = w[k] * 747796405u + 1u;
+  fe b = fe_from_u256(w);
+  gej J;
+  J.x = a; J.y = b; J.z = fe_normalize_weak(fe_add(a, b));
+  ge q;
+  q.x = b; q.y = a;
+  sc s1, s2;
+  for (int k = 0; k < 8; ++k) { s1.v[k] = w[k] >> 1; s2.v[k] = w[k] * 3u >> 1; }
+  uint32_t acc = 0;
+#pragma unroll 1
+  for (int r = 0; r < reps; ++r) {
+    if constexpr (OP == 0) a = fe_mul(a, b);
+    else if constexpr (OP == 1) a = fe_sqr(a);
+    else if constexpr (OP == 2) J = gej_double(J);
+    else if constexpr (OP == 3) { bool hz, rz; J = gej_add_ge(J, q, hz, rz); acc += hz + rz; }
+    else if constexpr (OP == 4) a = fe_normalize(fe_add(a, b));
+    else if constexpr (OP == 5) a = fe_normalize_weak(fe_sub<2>(a, fe_add(b, b)));
+    else if constexpr (OP == 6) s1 = sc_mul(s1, s2);
+    else if constexpr (OP == 7) { bool z = fe_is_zero(a); acc += z; a = fe_normalize_weak(fe_add(a, b)); }
+  }
+  for (int k = 0; k < 10; ++k) acc += a.v[k] + J.x.v[k] + J.y.v[k] + J.z.v[k];
+  for (int k = 0; k < 8; ++k) acc += s1.v[k];
+  sink[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+}  // namespace eges
+
+// SIMD-cycles per lane-op at 2.4 GHz nominal: wall * 2.4e9 * (CUs * 4 SIMDs) / (lanes * reps)
+extern "C" double eges_opbench(int op, int reps) {
+  hipDeviceProp_t prop;
+  (void)hipGetDeviceProperties(&prop, 0);
+  const int blocks = prop.multiProcessorCount * 2;
+  uint32_t* sink;
+  if (hipMalloc(&sink, (size_t)blocks * 256 * 4) != hipSuccess) return -1;
+  auto launch = [&](int r) {
+    switch (op) {
+      case 0: hipLaunchKernelGGL(eges::opbench_kernel<0>, dim3(blocks), dim3(256), 0, 0, sink, r); break;
+      case 1: hipLaunchKernelGGL(eges::opbench_kernel<1>, dim3(blocks), dim3(256), 0, 0, sink, r); break;
+      case 2: hipLaunchKernelGGL(eges::opbench_kernel<2>, dim3(blocks), dim3(256), 0, 0, sink, r); break;
+      case 3: hipLaunchKernelGGL(eges::opbench_kernel<3>, dim3(blocks), dim3(256), 0, 0, sink, r); break;
+      case 4: hipLaunchKernelGGL(eges::opbench_kernel<4>, dim3(blocks), dim3(256), 0, 0, sink, r); break;
+      case 5: hipLaunchKernelGGL(eges::opbench_kernel<5>, dim3(blocks), dim3(256), 0, 0, sink, r); break;
+      case 6: hipLaunchKernelGGL(eges::opbench_kernel<6>, dim3(blocks), dim3(256), 0, 0, sink, r); break;
+      case 7: hipLaunchKernelGGL(eges::opbench_kernel<7>, dim3(blocks), dim3(256), 0, 0, sink, r); break;
+    }
+  };
+  launch(8);
+  (void)hipDeviceSynchronize();
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, 0);
+  launch(reps);
+  (void)hipEventRecord(e1, 0);
+  (void)hipEventSynchronize(e1);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipFree(sink);
+  const double lanes = (double)blocks * 256;
+  return (double)ms * 2.4e6 * prop.multiProcessorCount * 4 / (lanes * reps);
 }
