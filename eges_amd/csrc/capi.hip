@@ -135,11 +135,25 @@ struct Serial {
 
 // ------------------------------------------------------------------ device-side pipelines
 // All pointers device pointers; d.mu held by the caller.
+#ifdef EGES_PHASE_STAMPS
+// Diagnostic build (libeges_diag.so): per-wave phase cycle sums of the last recover launch.
+static uint64_t* g_stamps = nullptr;
+static size_t g_stamp_waves = 0;
+extern "C" size_t eges_diag_read_stamps(uint64_t* out, size_t max_waves) {
+  const size_t w = g_stamp_waves < max_waves ? g_stamp_waves : max_waves;
+  if (g_stamps && out && w) {
+    if (hipDeviceSynchronize() != hipSuccess) return 0;
+    if (hipMemcpy(out, g_stamps, w * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  }
+  return w;
+}
+#endif
+
 int run_recover_dev(Dev& d, const uint8_t* msg, const uint8_t* sig, size_t n, uint8_t* pub, uint8_t* addr,
                     uint8_t* status, hipStream_t st) {
   const size_t c = std::min(n, CHUNK);
   const size_t n_pad = align_up(c, 64);
-  int rc = dev_ensure_buf(d, n_pad * REC_ROWS * 4);
+  int rc = dev_ensure_buf(d, recover_scratch_bytes(n_pad));
   if (rc) return rc;
   uint32_t* rec = reinterpret_cast<uint32_t*>(d.buf);
   Serial ser(d, st);
@@ -148,7 +162,14 @@ int run_recover_dev(Dev& d, const uint8_t* msg, const uint8_t* sig, size_t n, ui
     HIPCHK(launch_prep_ecrecover(msg + off * 32, sig + off * 65, m, (uint32_t)n_pad, rec, st));
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr ? addr + off * 20 : nullptr, pub ? pub + off * 65 : nullptr,
                     d.gtab, d.ws};
+#ifdef EGES_PHASE_STAMPS
+    if (!g_stamps) HIPCHK(hipMalloc(&g_stamps, (size_t)d.mb_recover * 4 /* waves per block */ * 8 * sizeof(uint64_t)));
+    g_stamp_waves = (size_t)d.mb_recover * 4 /* waves per block */;
+    HIPCHK(hipMemsetAsync(g_stamps, 0, g_stamp_waves * 8 * sizeof(uint64_t), st));
+    HIPCHK(launch_recover_stamped(p, d.mb_recover, st, g_stamps));
+#else
     HIPCHK(launch_recover(p, d.mb_recover, st));
+#endif
   }
   return EGES_SUCCESS;
 }
@@ -158,7 +179,7 @@ int run_sender_dev(Dev& d, const uint8_t* sighash, const uint8_t* r, const uint8
                    hipStream_t st) {
   const size_t c = std::min(n, CHUNK);
   const size_t n_pad = align_up(c, 64);
-  int rc = dev_ensure_buf(d, n_pad * REC_ROWS * 4);
+  int rc = dev_ensure_buf(d, recover_scratch_bytes(n_pad));
   if (rc) return rc;
   uint32_t* rec = reinterpret_cast<uint32_t*>(d.buf);
   Serial ser(d, st);
@@ -208,7 +229,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       case HostJob::SENDER: in_bytes = m * (32 * 4 + 1); break;
       case HostJob::VERIFY: in_bytes = m * (65 + 1 + 32 + 64); break;
     }
-    const size_t rec_bytes = (j.kind == HostJob::VERIFY) ? 0 : m_pad * REC_ROWS * 4;
+    const size_t rec_bytes = (j.kind == HostJob::VERIFY) ? 0 : recover_scratch_bytes(m_pad);
     const size_t out_bytes = m * (65 + 20 + 1);
     const size_t o_in = 0, o_rec = align_up(in_bytes, 256), o_out = o_rec + align_up(rec_bytes, 256);
     int rc = dev_ensure_buf(d, o_out + out_bytes);

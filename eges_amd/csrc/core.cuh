@@ -213,6 +213,28 @@ DEV void add_step(gej& acc, bool& inf, const ge& p, bool use) {
   inf = use ? (inf ? false : to_inf) : inf;
 }
 
+// acc (on the table's isomorphic curve, global Z = zeta) += p (affine on the true curve).
+DEV void add_step_zinv(gej& acc, bool& inf, const ge& p, bool use, const fe& zeta) {
+  bool hz, rz;
+  gej s = gej_add_ge_zinv(acc, p, zeta, hz, rz);
+  const bool exc = use && !inf && hz;
+  if (__any(exc)) {
+    gej d = gej_double(acc);
+    s = gej_select(exc && rz, d, s);
+  }
+  const bool to_inf = exc && !rz;
+  if (__any(use && inf)) {  // acc = p mapped onto the isomorphic curve: (x zeta^2, y zeta^3, 1)
+    const fe z2 = fe_sqr(zeta);
+    gej pj;
+    pj.x = fe_mul(p.x, z2);
+    pj.y = fe_mul(p.y, fe_mul(z2, zeta));
+    pj.z = fe_one();
+    s = gej_select(inf, pj, s);
+  }
+  acc = gej_select(use, s, acc);
+  inf = use ? (inf ? false : to_inf) : inf;
+}
+
 DEV ge neg_if(const ge& p, bool neg) {  // y magnitude <= 2 afterwards
   ge r;
   r.x = p.x;
@@ -224,11 +246,24 @@ struct CoreLds {
   int8_t rdig[2][RWIN][WG];    // R / lambda R digits
   int16_t gdig[2][GWIN][WG];   // G / lambda G digits
   uint32_t inv_scratch[2 * NWAVES * 10];
+  uint32_t zeta[10][WG];       // per-lane global Z of the R table
+  uint32_t park[18][WG];       // registers parked across ecmult_core by the lane-serial kernels
 };
 
+template <int N>
+DEV void lds_put(uint32_t (*a)[WG], const uint32_t* v) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) a[i][threadIdx.x] = v[i];
+}
+template <int N>
+DEV void lds_get(uint32_t (*a)[WG], uint32_t* v) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = a[i][threadIdx.x];
+}
+
 // Per-block workspace (global memory, this block's lanes only):
-//   [0, PTAB*WG*16)            affine table {1..8}*P, entry-major then lane, 16 words/entry
-//   [PTAB*WG*16, +(PTAB-1)*WG*16)  Z_i and prefix products while the table is built
+//   [0, PTAB*WG*PT_WORDS)              table {1..8}*P, entry-major then lane
+//   [PTAB*WG*PT_WORDS, +(PTAB-1)*...)  Z ratios Z_{i+1}/Z_i while the table is built
 constexpr size_t WS_WORDS = (size_t)(2 * PTAB - 1) * WG * PT_WORDS;
 
 DEV void store_fe2(uint32_t* dst, const fe& a, const fe& b) {
@@ -238,10 +273,30 @@ DEV void store_fe2(uint32_t* dst, const fe& a, const fe& b) {
   store_pt(dst, p);
 }
 
+// Diagnostic phase stamps (EGES_PHASE_STAMPS builds only): per-wave s_memtime deltas.
+struct NoStamp {
+  DEV void mark(int) {}
+};
+struct Stamper {
+  uint64_t acc[8];
+  uint64_t last;
+  DEV Stamper() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0;
+    last = __builtin_amdgcn_s_memtime();
+  }
+  DEV void mark(int i) {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    acc[i] += now - last;
+    last = now;
+  }
+};
+
 // Q = u_r * P + u_g * G for the workgroup's 256 lanes. P given affine (a valid curve point,
 // possibly a dummy for failed lanes). Returns Jacobian Q and its infinity flag.
+template <class ST = NoStamp>
 DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& u_g, const uint32_t* gtab,
-                     uint32_t* ws, CoreLds& L) {
+                     uint32_t* ws, CoreLds& L, ST* st = nullptr) {
   const int tid = threadIdx.x;
   uint32_t* const base = ws + (size_t)blockIdx.x * WS_WORDS;
   uint32_t* const zp = base + (size_t)PTAB * WG * PT_WORDS;
@@ -255,8 +310,12 @@ DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& 
     recode<12, GWIN, int16_t>(h1, &L.gdig[0][0][0]);
     recode<12, GWIN, int16_t>(h2, &L.gdig[1][0][0]);
   }
-  // --- per-lane table {1..8} * P: Jacobian T_{i+1} = T_i + P streamed to the workspace,
-  //     then one workgroup batch inversion of prod Z_i and a backward Montgomery pass.
+  if (st) st->mark(2);
+  // --- per-lane table {1..8} * P with one global Z (ecmult_impl.h:52-110): T_1 = P,
+  //     T_2 = 2P, T_{i+1} = T_i + P in Jacobian, recording the ratios Z_{i+1}/Z_i; a backward
+  //     pass rescales every T_i to Z_8 = zeta. The entries are then affine points of the
+  //     isomorphic curve y^2 = x^3 + 7 zeta^6 — no field inversion.
+  fe zeta;
   {
     store_pt(base + (size_t)tid * PT_WORDS, P);
     gej T;
@@ -264,35 +323,32 @@ DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& 
     T.y = P.y;
     T.z = fe_one();
     T = gej_double(T);
-    fe pre = T.z;
     store_fe2(base + (size_t)(1 * WG + tid) * PT_WORDS, T.x, T.y);
-    store_fe2(zp + (size_t)(0 * WG + tid) * PT_WORDS, T.z, pre);
+    store_fe2(zp + (size_t)(0 * WG + tid) * PT_WORDS, T.z, T.z);  // Z_2 / Z_1 = Z_2
 #pragma unroll 1
     for (int i = 2; i < PTAB; ++i) {
       bool hz, rz;
-      T = gej_add_ge(T, P, hz, rz);  // i*P + P, never exceptional for i < 8 < n
-      pre = fe_mul(pre, T.z);
+      fe zr;
+      T = gej_add_ge_zr(T, P, zr, hz, rz);  // i*P + P, never exceptional for i < 8 < n
       store_fe2(base + (size_t)(i * WG + tid) * PT_WORDS, T.x, T.y);
-      store_fe2(zp + (size_t)((i - 1) * WG + tid) * PT_WORDS, T.z, pre);
+      store_fe2(zp + (size_t)((i - 1) * WG + tid) * PT_WORDS, zr, zr);
     }
-    fe inv = wg_batch_inv<FieldOps>(pre, true, L.inv_scratch);  // 1 / (Z_1 ... Z_7)
+    zeta = T.z;
+    fe rho = fe_one();
 #pragma unroll 1
-    for (int i = PTAB - 1; i >= 1; --i) {
-      const ge zz = load_pt(zp + (size_t)((i - 1) * WG + tid) * PT_WORDS);  // .x = Z_i
-      fe zi = inv;
-      if (i > 1) {
-        const ge pp = load_pt(zp + (size_t)((i - 2) * WG + tid) * PT_WORDS);  // .y = pre_{i-1}
-        zi = fe_mul(inv, pp.y);
-        inv = fe_mul(inv, zz.x);
-      }
+    for (int i = PTAB - 2; i >= 0; --i) {
+      const fe zr = load_pt(zp + (size_t)(i * WG + tid) * PT_WORDS).x;  // Z_{i+2} / Z_{i+1}
+      rho = i == PTAB - 2 ? zr : fe_mul(rho, zr);                        // Z_8 / Z_{i+1}
       const ge J = load_pt(base + (size_t)(i * WG + tid) * PT_WORDS);
-      const fe zi2 = fe_sqr(zi);
+      const fe r2 = fe_sqr(rho);
       ge a;
-      a.x = fe_mul(J.x, zi2);
-      a.y = fe_mul(J.y, fe_mul(zi2, zi));
+      a.x = fe_mul(J.x, r2);
+      a.y = fe_mul(J.y, fe_mul(r2, rho));
       store_pt(base + (size_t)(i * WG + tid) * PT_WORDS, a);
     }
+    lds_put<10>(L.zeta, zeta.v);
   }
+  if (st) st->mark(3);
   // --- Strauss-Shamir: 33 windows of 4 bits (R, lambda R) interleaved with 11 windows of
   //     12 bits (G, lambda G) every third window.
   inf = true;
@@ -317,10 +373,22 @@ DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& 
       if (j < 2) p = load_pt(base + (size_t)(e * WG + tid) * PT_WORDS);
       else p = load_pt(gtab + ((size_t)(j - 2) * GTAB + e) * PT_WORDS);
       if (j == 1) p.x = fe_mul(p.x, fe_const(FE_BETA));
-      add_step(acc, inf, neg_if(p, d < 0), d != 0);
+      if (j < 2) {
+        add_step(acc, inf, neg_if(p, d < 0), d != 0);
+      } else {
+        fe z;
+        lds_get<10>(L.zeta, z.v);
+        add_step_zinv(acc, inf, neg_if(p, d < 0), d != 0, z);
+      }
     }
   }
-  __syncthreads();
+  // true Jacobian Z of the accumulator
+  {
+    fe z;
+    lds_get<10>(L.zeta, z.v);
+    acc.z = fe_mul(acc.z, z);
+  }
+  if (st) st->mark(4);
 }
 
 // ------------------------------------------------------------------ byte helpers

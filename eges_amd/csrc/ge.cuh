@@ -2,7 +2,9 @@
 //
 // Value-level restatement of libsecp256k1's group module (src/group_impl.h: gej_double_var
 // :301-354, gej_add_ge_var :414-461, ge_set_xo_var :216-237, ge_is_valid_var :287-299).
-// Formulas: doubling dbl-2009-l (2M + 5S), mixed addition madd-2007-bl (7M + 4S). The
+// Formulas: doubling dbl-2009-l (2M + 5S), mixed addition madd-2007-bl (7M + 4S);
+// the table/accumulator "effective affine" trick follows ecmult_impl.h:52-110 (odd multiples
+// on an isomorphic curve sharing one global Z). The
 // exceptional cases libsecp256k1 handles with branches (a == infinity, a == b, a == -b) are
 // reported through flags so the kernel can resolve them with wave-uniform control flow.
 //
@@ -41,10 +43,18 @@ DEV gej gej_double(const gej& a) {
 // Mixed addition a (Jacobian, not infinity) + b (affine, x magnitude 1, y magnitude <= 2).
 // Sets h_zero when U2 == X1 (a == +-b); then r_zero tells doubling (a == b) from infinity
 // (a == -b) and the returned point is meaningless.
-DEV gej gej_add_ge(const gej& a, const ge& b, bool& h_zero, bool& r_zero) {
-  const fe Z1Z1 = fe_sqr(a.z);                                       // 1
+//   ADD_PLAIN  b is affine in a's coordinates (madd-2007-bl, Z3 = (Z1 + H)^2 - Z1^2 - H^2).
+//   ADD_ZINV   b is affine on the true curve while a lives on the isomorphic curve of a table
+//              with global Z = bzinv (a's true Jacobian Z is a.z * bzinv); the result stays in
+//              a's coordinates (group_impl.h:463-517, gej_add_zinv_var; used at ecmult_impl.h:383). One extra mul.
+//   ADD_ZR     as ADD_PLAIN, and *zr = Z3 / Z1 = 2H (group_impl.h:414-461, the rzr output).
+enum AddMode { ADD_PLAIN, ADD_ZINV, ADD_ZR };
+template <AddMode M>
+DEV gej gej_add_ge_t(const gej& a, const ge& b, const fe* bzinv, bool& h_zero, bool& r_zero, fe* zr) {
+  const fe az = M == ADD_ZINV ? fe_mul(a.z, *bzinv) : a.z;           // 1
+  const fe Z1Z1 = fe_sqr(az);                                        // 1
   const fe U2 = fe_mul(b.x, Z1Z1);                                   // 1
-  const fe S2 = fe_mul(fe_mul(b.y, a.z), Z1Z1);                      // 1
+  const fe S2 = fe_mul(fe_mul(b.y, az), Z1Z1);                       // 1
   const fe H = fe_sub<1>(U2, a.x);                                   // 3
   const fe R = fe_normalize_weak(fe_sub<1>(S2, a.y));                // 1
   h_zero = fe_is_zero(H);
@@ -61,9 +71,26 @@ DEV gej gej_add_ge(const gej& a, const ge& b, bool& h_zero, bool& r_zero) {
   const fe YJ = fe_mul(a.y, J);                                      // 1
   const fe m = fe_mul(R2, fe_sub<1>(V, r.x));                        // in 2, 3 -> 1
   r.y = fe_normalize_weak(fe_sub<2>(m, fe_add(YJ, YJ)));             // 1 + 4 -> 1
-  const fe zh = fe_sqr(fe_add(a.z, H));                              // in 4 -> 1
-  r.z = fe_normalize_weak(fe_sub<2>(zh, fe_add(Z1Z1, HH)));          // 2 Z1 H: 1 + 4 -> 1
+  if (M == ADD_PLAIN) {
+    const fe zh = fe_sqr(fe_add(a.z, H));                            // in 4 -> 1
+    r.z = fe_normalize_weak(fe_sub<2>(zh, fe_add(Z1Z1, HH)));        // 2 Z1 H: 1 + 4 -> 1
+  } else if (M == ADD_ZINV) {
+    const fe zh = fe_mul(a.z, H);                                    // 1
+    r.z = fe_normalize_weak(fe_add(zh, zh));                         // 2 Z1 H
+  } else {
+    *zr = fe_normalize_weak(fe_add(H, H));                           // 2H, 1
+    r.z = fe_mul(a.z, *zr);
+  }
   return r;
+}
+DEV gej gej_add_ge(const gej& a, const ge& b, bool& h_zero, bool& r_zero) {
+  return gej_add_ge_t<ADD_PLAIN>(a, b, nullptr, h_zero, r_zero, nullptr);
+}
+DEV gej gej_add_ge_zinv(const gej& a, const ge& b, const fe& bzinv, bool& h_zero, bool& r_zero) {
+  return gej_add_ge_t<ADD_ZINV>(a, b, &bzinv, h_zero, r_zero, nullptr);
+}
+DEV gej gej_add_ge_zr(const gej& a, const ge& b, fe& zr, bool& h_zero, bool& r_zero) {
+  return gej_add_ge_t<ADD_ZR>(a, b, nullptr, h_zero, r_zero, &zr);
 }
 
 DEV gej gej_from_ge(const ge& b) {

@@ -9,6 +9,14 @@ namespace eges {
 // Record layout produced by the prep kernels: 25 SoA rows of n_pad words
 // (z[8], r[8], s[8], meta) — see kernels.hip.
 constexpr int REC_ROWS = 25;
+// The recover kernel keeps per-signature state between its phases in SLOT_ROWS uint4 rows of
+// n_pad entries right after the record rows (k_recover.hip). A thread owns <= MAX_SLOTS.
+constexpr int SLOT_ROWS = 12;
+constexpr uint32_t MAX_SLOTS = 32;
+inline size_t recover_scratch_bytes(size_t n_pad) { return n_pad * ((size_t)REC_ROWS * 4 + (size_t)SLOT_ROWS * 16); }
+__host__ __device__ inline uint4* recover_slots(const uint32_t* rec, uint32_t n_pad) {
+  return reinterpret_cast<uint4*>(const_cast<uint32_t*>(rec) + (size_t)REC_ROWS * n_pad);
+}
 
 struct RecoverParams {
   const uint32_t* rec;
@@ -47,6 +55,9 @@ hipError_t launch_prep_ecrecover(const uint8_t* msg, const uint8_t* sig, uint32_
 hipError_t launch_prep_sender(const uint8_t* sighash, const uint8_t* r, const uint8_t* s, const uint8_t* v,
                               const uint8_t* vflags, uint32_t n, uint32_t n_pad, int signer, uint64_t chain_id,
                               uint32_t* rec, hipStream_t st);
+#ifdef EGES_PHASE_STAMPS
+hipError_t launch_recover_stamped(const RecoverParams& p, int max_blocks, hipStream_t st, uint64_t* stamps);
+#endif
 hipError_t launch_recover(const RecoverParams& p, int max_blocks, hipStream_t st);
 hipError_t launch_verify(const VerifyParams& p, int max_blocks, hipStream_t st);
 hipError_t launch_synth(const SynthParams& p, int max_blocks, hipStream_t st);

@@ -1,0 +1,59 @@
+"""Phase breakdown of the recover kernel (diagnostic build eges_amd/libeges_diag.so).
+
+Runs one 1M-signature ecrecover launch through the phase-stamped kernel and prints, per
+phase, the mean s_memtime cycles each wave spent there and the share of the total.
+Usage: python tools/phases.py [n]
+"""
+import ctypes
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from eges_amd import _lib  # noqa: E402
+
+lib = ctypes.CDLL(os.path.join(ROOT, "eges_amd", "libeges_diag.so"))
+for name, (res, args) in _lib.SIGNATURES.items():
+    f = getattr(lib, name)
+    f.restype, f.argtypes = res, args
+lib.eges_diag_read_stamps.restype = ctypes.c_size_t
+lib.eges_diag_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+
+PHASES = ["parse+sqrt", "r^-1 batch+u1/u2", "GLV+digits", "R table+affine", "Strauss", "Z^-1 batch",
+          "keccak+store", "-"]
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+assert lib.eges_init(0, 0) == 0, lib.eges_last_error()
+dev = torch.device("cuda:0")
+msg = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+sig = torch.empty(n * 65, dtype=torch.uint8, device=dev)
+exp = torch.empty(n * 20, dtype=torch.uint8, device=dev)
+addr = torch.empty(n * 20, dtype=torch.uint8, device=dev)
+status = torch.empty(n, dtype=torch.uint8, device=dev)
+torch.cuda.synchronize()
+assert lib.eges_synth_sign_dev(0, 0, n, msg.data_ptr(), sig.data_ptr(), exp.data_ptr(), None) == 0
+torch.cuda.synchronize()
+for it in range(2):
+    t0 = time.perf_counter()
+    rc = lib.eges_ecrecover_batch_dev(0, msg.data_ptr(), sig.data_ptr(), n, None, addr.data_ptr(),
+                                      status.data_ptr(), None)
+    assert rc == 0, lib.eges_last_error()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+assert bool((addr == exp).all()) and int(status.max()) == 0, "diag build disagrees with synth addresses"
+waves = lib.eges_diag_read_stamps(None, 1 << 30)
+buf = (ctypes.c_uint64 * (waves * 8))()
+lib.eges_diag_read_stamps(buf, waves)
+import numpy as np  # noqa: E402
+
+a = np.frombuffer(buf, dtype=np.uint64).reshape(waves, 8).astype(np.float64)
+tot = a.sum(axis=1)
+print(f"n={n} launch {dt * 1e3:.2f} ms ({n / dt / 1e6:.2f} M sigs/s, stamped build), waves={waves}")
+print(f"per-wave total: mean {tot.mean():.4g} min {tot.min():.4g} max {tot.max():.4g} (s_memtime ticks)")
+tiles_per_wave = n / 256 / (waves / 4)
+for i in range(7):
+    m = a[:, i].mean()
+    print(f"  {PHASES[i]:18s} {m:12.4g} ticks/wave  {100 * m / tot.mean():5.1f}%  {m / tiles_per_wave:10.4g}/tile")
