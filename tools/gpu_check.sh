@@ -1,0 +1,10 @@
+# GPU round check: parity tests, bench line, kernel-trace profile. Run via gpurun from the repo root.
+set -e
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1
+cat gpurun_out/bench.json
+tail -3 gpurun_out/pytest_gpu.log
