@@ -18,6 +18,8 @@
 
 #define DEV __device__ __forceinline__
 
+#include "modinv.cuh"
+
 namespace eges {
 
 struct fe {
@@ -314,14 +316,12 @@ DEV bool fe_sqrt(fe& r, const fe& a) {
   return fe_equal(fe_sqr(t), a);
 }
 
-// a^(p-2); p-2 = 1^223 0 1^22 0000 1 0 11 0 1 (255 sqr, 15 mul).
+// a^-1 (0 -> 0): constant-time safegcd (modinv.cuh) on the canonical value.
 DEV fe fe_inv(const fe& a) {
-  fe_chain c = fe_chain_223(a);
-  fe t = fe_mul(fe_sqr_n(c.x223, 23), c.x22);
-  t = fe_mul(fe_sqr_n(t, 5), a);
-  t = fe_mul(fe_sqr_n(t, 3), c.x2);
-  t = fe_mul(fe_sqr_n(t, 2), a);
-  return t;
+  uint32_t x[8], y[8];
+  fe_to_u256(x, fe_normalize(a));
+  modinv256<ModP>(y, x);
+  return fe_from_u256(y);
 }
 
 }  // namespace eges

@@ -259,18 +259,10 @@ DEV sc sc_from_limbs(const uint32_t x[8], bool& overflow) {
   return r;
 }
 
-// a^(n-2), MSB-first square-and-multiply. Executed by one wave per workgroup tile (the batch
-// inversion amortises it over the tile), so register economy matters more than op count.
+// a^-1 mod n (0 -> 0): constant-time safegcd (modinv.cuh).
 DEV sc sc_inv(const sc& a) {
-  // n - 2, little-endian limbs
-  const uint32_t e[8] = {0xD036413Fu, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
-                         0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  sc r = a;  // top bit of n-2 is 1
-#pragma unroll 1
-  for (int i = 254; i >= 0; --i) {
-    r = sc_sqr(r);
-    if ((e[i >> 5] >> (i & 31)) & 1u) r = sc_mul(r, a);  // wave-uniform branch
-  }
+  sc r;
+  modinv256<ModN>(r.v, a.v);
   return r;
 }
 
