@@ -235,6 +235,28 @@ DEV void add_step_zinv(gej& acc, bool& inf, const ge& p, bool use, const fe& zet
   inf = use ? (inf ? false : to_inf) : inf;
 }
 
+// Unchecked forms: an exceptional sum poisons acc (Z == 0, ge.cuh CHECK) instead of being
+// resolved; ecmult_core detects that once per signature and redoes the lane exactly.
+DEV void add_step_fast(gej& acc, bool& inf, const ge& p, bool use) {
+  gej s = gej_add_ge_fast(acc, p);
+  s = gej_select(inf, gej_from_ge(p), s);
+  acc = gej_select(use, s, acc);
+  inf = inf && !use;
+}
+DEV void add_step_zinv_fast(gej& acc, bool& inf, const ge& p, bool use, const fe& zeta) {
+  gej s = gej_add_ge_zinv_fast(acc, p, zeta);
+  if (__any(use && inf)) {
+    const fe z2 = fe_sqr(zeta);
+    gej pj;
+    pj.x = fe_mul(p.x, z2);
+    pj.y = fe_mul(p.y, fe_mul(z2, zeta));
+    pj.z = fe_one();
+    s = gej_select(inf, pj, s);
+  }
+  acc = gej_select(use, s, acc);
+  inf = inf && !use;
+}
+
 DEV ge neg_if(const ge& p, bool neg) {  // y magnitude <= 2 afterwards
   ge r;
   r.x = p.x;
@@ -292,6 +314,48 @@ struct Stamper {
   }
 };
 
+// Strauss-Shamir over the digits in L and the tables (per-lane R table at `base`, G / lambda G
+// in gtab): acc = sum of the window contributions on the R table's isomorphic curve.
+template <bool CHECKED>
+DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab, CoreLds& L) {
+  const int tid = threadIdx.x;
+  // 33 windows of 4 bits (R, lambda R) interleaved with 11 windows of
+  //     12 bits (G, lambda G) every third window.
+  inf = true;
+  acc.x = fe_zero();
+  acc.y = fe_zero();
+  acc.z = fe_zero();
+#pragma unroll 1
+  for (int w = RWIN - 1; w >= 0; --w) {
+    if (w != RWIN - 1) {
+#pragma unroll 1
+      for (int k = 0; k < 4; ++k) acc = gej_double(acc);
+    }
+    const int nadd = (w % 3) == 0 ? 4 : 2;
+#pragma unroll 1
+    for (int j = 0; j < nadd; ++j) {
+      int d;
+      if (j < 2) d = L.rdig[j][w][tid];
+      else d = L.gdig[j - 2][w / 3][tid];
+      const int a = d < 0 ? -d : d;
+      const int e = a > 0 ? a - 1 : 0;
+      ge p;
+      if (j < 2) p = load_pt(base + (size_t)(e * WG + tid) * PT_WORDS);
+      else p = load_pt(gtab + ((size_t)(j - 2) * GTAB + e) * PT_WORDS);
+      if (j == 1) p.x = fe_mul(p.x, fe_const(FE_BETA));
+      if (j < 2) {
+        if (CHECKED) add_step(acc, inf, neg_if(p, d < 0), d != 0);
+        else add_step_fast(acc, inf, neg_if(p, d < 0), d != 0);
+      } else {
+        fe z;
+        lds_get<10>(L.zeta, z.v);
+        if (CHECKED) add_step_zinv(acc, inf, neg_if(p, d < 0), d != 0, z);
+        else add_step_zinv_fast(acc, inf, neg_if(p, d < 0), d != 0, z);
+      }
+    }
+  }
+}
+
 // Q = u_r * P + u_g * G for the workgroup's 256 lanes. P given affine (a valid curve point,
 // possibly a dummy for failed lanes). Returns Jacobian Q and its infinity flag.
 template <class ST = NoStamp>
@@ -327,9 +391,8 @@ DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& 
     store_fe2(zp + (size_t)(0 * WG + tid) * PT_WORDS, T.z, T.z);  // Z_2 / Z_1 = Z_2
 #pragma unroll 1
     for (int i = 2; i < PTAB; ++i) {
-      bool hz, rz;
       fe zr;
-      T = gej_add_ge_zr(T, P, zr, hz, rz);  // i*P + P, never exceptional for i < 8 < n
+      T = gej_add_ge_zr_fast(T, P, zr);  // i*P + P, never exceptional for i < 8 < n
       store_fe2(base + (size_t)(i * WG + tid) * PT_WORDS, T.x, T.y);
       store_fe2(zp + (size_t)((i - 1) * WG + tid) * PT_WORDS, zr, zr);
     }
@@ -349,39 +412,9 @@ DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& 
     lds_put<10>(L.zeta, zeta.v);
   }
   if (st) st->mark(3);
-  // --- Strauss-Shamir: 33 windows of 4 bits (R, lambda R) interleaved with 11 windows of
-  //     12 bits (G, lambda G) every third window.
-  inf = true;
-  acc.x = fe_zero();
-  acc.y = fe_zero();
-  acc.z = fe_zero();
-#pragma unroll 1
-  for (int w = RWIN - 1; w >= 0; --w) {
-    if (w != RWIN - 1) {
-#pragma unroll 1
-      for (int k = 0; k < 4; ++k) acc = gej_double(acc);
-    }
-    const int nadd = (w % 3) == 0 ? 4 : 2;
-#pragma unroll 1
-    for (int j = 0; j < nadd; ++j) {
-      int d;
-      if (j < 2) d = L.rdig[j][w][tid];
-      else d = L.gdig[j - 2][w / 3][tid];
-      const int a = d < 0 ? -d : d;
-      const int e = a > 0 ? a - 1 : 0;
-      ge p;
-      if (j < 2) p = load_pt(base + (size_t)(e * WG + tid) * PT_WORDS);
-      else p = load_pt(gtab + ((size_t)(j - 2) * GTAB + e) * PT_WORDS);
-      if (j == 1) p.x = fe_mul(p.x, fe_const(FE_BETA));
-      if (j < 2) {
-        add_step(acc, inf, neg_if(p, d < 0), d != 0);
-      } else {
-        fe z;
-        lds_get<10>(L.zeta, z.v);
-        add_step_zinv(acc, inf, neg_if(p, d < 0), d != 0, z);
-      }
-    }
-  }
+  // --- Strauss-Shamir, unchecked; exact redo of the whole wave if any lane was poisoned
+  strauss<false>(acc, inf, base, gtab, L);
+  if (__any(!inf && fe_is_zero(acc.z))) strauss<true>(acc, inf, base, gtab, L);
   // true Jacobian Z of the accumulator
   {
     fe z;

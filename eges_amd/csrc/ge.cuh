@@ -48,8 +48,12 @@ DEV gej gej_double(const gej& a) {
 //              with global Z = bzinv (a's true Jacobian Z is a.z * bzinv); the result stays in
 //              a's coordinates (group_impl.h:463-517, gej_add_zinv_var; used at ecmult_impl.h:383). One extra mul.
 //   ADD_ZR     as ADD_PLAIN, and *zr = Z3 / Z1 = 2H (group_impl.h:414-461, the rzr output).
+//   CHECK      compute h_zero / r_zero. Without it an exceptional sum (H == 0) is not flagged
+//              but still recognisable afterwards: Z3 = 2 Z1 H == 0, and every later doubling
+//              or addition keeps Z == 0 (the accumulator is "poisoned"), so the caller can
+//              detect it once at the end and redo the lane exactly (core.cuh ecmult_core).
 enum AddMode { ADD_PLAIN, ADD_ZINV, ADD_ZR };
-template <AddMode M>
+template <AddMode M, bool CHECK = true>
 DEV gej gej_add_ge_t(const gej& a, const ge& b, const fe* bzinv, bool& h_zero, bool& r_zero, fe* zr) {
   const fe az = M == ADD_ZINV ? fe_mul(a.z, *bzinv) : a.z;           // 1
   const fe Z1Z1 = fe_sqr(az);                                        // 1
@@ -57,8 +61,10 @@ DEV gej gej_add_ge_t(const gej& a, const ge& b, const fe* bzinv, bool& h_zero, b
   const fe S2 = fe_mul(fe_mul(b.y, az), Z1Z1);                       // 1
   const fe H = fe_sub<1>(U2, a.x);                                   // 3
   const fe R = fe_normalize_weak(fe_sub<1>(S2, a.y));                // 1
-  h_zero = fe_is_zero(H);
-  r_zero = fe_is_zero(R);
+  if (CHECK) {
+    h_zero = fe_is_zero(H);
+    r_zero = fe_is_zero(R);
+  }
   const fe HH = fe_sqr(H);                                           // 1
   const fe HH2 = fe_add(HH, HH);
   const fe I = fe_add(HH2, HH2);                                     // 4 HH, 4
@@ -91,6 +97,19 @@ DEV gej gej_add_ge_zinv(const gej& a, const ge& b, const fe& bzinv, bool& h_zero
 }
 DEV gej gej_add_ge_zr(const gej& a, const ge& b, fe& zr, bool& h_zero, bool& r_zero) {
   return gej_add_ge_t<ADD_ZR>(a, b, nullptr, h_zero, r_zero, &zr);
+}
+// Unchecked forms (see CHECK above).
+DEV gej gej_add_ge_fast(const gej& a, const ge& b) {
+  bool h, r;
+  return gej_add_ge_t<ADD_PLAIN, false>(a, b, nullptr, h, r, nullptr);
+}
+DEV gej gej_add_ge_zinv_fast(const gej& a, const ge& b, const fe& bzinv) {
+  bool h, r;
+  return gej_add_ge_t<ADD_ZINV, false>(a, b, &bzinv, h, r, nullptr);
+}
+DEV gej gej_add_ge_zr_fast(const gej& a, const ge& b, fe& zr) {
+  bool h, r;
+  return gej_add_ge_t<ADD_ZR, false>(a, b, nullptr, h, r, &zr);
 }
 
 DEV gej gej_from_ge(const ge& b) {

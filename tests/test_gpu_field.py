@@ -157,3 +157,40 @@ def test_scalar_and_glv(st):
         k2 = -m2 if f & 2 else m2
         assert (k1 + k2 * LAM - x) % N == 0
         assert abs(k1) < 2**129 and abs(k2) < 2**129
+
+
+def test_ecmult_core_exceptional(st):
+    """ecmult_core (unchecked Strauss + exact redo) on scalars chosen to hit P == +-Q mid-loop
+    and an infinite result, against big-integer double-and-add."""
+    lib = st
+    lib.eges_selftest_ecmult.argtypes = [ctypes.c_uint32] + [ctypes.c_void_p] * 7
+    rnd = random.Random(16)
+    G = (GX, GY)
+    cases = [(G, 1, 1), (G, 5, N - 5), (G, 7, 7), (G, 0, 3), (G, 3, 0), (G, 0, 0), (G, N - 1, 1),
+             (ec_mul(2, G), 3, N - 6), (ec_mul(2, G), 3, 6), (ec_mul(LAM, G), 1, N - LAM),
+             (ec_mul(LAM, G), 2, 2 * LAM % N)]
+    for _ in range(8):
+        a = rnd.randrange(1, N)
+        cases.append((G, a, N - a))  # infinity
+        cases.append((G, a, a))      # acc == p in the first windows
+        k = rnd.randrange(1, N)
+        b = rnd.randrange(1, N)
+        cases.append((ec_mul(k, G), b, (N - b * k % N) % N))  # u_r*kG + u_g*G == infinity
+    while len(cases) < 300:
+        k = rnd.randrange(1, N)
+        cases.append((ec_mul(k, G), rnd.randrange(N), rnd.randrange(N)))
+    n = len(cases)
+    px, py, ur, ug = (enc([c[0][0] for c in cases]), enc([c[0][1] for c in cases]), enc([c[1] for c in cases]),
+                      enc([c[2] for c in cases]))
+    ox = np.zeros((n, 8), np.uint32)
+    oy = np.zeros((n, 8), np.uint32)
+    fl = np.zeros(n, np.uint32)
+    p = lambda x: ctypes.c_void_p(x.ctypes.data)
+    assert lib.eges_selftest_ecmult(n, p(px), p(py), p(ur), p(ug), p(ox), p(oy), p(fl)) == 0
+    xs, ys = dec(ox), dec(oy)
+    for i, (pt, a, b) in enumerate(cases):
+        exp = ec_add(ec_mul(a, pt), ec_mul(b, G))
+        if exp is None:
+            assert fl[i] == 1, i
+        else:
+            assert fl[i] == 0 and (xs[i], ys[i]) == exp, i
