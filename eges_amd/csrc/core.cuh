@@ -269,7 +269,6 @@ struct CoreLds {
   int16_t gdig[2][GWIN][WG];   // G / lambda G digits
   uint32_t inv_scratch[2 * NWAVES * 10];
   uint32_t zeta[10][WG];       // per-lane global Z of the R table
-  uint32_t park[18][WG];       // registers parked across ecmult_core by the lane-serial kernels
 };
 
 template <int N>
@@ -286,7 +285,24 @@ DEV void lds_get(uint32_t (*a)[WG], uint32_t* v) {
 // Per-block workspace (global memory, this block's lanes only):
 //   [0, PTAB*WG*PT_WORDS)              table {1..8}*P, entry-major then lane
 //   [PTAB*WG*PT_WORDS, +(PTAB-1)*...)  Z ratios Z_{i+1}/Z_i while the table is built
-constexpr size_t WS_WORDS = (size_t)(2 * PTAB - 1) * WG * PT_WORDS;
+//   [PARK_OFF, +PARK_ROWS*WG)          per-thread registers parked across ecmult_core
+constexpr int PARK_ROWS = 18;
+constexpr size_t PARK_OFF = (size_t)(2 * PTAB - 1) * WG * PT_WORDS;
+constexpr size_t WS_WORDS = PARK_OFF + (size_t)PARK_ROWS * WG;
+
+// park / unpark N words of this thread at row offset r of the block's park area
+template <int N>
+DEV void park_put(uint32_t* ws, int r, const uint32_t* v) {
+  uint32_t* a = ws + (size_t)blockIdx.x * WS_WORDS + PARK_OFF + (size_t)r * WG + threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < N; ++i) a[(size_t)i * WG] = v[i];
+}
+template <int N>
+DEV void park_get(const uint32_t* ws, int r, uint32_t* v) {
+  const uint32_t* a = ws + (size_t)blockIdx.x * WS_WORDS + PARK_OFF + (size_t)r * WG + threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = a[(size_t)i * WG];
+}
 
 DEV void store_fe2(uint32_t* dst, const fe& a, const fe& b) {
   ge p;

@@ -62,6 +62,23 @@ DEV void rec_get(const RecoverParams& prm, int row, uint32_t idx, uint32_t out[8
   for (int k = 0; k < 8; ++k) out[k] = prm.rec[(size_t)(row + k) * prm.n_pad + idx];
 }
 
+// Progress-balanced issue priority. Co-resident waves of a SIMD are otherwise arbitrated by
+// age: the older wave finishes far ahead and the younger one then runs alone at a fraction
+// of the issue rate (measured: per-wave lifetimes spread 1.8x). A wave lowers its priority
+// as it advances (units: 1 per lift, 4 per ecmult), so lagging waves catch up and the SIMD
+// keeps two waves busy to the end. p must be wave-uniform.
+DEV void balance_prio(uint32_t done, uint32_t total) {
+#ifndef EGES_NO_PRIO
+  const uint32_t q = __builtin_amdgcn_readfirstlane(total ? (4u * done) / total : 0u);
+  switch (q) {
+    case 0: __builtin_amdgcn_s_setprio(3); break;
+    case 1: __builtin_amdgcn_s_setprio(2); break;
+    case 2: __builtin_amdgcn_s_setprio(1); break;
+    default: __builtin_amdgcn_s_setprio(0); break;
+  }
+#endif
+}
+
 template <class ST>
 DEV void recover_body(const RecoverParams& prm, uint64_t* stamps) {
   __shared__ CoreLds L;
@@ -73,10 +90,12 @@ DEV void recover_body(const RecoverParams& prm, uint64_t* stamps) {
   const uint32_t g = blockIdx.x * WG + threadIdx.x;
   const uint32_t K = g < prm.n ? (prm.n - g + GT - 1) / GT : 0;  // my signatures
   uint32_t okm = 0;
+  const uint32_t units = 5u * K;
   // --- phase A: parse, lift R, prefix products of r
   sc pre = sc_one();
 #pragma unroll 1
   for (uint32_t k = 0; k < K; ++k) {
+    balance_prio(k, units);
     const uint32_t idx = k * GT + g;
     uint32_t rl[8];
     rec_get(prm, 8, idx, rl);
@@ -125,6 +144,7 @@ DEV void recover_body(const RecoverParams& prm, uint64_t* stamps) {
   fe zpre = fe_one();
 #pragma unroll 1
   for (int k = (int)K - 1; k >= 0; --k) {
+    balance_prio(K + 4u * (K - 1u - (uint32_t)k), units);
     const uint32_t idx = (uint32_t)k * GT + g;
     bool ok = (okm >> k) & 1u;
     sc rinv, u1, u2;
@@ -144,13 +164,13 @@ DEV void recover_body(const RecoverParams& prm, uint64_t* stamps) {
     }
     st->mark(1);
     const ge Rp = slot_get_pt(slot, np, 0, idx);
-    lds_put<8>(L.park, rinv_acc.v);
-    lds_put<10>(L.park + 8, zpre.v);
+    park_put<8>(prm.ws, 0, rinv_acc.v);
+    park_put<10>(prm.ws, 8, zpre.v);
     gej Q;
     bool qinf;
     ecmult_core(Q, qinf, Rp, u2, u1, prm.gtab, prm.ws, L, st);
-    lds_get<8>(L.park, rinv_acc.v);
-    lds_get<10>(L.park + 8, zpre.v);
+    park_get<8>(prm.ws, 0, rinv_acc.v);
+    park_get<10>(prm.ws, 8, zpre.v);
     ok = ok && !qinf;  // main_impl.h:120
     okm = (okm & ~(1u << k)) | ((ok ? 1u : 0u) << k);
     Q.z = fe_select(ok, Q.z, fe_one());
@@ -210,7 +230,10 @@ DEV void recover_body(const RecoverParams& prm, uint64_t* stamps) {
   }
 }
 
-__global__ void __launch_bounds__(WG, 2) recover_kernel(RecoverParams prm) { recover_body<NoStamp>(prm, nullptr); }
+#ifndef EGES_RECOVER_WAVES
+#define EGES_RECOVER_WAVES 2
+#endif
+__global__ void __launch_bounds__(WG, EGES_RECOVER_WAVES) recover_kernel(RecoverParams prm) { recover_body<NoStamp>(prm, nullptr); }
 
 #ifdef EGES_PHASE_STAMPS
 __global__ void __launch_bounds__(WG, 2) recover_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
