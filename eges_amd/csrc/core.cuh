@@ -54,7 +54,7 @@ __constant__ const uint32_t P_MINUS_N[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75FC4
 DEV fe fe_const(const uint32_t* c) { return fe_from_u256(c); }
 
 template <class T>
-constexpr int NL = sizeof(T) / sizeof(uint32_t);  // limbs of fe (10) / sc (8)
+constexpr int NL = sizeof(T) / sizeof(uint32_t);  // limbs of fe (9) / sc (8)
 DEV ge gen_point() {
   ge g;
   g.x = fe_const(GEN_X);
@@ -95,7 +95,7 @@ struct ScalarOps {
 
 // Workgroup Montgomery batch inversion: returns a^-1 for valid lanes (garbage otherwise).
 // Invalid lanes contribute 1 to the products so they cannot poison the batch.
-// lds: at least 2 * NWAVES * 10 words. Every thread of the workgroup must call this.
+// lds: at least 2 * NWAVES * 10 words (NL <= 10). Every thread of the workgroup must call this.
 template <class Ops>
 DEV typename Ops::T wg_batch_inv(const typename Ops::T& a, bool valid, uint32_t* lds) {
   using T = typename Ops::T;
@@ -172,26 +172,46 @@ DEV void recode(const glv_half& h, D* out /* [NW][WG] */) {
 }
 
 // ------------------------------------------------------------------ tables
-// Affine point record: x then y, 10 radix-2^26 limbs each (80 bytes, 16-byte aligned).
+// Affine point record: x (9 radix-2^29 limbs), y (9 limbs), 2 words of padding: 80 bytes,
+// 16-byte aligned, moved as five 16-byte accesses.
 constexpr int PT_WORDS = 20;
 
-DEV void store_pt(uint32_t* dst, const ge& p) {  // coordinates must have magnitude <= 1
+DEV void pt_pack(uint32_t w[PT_WORDS], const fe& x, const fe& y) {
+#pragma unroll
+  for (int i = 0; i < FE_LIMBS; ++i) {
+    w[i] = x.v[i];
+    w[FE_LIMBS + i] = y.v[i];
+  }
+  w[18] = 0;
+  w[19] = 0;
+}
+DEV void pt_unpack(const uint32_t w[PT_WORDS], fe& x, fe& y) {
+#pragma unroll
+  for (int i = 0; i < FE_LIMBS; ++i) {
+    x.v[i] = w[i];
+    y.v[i] = w[FE_LIMBS + i];
+  }
+}
+DEV void store_pt(uint32_t* dst, const ge& p) {
+  uint32_t w[PT_WORDS];
+  pt_pack(w, p.x, p.y);
   uint4* d = reinterpret_cast<uint4*>(dst);
-  d[0] = make_uint4(p.x.v[0], p.x.v[1], p.x.v[2], p.x.v[3]);
-  d[1] = make_uint4(p.x.v[4], p.x.v[5], p.x.v[6], p.x.v[7]);
-  d[2] = make_uint4(p.x.v[8], p.x.v[9], p.y.v[0], p.y.v[1]);
-  d[3] = make_uint4(p.y.v[2], p.y.v[3], p.y.v[4], p.y.v[5]);
-  d[4] = make_uint4(p.y.v[6], p.y.v[7], p.y.v[8], p.y.v[9]);
+#pragma unroll
+  for (int q = 0; q < 5; ++q) d[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 DEV ge load_pt(const uint32_t* src) {
   const uint4* s = reinterpret_cast<const uint4*>(src);
-  const uint4 a = s[0], b = s[1], c = s[2], d = s[3], e = s[4];
+  uint32_t w[PT_WORDS];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const uint4 u = s[q];
+    w[4 * q] = u.x;
+    w[4 * q + 1] = u.y;
+    w[4 * q + 2] = u.z;
+    w[4 * q + 3] = u.w;
+  }
   ge p;
-  p.x.v[0] = a.x; p.x.v[1] = a.y; p.x.v[2] = a.z; p.x.v[3] = a.w;
-  p.x.v[4] = b.x; p.x.v[5] = b.y; p.x.v[6] = b.z; p.x.v[7] = b.w;
-  p.x.v[8] = c.x; p.x.v[9] = c.y; p.y.v[0] = c.z; p.y.v[1] = c.w;
-  p.y.v[2] = d.x; p.y.v[3] = d.y; p.y.v[4] = d.z; p.y.v[5] = d.w;
-  p.y.v[6] = e.x; p.y.v[7] = e.y; p.y.v[8] = e.z; p.y.v[9] = e.w;
+  pt_unpack(w, p.x, p.y);
   return p;
 }
 
@@ -268,7 +288,7 @@ struct CoreLds {
   int8_t rdig[2][RWIN][WG];    // R / lambda R digits
   int16_t gdig[2][GWIN][WG];   // G / lambda G digits
   uint32_t inv_scratch[2 * NWAVES * 10];
-  uint32_t zeta[10][WG];       // per-lane global Z of the R table
+  uint32_t zeta[FE_LIMBS][WG];  // per-lane global Z of the R table
 };
 
 template <int N>
@@ -364,7 +384,7 @@ DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab
         else add_step_fast(acc, inf, neg_if(p, d < 0), d != 0);
       } else {
         fe z;
-        lds_get<10>(L.zeta, z.v);
+        lds_get<FE_LIMBS>(L.zeta, z.v);
         if (CHECKED) add_step_zinv(acc, inf, neg_if(p, d < 0), d != 0, z);
         else add_step_zinv_fast(acc, inf, neg_if(p, d < 0), d != 0, z);
       }
@@ -425,7 +445,7 @@ DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& 
       a.y = fe_mul(J.y, fe_mul(r2, rho));
       store_pt(base + (size_t)(i * WG + tid) * PT_WORDS, a);
     }
-    lds_put<10>(L.zeta, zeta.v);
+    lds_put<FE_LIMBS>(L.zeta, zeta.v);
   }
   if (st) st->mark(3);
   // --- Strauss-Shamir, unchecked; exact redo of the whole wave if any lane was poisoned
@@ -434,7 +454,7 @@ DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& 
   // true Jacobian Z of the accumulator
   {
     fe z;
-    lds_get<10>(L.zeta, z.v);
+    lds_get<FE_LIMBS>(L.zeta, z.v);
     acc.z = fe_mul(acc.z, z);
   }
   if (st) st->mark(4);

@@ -1,17 +1,20 @@
-// Field arithmetic mod p = 2^256 - 2^32 - 977 for gfx950, radix 2^26 (10 limbs).
+// Field arithmetic mod p = 2^256 - 2^32 - 977 for gfx950, radix 2^29 (9 limbs).
 //
 // Same values as libsecp256k1's field (crypto/secp256k1/libsecp256k1/src/field_10x26_impl.h,
-// field_impl.h). The radix is chosen for the MI355X VALU, not copied: every 26x26-bit partial
-// product (up to 28x28 with lazy additions) accumulates IN PLACE into a 64-bit column with one
-// v_mad_u64_u32 (4.4 cyc / wave64 instruction, tools/ubench_valu.hip) — no carry flags, no
-// zero-extension moves — and additions / subtractions are plain 32-bit v_add_u32 (2.5 cyc) on
-// limbs with headroom. A full 32-bit-limb multiply instead needs a carry op per product.
+// field_impl.h); the representation is this engine's own, chosen for the MI355X VALU: every
+// 29x29-bit partial product accumulates IN PLACE into a 64-bit column with one
+// v_mad_u64_u32 (a half-rate instruction, ~4.5 cycles per wave64 issue; tools/ubench_valu.hip)
+// — no carry flags, no zero-extension moves — and additions / subtractions are full-rate 32-bit
+// v_add_u32 / v_sub_u32 on limbs with 3 bits of headroom. 9 limbs need 81 partial products
+// per multiply (radix 2^26: 100; 32-bit limbs: 64 products but a carry op for each).
 //
-// Representation: value = sum_k v[k] * 2^(26 k), k = 0..9 (up to 2^260). "Magnitude m": every
-// limb <= m * 2^26 (+ a 2^19 slack on the outputs of mul/sqr/normalize_weak, which are
-// magnitude 1). Inputs of fe_mul / fe_sqr must have magnitude <= 4; fe_sub<M>(a, b) needs
-// magnitude(b) < 2M and returns magnitude(a) + 2M. Values are weak (congruent mod p, possibly
-// >= p) until fe_normalize().
+// Representation: value = sum_k v[k] * 2^(29 k), k = 0..8 (up to 2^261). "Magnitude m": every
+// limb <= m * (2^29 + 2^16). Outputs of fe_mul / fe_sqr / fe_normalize_weak have magnitude 1.
+// Rules (each keeps every 64-bit column below 2^64 and every limb below 2^32):
+//   fe_mul(a, b): m(a) * m(b) <= 6.5          fe_sqr(a): m(a) <= 2.5
+//   fe_sub<M>(a, b): m(b) < 2M, result m(a) + 2M, which must stay <= 7 (so M <= 3)
+//   any limb-wise sum: magnitude <= 7
+// Values are weak (congruent mod p, possibly >= p) until fe_normalize().
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -22,17 +25,18 @@
 
 namespace eges {
 
+constexpr int FE_LIMBS = 9;
+
 struct fe {
-  uint32_t v[10];
+  uint32_t v[FE_LIMBS];
 };
 
-constexpr uint32_t M26 = 0x3FFFFFFu;
-// 2^260 mod p = 2^36 + 15632  -> fold v * 2^260 as v * 15632 (same limb) + v * 2^10 (next limb)
-constexpr uint32_t FOLD0 = 15632u;
-constexpr uint32_t FOLD1 = 1024u;
-// 2^256 mod p = 2^32 + 977 = 977 + 2^6 * 2^26
+constexpr uint32_t M29 = 0x1FFFFFFFu;
+// 2^261 mod p = 2^37 + 31264: fold v * 2^261 as v * 31264 (same limb) + v * 2^8 (next limb)
+constexpr uint32_t FOLD0 = 31264u;
+// 2^256 mod p = 2^32 + 977 = 977 + 2^3 * 2^29
 constexpr uint32_t C256_0 = 977u;
-constexpr uint32_t C256_1 = 64u;
+constexpr uint32_t C256_1 = 8u;
 
 DEV uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
 
@@ -47,102 +51,101 @@ DEV uint32_t opaque_u32(uint32_t x) {
 DEV fe fe_zero() {
   fe r;
 #pragma unroll
-  for (int i = 0; i < 10; ++i) r.v[i] = 0;
+  for (int i = 0; i < FE_LIMBS; ++i) r.v[i] = 0;
   return r;
 }
 DEV fe fe_one() { fe r = fe_zero(); r.v[0] = 1; return r; }
-DEV fe fe_from_u32(uint32_t x) {  // x < 2^26 suffices for the constants used here
+DEV fe fe_from_u32(uint32_t x) {
   fe r = fe_zero();
-  r.v[0] = x & M26;
-  r.v[1] = x >> 26;
+  r.v[0] = x & M29;
+  r.v[1] = x >> 29;
   return r;
 }
 
-// 256-bit little-endian 32-bit limbs -> radix 2^26 (value unchanged, magnitude 1)
+// 256-bit little-endian 32-bit limbs -> radix 2^29 (value unchanged, magnitude 1)
 DEV fe fe_from_u256(const uint32_t x[8]) {
   fe r;
-  r.v[0] = x[0] & M26;
-  r.v[1] = ((x[0] >> 26) | (x[1] << 6)) & M26;
-  r.v[2] = ((x[1] >> 20) | (x[2] << 12)) & M26;
-  r.v[3] = ((x[2] >> 14) | (x[3] << 18)) & M26;
-  r.v[4] = ((x[3] >> 8) | (x[4] << 24)) & M26;
-  r.v[5] = (x[4] >> 2) & M26;
-  r.v[6] = ((x[4] >> 28) | (x[5] << 4)) & M26;
-  r.v[7] = ((x[5] >> 22) | (x[6] << 10)) & M26;
-  r.v[8] = ((x[6] >> 16) | (x[7] << 16)) & M26;
-  r.v[9] = x[7] >> 10;
+  r.v[0] = x[0] & M29;
+  r.v[1] = ((x[0] >> 29) | (x[1] << 3)) & M29;
+  r.v[2] = ((x[1] >> 26) | (x[2] << 6)) & M29;
+  r.v[3] = ((x[2] >> 23) | (x[3] << 9)) & M29;
+  r.v[4] = ((x[3] >> 20) | (x[4] << 12)) & M29;
+  r.v[5] = ((x[4] >> 17) | (x[5] << 15)) & M29;
+  r.v[6] = ((x[5] >> 14) | (x[6] << 18)) & M29;
+  r.v[7] = ((x[6] >> 11) | (x[7] << 21)) & M29;
+  r.v[8] = x[7] >> 8;
   return r;
 }
 
-// Canonical (fully normalised) radix-2^26 -> 256-bit 32-bit limbs.
+// Canonical (fully normalised) radix-2^29 -> 256-bit 32-bit limbs.
 DEV void fe_to_u256(uint32_t x[8], const fe& a) {
-  x[0] = a.v[0] | (a.v[1] << 26);
-  x[1] = (a.v[1] >> 6) | (a.v[2] << 20);
-  x[2] = (a.v[2] >> 12) | (a.v[3] << 14);
-  x[3] = (a.v[3] >> 18) | (a.v[4] << 8);
-  x[4] = (a.v[4] >> 24) | (a.v[5] << 2) | (a.v[6] << 28);
-  x[5] = (a.v[6] >> 4) | (a.v[7] << 22);
-  x[6] = (a.v[7] >> 10) | (a.v[8] << 16);
-  x[7] = (a.v[8] >> 16) | (a.v[9] << 10);
+  x[0] = a.v[0] | (a.v[1] << 29);
+  x[1] = (a.v[1] >> 3) | (a.v[2] << 26);
+  x[2] = (a.v[2] >> 6) | (a.v[3] << 23);
+  x[3] = (a.v[3] >> 9) | (a.v[4] << 20);
+  x[4] = (a.v[4] >> 12) | (a.v[5] << 17);
+  x[5] = (a.v[5] >> 15) | (a.v[6] << 14);
+  x[6] = (a.v[6] >> 18) | (a.v[7] << 11);
+  x[7] = (a.v[7] >> 21) | (a.v[8] << 8);
 }
 
-// ------------------------------------------------------------------ reduction of 19 columns
-// S[0..18]: column sums (each < 2^59.4). Returns magnitude-1 limbs.
-DEV fe fe_reduce_cols(uint64_t S[19]) {
-  const uint32_t f1 = opaque_u32(FOLD1), f16 = opaque_u32(1u << 16);
-  // fold columns 18..10 (descending: column 18 spills into column 10, folded afterwards).
-  // S_k 2^(26k) = (hi 2^32 + lo) 2^(26(k-10)) (2^36 + 15632)
+// ------------------------------------------------------------------ reduction of 17 columns
+// S[0..16]: column sums (each < 2^63.9). Returns magnitude-1 limbs (limb 2 carries < 2^15 slack).
+DEV fe fe_reduce_cols(uint64_t S[17]) {
+  const uint32_t f8 = opaque_u32(1u << 8), f11 = opaque_u32(1u << 11), fhi = opaque_u32(FOLD0 << 3);
+  // fold columns 16..9, descending (column 16 spills into column 9, folded afterwards).
+  // S_k 2^(29k) = (hi 2^32 + lo) 2^(29(k-9)) (2^37 + 31264)
 #pragma unroll
-  for (int k = 18; k >= 10; --k) {
+  for (int k = 16; k >= 9; --k) {
     const uint32_t lo = (uint32_t)S[k];
     const uint32_t hi = (uint32_t)(S[k] >> 32);
-    S[k - 10] = mad64(lo, FOLD0, S[k - 10]);
-    S[k - 9] = mad64(lo, f1, S[k - 9]);
-    S[k - 9] = mad64(hi, FOLD0 << 6, S[k - 9]);
-    S[k - 8] = mad64(hi, f16, S[k - 8]);
+    S[k - 9] = mad64(lo, FOLD0, S[k - 9]);
+    S[k - 8] = mad64(lo, f8, S[k - 8]);
+    S[k - 8] = mad64(hi, fhi, S[k - 8]);
+    S[k - 7] = mad64(hi, f11, S[k - 7]);
   }
   fe r;
 #pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    r.v[k] = (uint32_t)S[k] & M26;
-    S[k + 1] += S[k] >> 26;
+  for (int k = 0; k < 8; ++k) {
+    r.v[k] = (uint32_t)S[k] & M29;
+    S[k + 1] += S[k] >> 29;
   }
-  r.v[9] = (uint32_t)S[9] & M26;
-  const uint64_t c = S[9] >> 26;  // < 2^33.5: multiple of 2^260
+  r.v[8] = (uint32_t)S[8] & M29;
+  const uint64_t c = S[8] >> 29;  // < 2^35: multiple of 2^261
   const uint32_t cl = (uint32_t)c, ch = (uint32_t)(c >> 32);
-  uint64_t t0 = mad64(cl, FOLD0, r.v[0]);
-  uint64_t t1 = mad64(cl, f1, r.v[1]);
-  t1 = mad64(ch, FOLD0 << 6, t1);
-  r.v[0] = (uint32_t)t0 & M26;
-  t1 += t0 >> 26;
-  r.v[1] = (uint32_t)t1 & M26;
-  r.v[2] += (uint32_t)(t1 >> 26) + (ch << 16);
+  const uint64_t t0 = mad64(cl, FOLD0, r.v[0]);
+  uint64_t t1 = mad64(cl, f8, r.v[1]);
+  t1 = mad64(ch, fhi, t1);
+  r.v[0] = (uint32_t)t0 & M29;
+  t1 += t0 >> 29;
+  r.v[1] = (uint32_t)t1 & M29;
+  r.v[2] += (uint32_t)(t1 >> 29) + (ch << 11);
   return r;
 }
 
 DEV fe fe_mul(const fe& a, const fe& b) {
-  uint64_t S[19];
+  uint64_t S[17];
 #pragma unroll
-  for (int k = 0; k < 19; ++k) S[k] = 0;
+  for (int k = 0; k < 17; ++k) S[k] = 0;
 #pragma unroll
-  for (int i = 0; i < 10; ++i)
+  for (int i = 0; i < FE_LIMBS; ++i)
 #pragma unroll
-    for (int j = 0; j < 10; ++j) S[i + j] = mad64(a.v[i], b.v[j], S[i + j]);
+    for (int j = 0; j < FE_LIMBS; ++j) S[i + j] = mad64(a.v[i], b.v[j], S[i + j]);
   return fe_reduce_cols(S);
 }
 
 DEV fe fe_sqr(const fe& a) {
-  uint32_t d[10];
+  uint32_t d[FE_LIMBS];
 #pragma unroll
-  for (int i = 0; i < 10; ++i) d[i] = a.v[i] << 1;  // < 2^29.1 for magnitude <= 4
-  uint64_t S[19];
+  for (int i = 0; i < FE_LIMBS; ++i) d[i] = a.v[i] << 1;  // < 2^31.4 for magnitude <= 2.5
+  uint64_t S[17];
 #pragma unroll
-  for (int k = 0; k < 19; ++k) S[k] = 0;
+  for (int k = 0; k < 17; ++k) S[k] = 0;
 #pragma unroll
-  for (int i = 0; i < 10; ++i) {
+  for (int i = 0; i < FE_LIMBS; ++i) {
     S[2 * i] = mad64(a.v[i], a.v[i], S[2 * i]);
 #pragma unroll
-    for (int j = i + 1; j < 10; ++j) S[i + j] = mad64(a.v[i], d[j], S[i + j]);
+    for (int j = i + 1; j < FE_LIMBS; ++j) S[i + j] = mad64(a.v[i], d[j], S[i + j]);
   }
   return fe_reduce_cols(S);
 }
@@ -157,23 +160,21 @@ DEV fe fe_sqr_n(fe a, int n) {
 DEV fe fe_add(const fe& a, const fe& b) {
   fe r;
 #pragma unroll
-  for (int i = 0; i < 10; ++i) r.v[i] = a.v[i] + b.v[i];
+  for (int i = 0; i < FE_LIMBS; ++i) r.v[i] = a.v[i] + b.v[i];
   return r;
 }
 
-// Limbs of K1 = a multiple of p whose every limb is ~2 * 2^26.
-__constant__ const uint32_t FE_K1[10] = {0x7ff85e0u, 0x7fff7feu, 0x7fffffeu, 0x7fffffeu, 0x7fffffeu,
-                                         0x7fffffeu, 0x7fffffeu, 0x7fffffeu, 0x7fffffeu, 0x7fffffeu};
-
-// a - b for magnitude(b) < 2M; result magnitude(a) + 2M.
+// a - b for magnitude(b) < 2M; result magnitude(a) + 2M. The subtrahend constant is 64p with
+// every limb ~2^30 (= magnitude 2): limbs 2^30 - 62528, 2^30 - 514, 2^30 - 2 (x7).
 template <int M>
 DEV fe fe_sub(const fe& a, const fe& b) {
-  constexpr uint32_t k0 = 0x7ff85e0u * M, k1 = 0x7fff7feu * M, kk = 0x7fffffeu * M;
+  static_assert(M >= 1 && M <= 3, "fe_sub: M in 1..3");
+  constexpr uint32_t k0 = 0x3FFF0BC0u * M, k1 = 0x3FFFFDFEu * M, kk = 0x3FFFFFFEu * M;
   fe r;
   r.v[0] = a.v[0] + k0 - b.v[0];
   r.v[1] = a.v[1] + k1 - b.v[1];
 #pragma unroll
-  for (int i = 2; i < 10; ++i) r.v[i] = a.v[i] + kk - b.v[i];
+  for (int i = 2; i < FE_LIMBS; ++i) r.v[i] = a.v[i] + kk - b.v[i];
   return r;
 }
 
@@ -186,81 +187,80 @@ DEV fe fe_neg(const fe& a) {
 DEV fe fe_mul_small(const fe& a, uint32_t k) {
   fe r;
 #pragma unroll
-  for (int i = 0; i < 10; ++i) r.v[i] = a.v[i] * k;
+  for (int i = 0; i < FE_LIMBS; ++i) r.v[i] = a.v[i] * k;
   return r;
 }
 
-// Carry pass: any magnitude (limbs < 2^32) -> magnitude 1 (same value mod p).
+// Carry pass: any limbs < 2^32 -> magnitude 1 (same value mod p).
 DEV fe fe_normalize_weak(const fe& a) {
   fe r;
   uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 9; ++i) {
+  for (int i = 0; i < FE_LIMBS - 1; ++i) {
     const uint32_t t = a.v[i] + c;
-    r.v[i] = t & M26;
-    c = t >> 26;
+    r.v[i] = t & M29;
+    c = t >> 29;
   }
-  const uint32_t t9 = a.v[9] + c;
-  r.v[9] = t9 & M26;
-  const uint32_t h = t9 >> 26;  // multiple of 2^260, < 2^7
+  const uint32_t t8 = a.v[8] + c;
+  r.v[8] = t8 & M29;
+  const uint32_t h = t8 >> 29;  // multiple of 2^261, < 2^4
   const uint32_t u0 = r.v[0] + h * FOLD0;
-  r.v[0] = u0 & M26;
-  r.v[1] += (u0 >> 26) + h * FOLD1;
+  r.v[0] = u0 & M29;
+  r.v[1] += (u0 >> 29) + (h << 8);
   return r;
 }
 
 // Canonical representative in [0, p), any magnitude.
 DEV fe fe_normalize(const fe& a) {
-  fe r = fe_normalize_weak(a);  // < 2^260 + small
-  // fold bits >= 2^256 (limb 9 bits 22..25): h * (2^32 + 977)
-  uint32_t h = r.v[9] >> 22;
-  r.v[9] &= 0x3FFFFFu;
-  uint32_t c = h * C256_0;
-  {
-    uint32_t t = r.v[0] + c;
-    r.v[0] = t & M26;
-    t = r.v[1] + (t >> 26) + h * C256_1;
-    r.v[1] = t & M26;
-    c = t >> 26;
-#pragma unroll
-    for (int i = 2; i < 9; ++i) {
-      t = r.v[i] + c;
-      r.v[i] = t & M26;
-      c = t >> 26;
-    }
-    r.v[9] += c;  // value now < 2^256 + 2^32 (r.v[9] <= 2^22)
-  }
-  // one more fold if it reached 2^256, then the value is < 2^33: no further carries past limb 2
-  h = r.v[9] >> 22;
-  r.v[9] &= 0x3FFFFFu;
+  fe r = fe_normalize_weak(a);  // < 2^261 + small
+  // fold bits >= 2^256 (limb 8 bits 24..28): h * (2^32 + 977)
+  uint32_t h = r.v[8] >> 24;
+  r.v[8] &= 0xFFFFFFu;
   {
     uint32_t t = r.v[0] + h * C256_0;
-    r.v[0] = t & M26;
-    t = r.v[1] + (t >> 26) + h * C256_1;
-    r.v[1] = t & M26;
-    r.v[2] += t >> 26;
+    r.v[0] = t & M29;
+    t = r.v[1] + (t >> 29) + h * C256_1;
+    r.v[1] = t & M29;
+    uint32_t c = t >> 29;
+#pragma unroll
+    for (int i = 2; i < 8; ++i) {
+      t = r.v[i] + c;
+      r.v[i] = t & M29;
+      c = t >> 29;
+    }
+    r.v[8] += c;  // value now < 2^256 + 2^35 (r.v[8] <= 2^24)
+  }
+  // one more fold if it reached 2^256; then the value is < 2^36: no carry past limb 1
+  h = r.v[8] >> 24;
+  r.v[8] &= 0xFFFFFFu;
+  {
+    uint32_t t = r.v[0] + h * C256_0;
+    r.v[0] = t & M29;
+    t = r.v[1] + (t >> 29) + h * C256_1;
+    r.v[1] = t & M29;
+    r.v[2] += t >> 29;
   }
   // r < 2^256; subtract p if r >= p  <=>  r + 2^32 + 977 >= 2^256
-  uint32_t s[10];
+  uint32_t s[FE_LIMBS];
   {
     uint32_t t = r.v[0] + C256_0;
-    s[0] = t & M26;
-    t = r.v[1] + (t >> 26) + C256_1;
-    s[1] = t & M26;
-    uint32_t cc = t >> 26;
+    s[0] = t & M29;
+    t = r.v[1] + (t >> 29) + C256_1;
+    s[1] = t & M29;
+    uint32_t cc = t >> 29;
 #pragma unroll
-    for (int i = 2; i < 10; ++i) {
+    for (int i = 2; i < FE_LIMBS; ++i) {
       t = r.v[i] + cc;
-      s[i] = t & M26;
-      cc = t >> 26;
+      s[i] = t & M29;
+      cc = t >> 29;
     }
-    // s[9] bit 22 set <=> r + 2^32 + 977 >= 2^256
+    // s[8] bit 24 set <=> r + 2^32 + 977 >= 2^256
   }
-  const bool ge = (s[9] >> 22) != 0;
-  s[9] &= 0x3FFFFFu;
+  const bool ge = (s[8] >> 24) != 0;
+  s[8] &= 0xFFFFFFu;
   fe o;
 #pragma unroll
-  for (int i = 0; i < 10; ++i) o.v[i] = ge ? s[i] : r.v[i];
+  for (int i = 0; i < FE_LIMBS; ++i) o.v[i] = ge ? s[i] : r.v[i];
   return o;
 }
 
@@ -268,7 +268,7 @@ DEV bool fe_is_zero(const fe& a) {
   const fe n = fe_normalize(a);
   uint32_t o = 0;
 #pragma unroll
-  for (int i = 0; i < 10; ++i) o |= n.v[i];
+  for (int i = 0; i < FE_LIMBS; ++i) o |= n.v[i];
   return o == 0;
 }
 
@@ -279,7 +279,7 @@ DEV bool fe_is_odd(const fe& a) { return fe_normalize(a).v[0] & 1u; }
 DEV fe fe_select(bool c, const fe& a, const fe& b) {
   fe r;
 #pragma unroll
-  for (int i = 0; i < 10; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+  for (int i = 0; i < FE_LIMBS; ++i) r.v[i] = c ? a.v[i] : b.v[i];
   return r;
 }
 

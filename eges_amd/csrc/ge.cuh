@@ -2,14 +2,15 @@
 //
 // Value-level restatement of libsecp256k1's group module (src/group_impl.h: gej_double_var
 // :301-354, gej_add_ge_var :414-461, ge_set_xo_var :216-237, ge_is_valid_var :287-299).
-// Formulas: doubling dbl-2009-l (2M + 5S), mixed addition madd-2007-bl (7M + 4S);
+// Formulas: doubling dbl-2009-l (2M + 5S), mixed addition madd-2007-bl (8M + 3S here: Z3 = 2 Z1 H
+// as a product keeps magnitudes in the radix-2^29 bounds);
 // the table/accumulator "effective affine" trick follows ecmult_impl.h:52-110 (odd multiples
 // on an isomorphic curve sharing one global Z). The
 // exceptional cases libsecp256k1 handles with branches (a == infinity, a == b, a == -b) are
 // reported through flags so the kernel can resolve them with wave-uniform control flow.
 //
-// Magnitudes (fe.cuh): every coordinate at rest has magnitude 1; comments give the magnitude
-// of each intermediate; fe_mul / fe_sqr inputs stay <= 4.
+// Magnitudes (fe.cuh rules): at rest X, Y (and affine x) have magnitude 1, Z and affine y
+// (after a conditional negation) at most 2; comments give the magnitude of each intermediate.
 #pragma once
 #include "fe.cuh"
 
@@ -22,28 +23,31 @@ struct ge {
   fe x, y;
 };
 
-// Jacobian doubling. Input with Z == 0 yields Z == 0 (infinity stays infinity).
+// Jacobian doubling (dbl-2009-l, 2M + 5S). Input with Z == 0 yields Z == 0.
 DEV gej gej_double(const gej& a) {
-  const fe A = fe_sqr(a.x);                           // 1
-  const fe B = fe_sqr(a.y);                           // 1
-  const fe C = fe_sqr(B);                             // 1
-  const fe t = fe_sub<2>(fe_sqr(fe_add(a.x, B)), fe_add(A, C));  // (X+B)^2 - A - C: 1 + 4 = 5
-  const fe D = fe_normalize_weak(fe_add(t, t));       // 4 X Y^2, 1
-  const fe E = fe_add(fe_add(A, A), A);               // 3 X^2, 3
-  const fe F = fe_sqr(E);                             // 1
+  const fe A = fe_sqr(a.x);                                                   // 1
+  const fe B = fe_sqr(a.y);                                                   // 1
+  const fe C = fe_sqr(B);                                                     // 1
+  const fe D = fe_normalize_weak(fe_sub<2>(fe_sqr(fe_add(a.x, B)), fe_add(A, C)));  // ((X+B)^2-A-C), 1
+  const fe E = fe_normalize_weak(fe_add(fe_add(A, A), A));                    // 3 X^2, 1
+  const fe F = fe_sqr(E);                                                     // 1
+  const fe D2 = fe_add(D, D);                                                 // 4 X Y^2, 2
   gej r;
-  r.x = fe_normalize_weak(fe_sub<2>(F, fe_add(D, D)));               // E^2 - 2D: 1 + 4 -> 1
-  const fe m = fe_mul(E, fe_sub<1>(D, r.x));                         // in 3, 3 -> 1
-  r.y = fe_normalize_weak(fe_sub<8>(m, fe_mul_small(C, 8)));         // 1 + 16 -> 1
-  const fe yz = fe_mul(a.y, a.z);                                    // 1
-  r.z = fe_normalize_weak(fe_add(yz, yz));                           // 2 Y Z, 1
+  r.x = fe_normalize_weak(fe_sub<3>(F, fe_add(D2, D2)));                      // E^2 - 2 D2: 1 + 6 -> 1
+  const fe m = fe_mul(E, fe_sub<1>(D2, r.x));                                 // 1 x 4 -> 1
+  const fe C2 = fe_add(C, C);
+  const fe C4 = fe_add(C2, C2);                                               // 4
+  r.y = fe_normalize_weak(fe_sub<3>(fe_normalize_weak(fe_sub<3>(m, C4)), C4));  // m - 8C -> 1
+  const fe yz = fe_mul(a.y, a.z);                                             // 1 x 2 -> 1
+  r.z = fe_add(yz, yz);                                                       // 2 Y Z, 2
   return r;
 }
 
-// Mixed addition a (Jacobian, not infinity) + b (affine, x magnitude 1, y magnitude <= 2).
+// Mixed addition a (Jacobian, not infinity; Y may have magnitude 2) + b (affine, x magnitude 1,
+// y magnitude <= 2).
 // Sets h_zero when U2 == X1 (a == +-b); then r_zero tells doubling (a == b) from infinity
 // (a == -b) and the returned point is meaningless.
-//   ADD_PLAIN  b is affine in a's coordinates (madd-2007-bl, Z3 = (Z1 + H)^2 - Z1^2 - H^2).
+//   ADD_PLAIN  b is affine in a's coordinates (madd-2007-bl; Z3 = 2 Z1 H as a product).
 //   ADD_ZINV   b is affine on the true curve while a lives on the isomorphic curve of a table
 //              with global Z = bzinv (a's true Jacobian Z is a.z * bzinv); the result stays in
 //              a's coordinates (group_impl.h:463-517, gej_add_zinv_var; used at ecmult_impl.h:383). One extra mul.
@@ -55,12 +59,12 @@ DEV gej gej_double(const gej& a) {
 enum AddMode { ADD_PLAIN, ADD_ZINV, ADD_ZR };
 template <AddMode M, bool CHECK = true>
 DEV gej gej_add_ge_t(const gej& a, const ge& b, const fe* bzinv, bool& h_zero, bool& r_zero, fe* zr) {
-  const fe az = M == ADD_ZINV ? fe_mul(a.z, *bzinv) : a.z;           // 1
+  const fe az = M == ADD_ZINV ? fe_mul(a.z, *bzinv) : a.z;           // <= 2
   const fe Z1Z1 = fe_sqr(az);                                        // 1
   const fe U2 = fe_mul(b.x, Z1Z1);                                   // 1
-  const fe S2 = fe_mul(fe_mul(b.y, az), Z1Z1);                       // 1
-  const fe H = fe_sub<1>(U2, a.x);                                   // 3
-  const fe R = fe_normalize_weak(fe_sub<1>(S2, a.y));                // 1
+  const fe S2 = fe_mul(fe_mul(b.y, az), Z1Z1);                       // 2 x 2, 1 x 1 -> 1
+  const fe H = fe_normalize_weak(fe_sub<1>(U2, a.x));                // 1
+  const fe R = fe_normalize_weak(fe_sub<2>(S2, a.y));                // a.y <= 2 (fresh from affine): 5 -> 1
   if (CHECK) {
     h_zero = fe_is_zero(H);
     r_zero = fe_is_zero(R);
@@ -68,24 +72,21 @@ DEV gej gej_add_ge_t(const gej& a, const ge& b, const fe* bzinv, bool& h_zero, b
   const fe HH = fe_sqr(H);                                           // 1
   const fe HH2 = fe_add(HH, HH);
   const fe I = fe_add(HH2, HH2);                                     // 4 HH, 4
-  const fe J = fe_mul(H, I);                                         // 1
+  const fe J = fe_mul(H, I);                                         // 1 x 4 -> 1
   const fe R2 = fe_add(R, R);                                        // 2 (S2 - Y1), 2
-  const fe V = fe_mul(a.x, I);                                       // 1
+  const fe V = fe_mul(a.x, I);                                       // 1 x 4 -> 1
   gej r;
   const fe JV = fe_add(J, fe_add(V, V));                             // 3
   r.x = fe_normalize_weak(fe_sub<2>(fe_sqr(R2), JV));                // R^2 - J - 2V: 1 + 4 -> 1
   const fe YJ = fe_mul(a.y, J);                                      // 1
-  const fe m = fe_mul(R2, fe_sub<1>(V, r.x));                        // in 2, 3 -> 1
+  const fe m = fe_mul(R2, fe_sub<1>(V, r.x));                        // 2 x 3 -> 1
   r.y = fe_normalize_weak(fe_sub<2>(m, fe_add(YJ, YJ)));             // 1 + 4 -> 1
-  if (M == ADD_PLAIN) {
-    const fe zh = fe_sqr(fe_add(a.z, H));                            // in 4 -> 1
-    r.z = fe_normalize_weak(fe_sub<2>(zh, fe_add(Z1Z1, HH)));        // 2 Z1 H: 1 + 4 -> 1
-  } else if (M == ADD_ZINV) {
-    const fe zh = fe_mul(a.z, H);                                    // 1
-    r.z = fe_normalize_weak(fe_add(zh, zh));                         // 2 Z1 H
+  if (M == ADD_ZR) {
+    *zr = fe_add(H, H);                                              // 2H, 2
+    r.z = fe_mul(a.z, *zr);                                          // 2 x 2 -> 1
   } else {
-    *zr = fe_normalize_weak(fe_add(H, H));                           // 2H, 1
-    r.z = fe_mul(a.z, *zr);
+    const fe zh = fe_mul(a.z, H);                                    // 2 x 1 -> 1
+    r.z = fe_add(zh, zh);                                            // 2 Z1 H, 2
   }
   return r;
 }

@@ -18,18 +18,14 @@ namespace eges {
 // Slot rows (uint4, n_pad each): 0-4 R (affine, store_pt) then Q.x/Q.y, 5-6 prefix prod r,
 // 7-11 Q.z and prefix prod Z (store_fe2).
 DEV void slot_put_pt(uint4* slot, uint32_t n_pad, int row, uint32_t idx, const ge& p) {
-  uint32_t w[20];
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    w[i] = p.x.v[i];
-    w[10 + i] = p.y.v[i];
-  }
+  uint32_t w[PT_WORDS];
+  pt_pack(w, p.x, p.y);
 #pragma unroll
   for (int q = 0; q < 5; ++q)
     slot[(size_t)(row + q) * n_pad + idx] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 DEV ge slot_get_pt(const uint4* slot, uint32_t n_pad, int row, uint32_t idx) {
-  uint32_t w[20];
+  uint32_t w[PT_WORDS];
 #pragma unroll
   for (int q = 0; q < 5; ++q) {
     const uint4 u = slot[(size_t)(row + q) * n_pad + idx];
@@ -39,11 +35,7 @@ DEV ge slot_get_pt(const uint4* slot, uint32_t n_pad, int row, uint32_t idx) {
     w[4 * q + 3] = u.w;
   }
   ge p;
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    p.x.v[i] = w[i];
-    p.y.v[i] = w[10 + i];
-  }
+  pt_unpack(w, p.x, p.y);
   return p;
 }
 DEV void slot_put_sc(uint4* slot, uint32_t n_pad, int row, uint32_t idx, const sc& a) {
@@ -165,12 +157,12 @@ DEV void recover_body(const RecoverParams& prm, uint64_t* stamps) {
     st->mark(1);
     const ge Rp = slot_get_pt(slot, np, 0, idx);
     park_put<8>(prm.ws, 0, rinv_acc.v);
-    park_put<10>(prm.ws, 8, zpre.v);
+    park_put<FE_LIMBS>(prm.ws, 8, zpre.v);
     gej Q;
     bool qinf;
     ecmult_core(Q, qinf, Rp, u2, u1, prm.gtab, prm.ws, L, st);
     park_get<8>(prm.ws, 0, rinv_acc.v);
-    park_get<10>(prm.ws, 8, zpre.v);
+    park_get<FE_LIMBS>(prm.ws, 8, zpre.v);
     ok = ok && !qinf;  // main_impl.h:120
     okm = (okm & ~(1u << k)) | ((ok ? 1u : 0u) << k);
     Q.z = fe_select(ok, Q.z, fe_one());

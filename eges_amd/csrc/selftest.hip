@@ -15,7 +15,7 @@ enum : int {
   OP_SUB = 3,      // a - b
   OP_INV = 4,      // a^-1
   OP_SQRT = 5,     // sqrt(a) (out) and is-square flag (flag)
-  OP_LAZY = 6,     // (4a) * (a + 3b) - 2b*(a - b) with maximal lazy magnitudes
+  OP_LAZY = 6,     // (2a) * (a + 2b) - 2b*(a - b) with maximal lazy magnitudes (2 x 3)
   OP_NEG = 7,      // -a
   OP_EQZ = 8,      // flag = (a == b mod p) via fe_equal on a raw (non-reduced) input
   OP_DBL = 9,      // Jacobian doubling of affine (a, b): out affine x, out2 affine y
@@ -57,9 +57,9 @@ __global__ void selftest_kernel(int op, uint32_t n, const uint32_t* A, const uin
       break;
     }
     case OP_LAZY: {
-      const fe a4 = fe_add(fe_add(a, a), fe_add(a, a));         // 4
-      const fe t = fe_add(a, fe_add(b, fe_add(b, b)));          // 4
-      const fe u = fe_mul(a4, t);                               // 1
+      const fe a2 = fe_add(a, a);                               // 2
+      const fe t = fe_add(a, fe_add(b, b));                     // 3
+      const fe u = fe_mul(a2, t);                               // 2 x 3 -> 1
       const fe w = fe_mul(fe_add(b, b), fe_sub<1>(a, b));       // 2 x 3
       st(out, i, fe_sub<1>(u, w));
       break;
@@ -246,7 +246,7 @@ __global__ void __launch_bounds__(256, 2) opbench_kernel(uint32_t* sink, int rep
     else if constexpr (OP == 6) s1 = sc_mul(s1, s2);
     else if constexpr (OP == 7) { bool z = fe_is_zero(a); acc += z; a = fe_normalize_weak(fe_add(a, b)); }
   }
-  for (int k = 0; k < 10; ++k) acc += a.v[k] + J.x.v[k] + J.y.v[k] + J.z.v[k];
+  for (int k = 0; k < FE_LIMBS; ++k) acc += a.v[k] + J.x.v[k] + J.y.v[k] + J.z.v[k];
   for (int k = 0; k < 8; ++k) acc += s1.v[k];
   sink[blockIdx.x * 256 + threadIdx.x] = acc;
 }

@@ -55,7 +55,8 @@ def run(st, op, a, b=None, c=None, d=None):
 
 def samples(rnd, n):
     edge = [0, 1, 2, P - 1, P, P + 1, 2**256 - 1, 2**256 - 2, 2**255, 2**26 - 1, 2**52 + 5, (2**256 - 1) // 3,
-            sum(((1 << 26) - 1) << (26 * k) for k in range(10)) % 2**256]
+            sum(((1 << 26) - 1) << (26 * k) for k in range(10)) % 2**256,
+            sum(((1 << 29) - 1) << (29 * k) for k in range(9)) % 2**256]
     xs = edge + [rnd.randrange(2**256) for _ in range(n - len(edge))]
     return xs
 
@@ -75,7 +76,7 @@ def test_field_ops(st):
     out, _, _ = run(st, "NEG", a)
     assert out == [(-x) % P for x in a]
     out, _, _ = run(st, "LAZY", a, b)
-    assert out == [((4 * x) * (x + 3 * y) - 2 * y * (x - y)) % P for x, y in zip(a, b)]
+    assert out == [((2 * x) * (x + 2 * y) - 2 * y * (x - y)) % P for x, y in zip(a, b)]
 
 
 def test_field_inv_sqrt(st):
