@@ -123,30 +123,69 @@ DEV fe fe_reduce_cols(uint64_t S[17]) {
   return r;
 }
 
-DEV fe fe_mul(const fe& a, const fe& b) {
-  uint64_t S[17];
-#pragma unroll
-  for (int k = 0; k < 17; ++k) S[k] = 0;
+// Column accumulation of a * b (81 MADs) / a^2 (45 MADs) on top of preset columns.
+DEV void cols_mul(uint64_t S[17], const fe& a, const fe& b) {
 #pragma unroll
   for (int i = 0; i < FE_LIMBS; ++i)
 #pragma unroll
     for (int j = 0; j < FE_LIMBS; ++j) S[i + j] = mad64(a.v[i], b.v[j], S[i + j]);
-  return fe_reduce_cols(S);
 }
-
-DEV fe fe_sqr(const fe& a) {
+DEV void cols_sqr(uint64_t S[17], const fe& a) {
   uint32_t d[FE_LIMBS];
 #pragma unroll
   for (int i = 0; i < FE_LIMBS; ++i) d[i] = a.v[i] << 1;  // < 2^31.4 for magnitude <= 2.5
-  uint64_t S[17];
-#pragma unroll
-  for (int k = 0; k < 17; ++k) S[k] = 0;
 #pragma unroll
   for (int i = 0; i < FE_LIMBS; ++i) {
     S[2 * i] = mad64(a.v[i], a.v[i], S[2 * i]);
 #pragma unroll
     for (int j = i + 1; j < FE_LIMBS; ++j) S[i + j] = mad64(a.v[i], d[j], S[i + j]);
   }
+}
+DEV void cols_zero(uint64_t S[17]) {
+#pragma unroll
+  for (int k = 0; k < 17; ++k) S[k] = 0;
+}
+// Columns preset to 2^SH * (M * 64p - c), c of magnitude < 2M: a product minus a linear term
+// then costs 9 subtractions and shares the product's single carry pass (64p: see fe_sub).
+template <int M, int SH>
+DEV void cols_preset_sub(uint64_t S[17], const fe& c) {
+  static_assert(M >= 1 && M <= 3 && SH >= 0 && SH <= 3, "cols_preset_sub");
+  constexpr uint32_t k0 = 0x3FFF0BC0u * M, k1 = 0x3FFFFDFEu * M, kk = 0x3FFFFFFEu * M;
+  S[0] = (uint64_t)(k0 - c.v[0]) << SH;
+  S[1] = (uint64_t)(k1 - c.v[1]) << SH;
+#pragma unroll
+  for (int i = 2; i < FE_LIMBS; ++i) S[i] = (uint64_t)(kk - c.v[i]) << SH;
+#pragma unroll
+  for (int k = FE_LIMBS; k < 17; ++k) S[k] = 0;
+}
+
+DEV fe fe_mul(const fe& a, const fe& b) {
+  uint64_t S[17];
+  cols_zero(S);
+  cols_mul(S, a, b);
+  return fe_reduce_cols(S);
+}
+
+DEV fe fe_sqr(const fe& a) {
+  uint64_t S[17];
+  cols_zero(S);
+  cols_sqr(S, a);
+  return fe_reduce_cols(S);
+}
+
+// a * b - 2^SH * c and a^2 - 2^SH * c (magnitude(c) < 2M), magnitude-1 results.
+template <int M, int SH = 0>
+DEV fe fe_mul_sub(const fe& a, const fe& b, const fe& c) {
+  uint64_t S[17];
+  cols_preset_sub<M, SH>(S, c);
+  cols_mul(S, a, b);
+  return fe_reduce_cols(S);
+}
+template <int M, int SH = 0>
+DEV fe fe_sqr_sub(const fe& a, const fe& c) {
+  uint64_t S[17];
+  cols_preset_sub<M, SH>(S, c);
+  cols_sqr(S, a);
   return fe_reduce_cols(S);
 }
 

@@ -23,23 +23,20 @@ struct ge {
   fe x, y;
 };
 
-// Jacobian doubling (dbl-2009-l, 2M + 5S). Input with Z == 0 yields Z == 0.
+// Jacobian doubling (dbl-2009-l, 2M + 5S; the three "product - linear" steps fused into the
+// product's reduction, fe_mul_sub). Input with Z == 0 yields Z == 0.
 DEV gej gej_double(const gej& a) {
-  const fe A = fe_sqr(a.x);                                                   // 1
-  const fe B = fe_sqr(a.y);                                                   // 1
-  const fe C = fe_sqr(B);                                                     // 1
-  const fe D = fe_normalize_weak(fe_sub<2>(fe_sqr(fe_add(a.x, B)), fe_add(A, C)));  // ((X+B)^2-A-C), 1
-  const fe E = fe_normalize_weak(fe_add(fe_add(A, A), A));                    // 3 X^2, 1
-  const fe F = fe_sqr(E);                                                     // 1
-  const fe D2 = fe_add(D, D);                                                 // 4 X Y^2, 2
+  const fe A = fe_sqr(a.x);                                   // 1
+  const fe B = fe_sqr(a.y);                                   // 1
+  const fe C = fe_sqr(B);                                     // 1
+  const fe D = fe_sqr_sub<2>(fe_add(a.x, B), fe_add(A, C));   // (X+B)^2 - A - C = 2 X Y^2, 1
+  const fe E = fe_normalize_weak(fe_add(fe_add(A, A), A));    // 3 X^2, 1
   gej r;
-  r.x = fe_normalize_weak(fe_sub<3>(F, fe_add(D2, D2)));                      // E^2 - 2 D2: 1 + 6 -> 1
-  const fe m = fe_mul(E, fe_sub<1>(D2, r.x));                                 // 1 x 4 -> 1
-  const fe C2 = fe_add(C, C);
-  const fe C4 = fe_add(C2, C2);                                               // 4
-  r.y = fe_normalize_weak(fe_sub<3>(fe_normalize_weak(fe_sub<3>(m, C4)), C4));  // m - 8C -> 1
-  const fe yz = fe_mul(a.y, a.z);                                             // 1 x 2 -> 1
-  r.z = fe_add(yz, yz);                                                       // 2 Y Z, 2
+  r.x = fe_sqr_sub<1, 2>(E, D);                               // E^2 - 2 (2D), 1
+  const fe D2 = fe_add(D, D);                                 // 4 X Y^2, 2
+  r.y = fe_mul_sub<1, 3>(E, fe_sub<1>(D2, r.x), C);           // E (4XY^2 - X3) - 8C: 1 x 4, 1
+  const fe yz = fe_mul(a.y, a.z);                             // <= 2 x <= 2 -> 1
+  r.z = fe_add(yz, yz);                                       // 2 Y Z, 2
   return r;
 }
 
@@ -61,10 +58,8 @@ template <AddMode M, bool CHECK = true>
 DEV gej gej_add_ge_t(const gej& a, const ge& b, const fe* bzinv, bool& h_zero, bool& r_zero, fe* zr) {
   const fe az = M == ADD_ZINV ? fe_mul(a.z, *bzinv) : a.z;           // <= 2
   const fe Z1Z1 = fe_sqr(az);                                        // 1
-  const fe U2 = fe_mul(b.x, Z1Z1);                                   // 1
-  const fe S2 = fe_mul(fe_mul(b.y, az), Z1Z1);                       // 2 x 2, 1 x 1 -> 1
-  const fe H = fe_normalize_weak(fe_sub<1>(U2, a.x));                // 1
-  const fe R = fe_normalize_weak(fe_sub<2>(S2, a.y));                // a.y <= 2 (fresh from affine): 5 -> 1
+  const fe H = fe_mul_sub<1>(b.x, Z1Z1, a.x);                        // U2 - X1, 1
+  const fe R = fe_mul_sub<2>(fe_mul(b.y, az), Z1Z1, a.y);            // S2 - Y1 (a.y <= 2), 1
   if (CHECK) {
     h_zero = fe_is_zero(H);
     r_zero = fe_is_zero(R);
@@ -76,11 +71,9 @@ DEV gej gej_add_ge_t(const gej& a, const ge& b, const fe* bzinv, bool& h_zero, b
   const fe R2 = fe_add(R, R);                                        // 2 (S2 - Y1), 2
   const fe V = fe_mul(a.x, I);                                       // 1 x 4 -> 1
   gej r;
-  const fe JV = fe_add(J, fe_add(V, V));                             // 3
-  r.x = fe_normalize_weak(fe_sub<2>(fe_sqr(R2), JV));                // R^2 - J - 2V: 1 + 4 -> 1
+  r.x = fe_sqr_sub<2>(R2, fe_add(J, fe_add(V, V)));                  // R2^2 - J - 2V (3 < 4), 1
   const fe YJ = fe_mul(a.y, J);                                      // 1
-  const fe m = fe_mul(R2, fe_sub<1>(V, r.x));                        // 2 x 3 -> 1
-  r.y = fe_normalize_weak(fe_sub<2>(m, fe_add(YJ, YJ)));             // 1 + 4 -> 1
+  r.y = fe_mul_sub<1, 1>(R2, fe_sub<1>(V, r.x), YJ);                 // R2 (V - X3) - 2 Y1 J: 2 x 3, 1
   if (M == ADD_ZR) {
     *zr = fe_add(H, H);                                              // 2H, 2
     r.z = fe_mul(a.z, *zr);                                          // 2 x 2 -> 1
