@@ -19,6 +19,8 @@
 // per tile (r mod n, the R-table Z's mod p, the final Z mod p) amortise each exponentiation
 // over 256 signatures. All control flow that depends on data is either per-lane selects or
 // wave-uniform (ballot) branches for the rare exceptional additions.
+#include <type_traits>
+
 #include "fe.cuh"
 #include "sc.cuh"
 #include "ge.cuh"
@@ -30,9 +32,18 @@ namespace eges {
 constexpr int WG = 256;
 constexpr int NWAVES = WG / 64;
 constexpr int RWIN = 33;    // 4-bit signed windows over |k| < 2^129 (132 bits)
-constexpr int GWIN = 11;    // 12-bit signed windows (132 bits)
-constexpr int GTAB = 2048;  // {1..2048}*G and {1..2048}*lambda*G
+// Fixed base: u_g = lo + 2^128 hi (libsecp's split_128, ecmult_impl.h:349), signed windows of
+// GBITS bits over each 128-bit half against the tables {1..GTAB}*G and {1..GTAB}*2^128*G.
+#ifndef EGES_GBITS
+#define EGES_GBITS 20
+#endif
+constexpr int GBITS = EGES_GBITS;                 // multiple of 4: aligned with the R windows
+constexpr int GSTEP = GBITS / 4;                  // R windows per G window
+constexpr int GWIN = (RWIN + GSTEP - 1) / GSTEP;  // G windows
+constexpr int GTAB = 1 << (GBITS - 1);
 constexpr int PTAB = 8;     // {1..8}*R per lane
+static_assert(GBITS % 4 == 0 && GWIN * GBITS >= 129, "G windows must cover a 128-bit half + carry");
+using gdig_t = std::conditional_t<(GBITS > 16), int32_t, int16_t>;
 
 enum : uint32_t {
   ST_OK = 0, ST_INVALID_CHAIN_ID = 1, ST_INVALID_SIG = 2, ST_INVALID_RECOVERY_ID = 5, ST_RECOVER_FAILED = 6
@@ -44,6 +55,11 @@ __constant__ const uint32_t GEN_X[8] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0
                                         0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu};
 __constant__ const uint32_t GEN_Y[8] = {0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u,
                                         0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
+// 2^128 * G (second fixed-base table)
+__constant__ const uint32_t G128_X[8] = {0x9EC4C0DAu, 0x1B7B444Cu, 0x723EA335u, 0xE88C5678u,
+                                         0x981F162Eu, 0x9239C1ADu, 0xF63B5F33u, 0x8F68B9D2u};
+__constant__ const uint32_t G128_Y[8] = {0x501FFF82u, 0xF23CBF79u, 0x95510BFDu, 0xBBEA2CFEu,
+                                         0xB6BE215Du, 0xDE1D90C2u, 0xBA063986u, 0x662A9F2Du};
 // p, little-endian 32-bit limbs (field_10x26_impl.h set_b32 rejects >= p)
 __constant__ const uint32_t FE_P[8] = {0xFFFFFC2Fu, 0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu,
                                        0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
@@ -286,7 +302,7 @@ DEV ge neg_if(const ge& p, bool neg) {  // y magnitude <= 2 afterwards
 
 struct CoreLds {
   int8_t rdig[2][RWIN][WG];    // R / lambda R digits
-  int16_t gdig[2][GWIN][WG];   // G / lambda G digits
+  gdig_t gdig[2][GWIN][WG];    // G / 2^128 G digits
   uint32_t inv_scratch[2 * NWAVES * 10];
   uint32_t zeta[FE_LIMBS][WG];  // per-lane global Z of the R table
 };
@@ -355,8 +371,8 @@ struct Stamper {
 template <bool CHECKED>
 DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab, CoreLds& L) {
   const int tid = threadIdx.x;
-  // 33 windows of 4 bits (R, lambda R) interleaved with 11 windows of
-  //     12 bits (G, lambda G) every third window.
+  // 33 windows of 4 bits (R, lambda R) interleaved with GWIN windows of GBITS bits
+  // (G, 2^128 G) every GSTEP-th window.
   inf = true;
   acc.x = fe_zero();
   acc.y = fe_zero();
@@ -367,12 +383,12 @@ DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab
 #pragma unroll 1
       for (int k = 0; k < 4; ++k) acc = gej_double(acc);
     }
-    const int nadd = (w % 3) == 0 ? 4 : 2;
+    const int nadd = (w % GSTEP) == 0 ? 4 : 2;
 #pragma unroll 1
     for (int j = 0; j < nadd; ++j) {
       int d;
       if (j < 2) d = L.rdig[j][w][tid];
-      else d = L.gdig[j - 2][w / 3][tid];
+      else d = L.gdig[j - 2][w / GSTEP][tid];
       const int a = d < 0 ? -d : d;
       const int e = a > 0 ? a - 1 : 0;
       ge p;
@@ -406,9 +422,18 @@ DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& 
     glv_split(h1, h2, u_r);
     recode<4, RWIN, int8_t>(h1, &L.rdig[0][0][0]);
     recode<4, RWIN, int8_t>(h2, &L.rdig[1][0][0]);
-    glv_split(h1, h2, u_g);
-    recode<12, GWIN, int16_t>(h1, &L.gdig[0][0][0]);
-    recode<12, GWIN, int16_t>(h2, &L.gdig[1][0][0]);
+    glv_half g0, g1;  // u_g = lo + 2^128 hi, both non-negative
+    g0.neg = false;
+    g1.neg = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      g0.mag[i] = u_g.v[i];
+      g1.mag[i] = u_g.v[4 + i];
+    }
+    g0.mag[4] = 0;
+    g1.mag[4] = 0;
+    recode<GBITS, GWIN, gdig_t>(g0, &L.gdig[0][0][0]);
+    recode<GBITS, GWIN, gdig_t>(g1, &L.gdig[1][0][0]);
   }
   if (st) st->mark(2);
   // --- per-lane table {1..8} * P with one global Z (ecmult_impl.h:52-110): T_1 = P,

@@ -3,31 +3,31 @@
 
 namespace eges {
 
-// Fixed-base tables: gtab[t][e] = (e+1) * (t ? lambda*G : G), affine, 16 words per entry.
-// One thread per entry; simple double-and-add + Fermat inversion (runs once per device).
+// Fixed-base tables: gtab[t][e] = (e+1) * (t ? 2^128 G : G), affine, one record per entry.
+// One thread per entry; simple double-and-add + inversion (runs once per device).
 __global__ void __launch_bounds__(256) init_gtab_kernel(uint32_t* gtab) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= GTAB) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * GTAB) return;
+  const int t = i / GTAB, e = i % GTAB;
   const uint32_t k = (uint32_t)e + 1;
-  const ge g = gen_point();
+  ge g;
+  g.x = fe_const(t ? G128_X : GEN_X);
+  g.y = fe_const(t ? G128_Y : GEN_Y);
   gej acc = gej_from_ge(g);
   int top = 31 - __clz(k);
   for (int b = top - 1; b >= 0; --b) {
     acc = gej_double(acc);
     if ((k >> b) & 1u) {
       bool hz, rz;
-      acc = gej_add_ge(acc, g, hz, rz);  // m*G + G with 2 <= m < n-1: never exceptional
+      acc = gej_add_ge(acc, g, hz, rz);  // m*B + B with 2 <= m < n-1: never exceptional
     }
   }
   fe zi = fe_inv(acc.z);
   fe zi2 = fe_sqr(zi);
   ge a;
-  a.x = fe_mul(acc.x, zi2);
-  a.y = fe_mul(acc.y, fe_mul(zi2, zi));
-  store_pt(gtab + (size_t)e * PT_WORDS, a);
-  ge l = a;
-  l.x = fe_mul(a.x, fe_const(FE_BETA));
-  store_pt(gtab + ((size_t)GTAB + e) * PT_WORDS, l);
+  a.x = fe_normalize(fe_mul(acc.x, zi2));
+  a.y = fe_normalize(fe_mul(acc.y, fe_mul(zi2, zi)));
+  store_pt(gtab + (size_t)i * PT_WORDS, a);
 }
 
 // ------------------------------------------------------------------ prep kernels
@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(256) prep_sender_kernel(const uint8_t* __restr
 
 // ------------------------------------------------------------------ launchers
 hipError_t launch_init_gtab(uint32_t* gtab, hipStream_t st) {
-  hipLaunchKernelGGL(init_gtab_kernel, dim3((GTAB + 255) / 256), dim3(256), 0, st, gtab);
+  hipLaunchKernelGGL(init_gtab_kernel, dim3((2 * GTAB + 255) / 256), dim3(256), 0, st, gtab);
   return hipGetLastError();
 }
 
