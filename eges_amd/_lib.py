@@ -56,6 +56,7 @@ SIGNATURES = {
     "eges_verify_batch_dev": (_I, [_I, _P, _P, _P, _P, _SZ, _P, _P]),
     "eges_keccak256": (None, [_P, _SZ, _P]),
     "eges_synth_sign_dev": (_I, [_I, _U64, _SZ, _P, _P, _P, _P]),
+    "eges_synth_sign_msg_dev": (_I, [_I, _U64, _SZ, _P, _P, _P, _P]),
 }
 
 

@@ -522,10 +522,8 @@ int eges_verify_batch_dev(int device, const uint8_t* pub, const uint8_t* publen,
   return run_verify_dev(*d, pub, publen, msg, sig, n, ok_out, (hipStream_t)stream);
 }
 
-int eges_synth_sign_dev(int device, uint64_t first_index, size_t n, uint8_t* msg, uint8_t* sig, uint8_t* addr_expected,
-                        void* stream) {
-  if (n == 0) return EGES_SUCCESS;
-  if (!msg || !sig || !addr_expected) return set_err(EGES_E_NULLPTR, "NULL argument");
+static int synth_common(int device, uint64_t first_index, size_t n, const uint8_t* msg_in, uint8_t* msg, uint8_t* sig,
+                        uint8_t* addr_expected, void* stream) {
   int rc = ensure_init();
   if (rc) return rc;
   Dev* d = dev_by_id(device);
@@ -536,10 +534,25 @@ int eges_synth_sign_dev(int device, uint64_t first_index, size_t n, uint8_t* msg
   Serial ser(*d, st);
   for (size_t off = 0; off < n; off += CHUNK) {
     const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
-    SynthParams p{first_index + off, m, msg + off * 32, sig + off * 65, addr_expected + off * 20, d->gtab, d->ws};
+    SynthParams p{first_index + off, m, msg_in ? msg_in + off * 32 : nullptr, msg ? msg + off * 32 : nullptr,
+                  sig + off * 65, addr_expected + off * 20, d->gtab, d->ws};
     HIPCHK(launch_synth(p, d->mb_synth, st));
   }
   return EGES_SUCCESS;
+}
+
+int eges_synth_sign_dev(int device, uint64_t first_index, size_t n, uint8_t* msg, uint8_t* sig, uint8_t* addr_expected,
+                        void* stream) {
+  if (n == 0) return EGES_SUCCESS;
+  if (!msg || !sig || !addr_expected) return set_err(EGES_E_NULLPTR, "NULL argument");
+  return synth_common(device, first_index, n, nullptr, msg, sig, addr_expected, stream);
+}
+
+int eges_synth_sign_msg_dev(int device, uint64_t first_index, size_t n, const uint8_t* msg_in, uint8_t* sig,
+                            uint8_t* addr_expected, void* stream) {
+  if (n == 0) return EGES_SUCCESS;
+  if (!msg_in || !sig || !addr_expected) return set_err(EGES_E_NULLPTR, "NULL argument");
+  return synth_common(device, first_index, n, msg_in, nullptr, sig, addr_expected, stream);
 }
 
 void eges_keccak256(const uint8_t* data, size_t len, uint8_t* out32) {

@@ -38,7 +38,8 @@ __global__ void __launch_bounds__(WG, 2) synth_sign_kernel(SynthParams prm) {
     const uint64_t gi = prm.first + li;
     uint32_t kl[8], ml[8], nl[8];
     keccak_tag_index(kl, "eges-key", 8, gi);
-    keccak_tag_index(ml, "eges-msg", 8, gi);
+    if (prm.msg_in && in) limbs_from_be32(ml, prm.msg_in + (size_t)li * 32);
+    else keccak_tag_index(ml, "eges-msg", 8, gi);
     keccak_tag_index(nl, "eges-nonce", 10, gi);
     bool ov;
     sc d = sc_from_limbs(kl, ov);
@@ -72,8 +73,7 @@ __global__ void __launch_bounds__(WG, 2) synth_sign_kernel(SynthParams prm) {
       recid ^= 1u;
     }
     if (in) {
-      uint8_t* m = prm.msg + (size_t)li * 32;
-      write_be32(m, ml);
+      if (prm.msg) write_be32(prm.msg + (size_t)li * 32, ml);
       uint8_t* sg = prm.sig + (size_t)li * 65;
       write_be32(sg, r.v);
       write_be32(sg + 32, s.v);

@@ -42,7 +42,8 @@ struct VerifyParams {
 struct SynthParams {
   uint64_t first;
   uint32_t n;
-  uint8_t* msg;
+  const uint8_t* msg_in;  // nullable: sign these hashes instead of the derived messages
+  uint8_t* msg;           // nullable output
   uint8_t* sig;
   uint8_t* addr;
   const uint32_t* gtab;

@@ -117,3 +117,43 @@ def synth_sign_dev(first_index, n, device, stream=None):
     st = ctypes.c_void_p(stream) if stream is not None else _stream_of(msg)
     check(lib.eges_synth_sign_dev(dev.index, int(first_index), n, _tp(msg), _tp(sig), _tp(addr), st))
     return msg, sig, addr
+
+
+def synth_sign_msg_dev(msg, first_index=0, stream=None):
+    """Sign caller-supplied 32-byte hashes (uint8 device tensor (n,32)) with the synthetic keys of
+    indices first_index.. -> (sig (n,65), expected addr (n,20))."""
+    import torch
+    n = msg.shape[0]
+    dev = msg.device
+    sig = torch.empty((n, 65), dtype=torch.uint8, device=dev)
+    addr = torch.empty((n, 20), dtype=torch.uint8, device=dev)
+    st = ctypes.c_void_p(stream) if stream is not None else _stream_of(msg)
+    check(lib.eges_synth_sign_msg_dev(dev.index, int(first_index), n, _tp(msg), _tp(sig), _tp(addr), st))
+    return sig, addr
+
+
+def verify_batch_dev(pub, publen, msg, sig, ok=None, stream=None):
+    """crypto.VerifySignature over device tensors: pub (n,65) left-aligned, publen (n,), msg (n,32),
+    sig (n,64) -> ok (n,) uint8. Asynchronous on `stream`."""
+    import torch
+    n = msg.shape[0]
+    if ok is None:
+        ok = torch.empty((n,), dtype=torch.uint8, device=msg.device)
+    st = ctypes.c_void_p(stream) if stream is not None else _stream_of(msg)
+    check(lib.eges_verify_batch_dev(msg.device.index, _tp(pub), _tp(publen), _tp(msg), _tp(sig), n, _tp(ok), st))
+    return ok
+
+
+def sender_batch_dev(sighash, r, s, v, vflags, signer, chain_id, addr=None, status=None, stream=None):
+    """types.Sender over device tensors (n,32) x4 + vflags (n,) -> (addr (n,20), status (n,))."""
+    import torch
+    n = sighash.shape[0]
+    dev = sighash.device
+    if addr is None:
+        addr = torch.empty((n, 20), dtype=torch.uint8, device=dev)
+    if status is None:
+        status = torch.empty((n,), dtype=torch.uint8, device=dev)
+    st = ctypes.c_void_p(stream) if stream is not None else _stream_of(sighash)
+    check(lib.eges_sender_batch_dev(dev.index, _tp(sighash), _tp(r), _tp(s), _tp(v), _tp(vflags), n, int(signer),
+                                    int(chain_id), _tp(addr), _tp(status), st))
+    return addr, status

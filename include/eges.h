@@ -141,6 +141,12 @@ void eges_keccak256(const uint8_t *data, size_t len, uint8_t *out32);
 int eges_synth_sign_dev(int device, uint64_t first_index, size_t n, uint8_t *msg, uint8_t *sig,
                         uint8_t *addr_expected, void *stream);
 
+/* Same signer over caller-supplied message hashes msg_in (n*32, device): item i signs
+ * msg_in[i] with key_i and nonce_i as above (used for synthetic Geec blocks whose messages are
+ * EIP-155 sighashes). */
+int eges_synth_sign_msg_dev(int device, uint64_t first_index, size_t n, const uint8_t *msg_in, uint8_t *sig,
+                            uint8_t *addr_expected, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
