@@ -2,14 +2,24 @@
 """bench.py — secp256k1 ecrecover + Keccak address throughput on MI355X.
 
 Metric (BASELINE.json): "secp256k1 ecrecover+address/sec at 1/8 MI355X; % of INT32 VALU peak".
-Workload (BASELINE.json configs[1]): 1M random-key secp256k1 signatures, batch ecrecover +
-Keccak address on one MI355X. One step = one pass of the hot path over the per-GPU batch
-(device-resident inputs -> 20-byte addresses + status bytes). Multi-GPU: one process per GPU
-(torch.distributed.run), each rank recovers its own contiguous index shard of the synthetic
-signature stream — no data-path collective ("scaling": "weak"); a barrier brackets the timed
-region and the max time over ranks is reported.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+--config c2 (default; BASELINE.json configs[1]): 1M random-key secp256k1 signatures per GPU,
+  batch ecrecover + Keccak address. One step = one pass of the hot path over the per-GPU batch
+  (device-resident inputs -> 20-byte addresses + status bytes). Multi-GPU: one process per GPU
+  (torch.distributed.run), each rank recovers its own contiguous index shard of the synthetic
+  signature stream — no data-path collective ("scaling": "weak"); a barrier brackets the
+  timed region and the max time over ranks is reported.
+--config c4 (configs[3]): a fixed 64M-signature batch split by index across the ranks
+  (eges_amd.shard.shard_range; "scaling": "strong"); every address checked.
+--config c3 (configs[2]): Geec block import, 1000 EIP-155 transactions with a 100-byte payload
+  per block, sender recovery through the host-buffer C-ABI (H2D + kernels + D2H) -> per-block
+  latency (median, p99) next to the reference's serial per-transaction loop on one core.
+--config c5 (configs[4]): 10% invalid signatures (high-s, bad recid / chain id, r >= n, s >= n,
+  non-residue R, zero r / s) through crypto.Ecrecover and types.Sender semantics, statuses
+  checked bit-exact against their by-construction expectation, plus VerifySignature mode.
+--config verify: crypto.VerifySignature throughput (65-byte and 33-byte keys).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config c2|c3|c4|c5|verify]
 """
 import argparse
 import ctypes
@@ -21,14 +31,17 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+METRIC = "secp256k1 ecrecover+address/sec at 1/8 MI355X; % of INT32 VALU peak"
 # Algorithmic work per recovered address: INT32 lane-ops of the reference
 # algorithm = 80 x 3085.2 field ops + 128 x 301 scalar ops + 6,300 (Keccak-f) = 291,644.
 W_RECOVER = 291_644
+W_VERIFY65 = 242_216
 # INT32 VALU peak of one MI355X for the multiply/carry instruction class the kernel is made of
 # (256 CU x 64 lane-ops/clk x 2.4 GHz; tools/ubench_valu.hip measures
 # v_mad_u64_u32 / v_add_co / v_addc at 4.4-4.9 cyc per wave64 instruction per SIMD, i.e. this
 # rate; only v_add_u32/v_bitop3 issue at the 2x rate).
 PEAK_INT32_OPS = 256 * 64 * 2.4e9  # 3.93e13 lane-ops/s
+C4_TOTAL = 64 << 20
 
 
 def parse():
@@ -36,7 +49,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=1 << 20, help="signatures per GPU per step")
+    ap.add_argument("--batch", type=int, default=None, help="c2: signatures per GPU; c4: total signatures")
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "verify"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -46,7 +60,6 @@ def cpu_baseline(msg_h, sig_h, target_s):
     """Reference libsecp256k1 (compiled in place, oracle/_ref) on the host cores: the
     goroutine-parallel types.Sender/Ecrecover path restated as one pthread per core.
     Returns the cpu_baseline object or None."""
-    import numpy as np
     try:
         from oracle import Oracle, RefLib, have_ref
     except Exception:
@@ -76,112 +89,295 @@ def cpu_baseline(msg_h, sig_h, target_s):
             "sample": f"first {n} of the batch, oracle restatement, 1 thread"}
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+def read_traffic(batch):
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(tf) as f:
+            tj = json.load(f)
+        return tj.get("bytes_per_launch") if tj.get("batch") == batch else None
+    except Exception:
+        return None
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
-    torch.cuda.set_device(local)
-    import eges_amd
+
+class Ctx:
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.args = torch, dist, args
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world > 1:
+            dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
+        torch.cuda.set_device(self.local)
+        import eges_amd
+        self.eges = eges_amd
+        eges_amd.init(1 << self.local)
+        self.dev = torch.device("cuda", self.local)
+        # a dedicated stream: the engine's kernels and the timing events share it
+        self.stream = torch.cuda.Stream(self.dev)
+        self.sp = self.stream.cuda_stream
+
+    def timed(self, step):
+        """W untimed steps, then K steps between barrier + synchronize on both sides; returns
+        (max elapsed over ranks, mean per-step time from HIP events on the engine's stream)."""
+        torch, dist, a = self.torch, self.dist, self.args
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            evs[i][0].record(self.stream)
+            step()
+            evs[i][1].record(self.stream)
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        kern_ms = sum(x.elapsed_time(y) for x, y in evs) / a.steps
+        return elapsed, kern_ms
+
+    def reduce_max(self, *vals):
+        if self.world == 1:
+            return vals
+        t = self.torch.tensor(list(vals), dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return tuple(t.tolist())
+
+    def finish(self, line, ok):
+        if self.rank == 0:
+            print(json.dumps(line), flush=True)
+        if self.world > 1:
+            self.dist.destroy_process_group()
+        if not ok:
+            sys.exit(1)
+
+
+def roofline(per_gpu_rate, work, batch, kern_ms):
+    achieved = per_gpu_rate * work / 1e12
+    peak = PEAK_INT32_OPS / 1e12
+    return {"bound": "valu", "achieved": round(achieved, 3), "peak": round(peak, 2),
+            "unit": "T INT32 lane-ops/s (reference-algorithm accounting, SURVEY.md 8(d))",
+            "frac": round(achieved / peak, 4), "traffic": read_traffic(batch), "kernel_ms": round(kern_ms, 3)}
+
+
+# ------------------------------------------------------------------ c2 / c4: throughput
+def run_throughput(c, strong):
+    torch, a = c.torch, c.args
+    from eges_amd.shard import shard_range
+    if strong:
+        total = a.batch or C4_TOTAL
+        lo, hi = shard_range(total, c.rank, c.world)
+    else:
+        B0 = a.batch or (1 << 20)
+        lo, hi = c.rank * B0, (c.rank + 1) * B0
+        total = B0 * c.world
+    B = hi - lo
+    # synthetic device-resident input: this rank's contiguous index shard
+    msg, sig, exp_addr = c.eges.synth_sign_dev(lo, B, c.local)
+    addr = torch.empty((B, 20), dtype=torch.uint8, device=c.dev)
+    status = torch.empty((B,), dtype=torch.uint8, device=c.dev)
+    torch.cuda.synchronize()
     from eges_amd._lib import check, lib
 
-    eges_amd.init(1 << local)
-    dev = torch.device("cuda", local)
-    B = args.batch
-
-    # synthetic device-resident input: this rank's contiguous index shard
-    msg, sig, exp_addr = eges_amd.synth_sign_dev(rank * B, B, local)
-    addr = torch.empty((B, 20), dtype=torch.uint8, device=dev)
-    status = torch.empty((B,), dtype=torch.uint8, device=dev)
-    torch.cuda.synchronize()
-
-    # a dedicated stream: the engine's kernels and the timing events share it
-    stream = torch.cuda.Stream(dev)
-    sp = ctypes.c_void_p(stream.cuda_stream)
-
     def step():
-        check(lib.eges_ecrecover_batch_dev(local, ctypes.c_void_p(msg.data_ptr()), ctypes.c_void_p(sig.data_ptr()), B,
+        check(lib.eges_ecrecover_batch_dev(c.local, ctypes.c_void_p(msg.data_ptr()), ctypes.c_void_p(sig.data_ptr()), B,
                                            None, ctypes.c_void_p(addr.data_ptr()), ctypes.c_void_p(status.data_ptr()),
-                                           sp))
+                                           ctypes.c_void_p(c.sp)))
 
-    for _ in range(args.warmup):
-        step()
+    step()
     torch.cuda.synchronize()
     # correctness of the measured path: every address equals the signer's (by construction)
     ok = bool((status == 0).all().item()) and bool(torch.equal(addr, exp_addr))
-
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        evs[i][0].record(stream)
-        step()
-        evs[i][1].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms, bad = t.tolist()
-        ok = bad == 0.0
-
-    total_sigs = B * world * args.steps
-    value = total_sigs / elapsed
+    elapsed, kern_ms = c.timed(step)
+    elapsed, kern_ms, bad = c.reduce_max(elapsed, kern_ms, 0.0 if ok else 1.0)
+    ok = bad == 0.0
+    value = total * a.steps / elapsed
     per_gpu_rate = B / (kern_ms / 1e3)  # from HIP events on the launch stream
-    achieved = per_gpu_rate * W_RECOVER / 1e12
-    peak = PEAK_INT32_OPS / 1e12
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tf):
-        try:
-            with open(tf) as f:
-                tj = json.load(f)
-            if tj.get("batch") == B:
-                traffic = tj.get("bytes_per_launch")
-        except Exception:
-            traffic = None
+    cpu = None
+    if c.rank == 0 and not a.no_cpu_baseline and c.world == 1 and not strong:
+        cpu = cpu_baseline(msg.cpu().numpy(), sig.cpu().numpy(), a.cpu_seconds)
+    wl = ("configs[3]: 64M-signature batch sharded by index across the GPUs, batch ecrecover + Keccak address"
+          if strong else "configs[1]: 1M random-key secp256k1 signatures, batch ecrecover + Keccak address per "
+          "MI355X (inputs resident in HBM)")
+    line = {"metric": METRIC, "value": round(value, 1), "unit": "sigs/s", "n_gpus": c.world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 3), "higher_is_better": True,
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": wl, "batch_per_gpu": B, "total_batch": total,
+                       "parallelism": f"index-sharded x{c.world}", "correct": ok},
+            "roofline": roofline(per_gpu_rate, W_RECOVER, B, kern_ms), "cpu_baseline": cpu}
+    c.finish(line, ok)
 
-    if rank == 0:
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(msg.cpu().numpy(), sig.cpu().numpy(), args.cpu_seconds)
-        line = {
-            "metric": "secp256k1 ecrecover+address/sec at 1/8 MI355X; % of INT32 VALU peak",
-            "value": round(value, 1),
-            "unit": "sigs/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic",
-            "config": {"workload": "configs[1]: 1M random-key secp256k1 signatures, batch ecrecover + Keccak address "
-                                   "per MI355X (inputs resident in HBM)",
-                       "batch_per_gpu": B, "parallelism": f"index-sharded x{world}", "correct": ok},
-            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": round(peak, 2),
-                         "unit": "T INT32 lane-ops/s (reference-algorithm accounting, SURVEY.md 8(d))",
-                         "frac": round(achieved / peak, 4), "traffic": traffic,
-                         "kernel_ms": round(kern_ms, 3)},
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
-    if not ok:
-        sys.exit(1)
+
+# ------------------------------------------------------------------ c3: Geec block latency
+def run_block_latency(c):
+    import numpy as np
+    torch, a = c.torch, c.args
+    from eges_amd import txs
+    from eges_amd._lib import SIGNER_EIP155
+    n = a.batch or 1000
+    sighash = txs.geec_block(0, n, payload=100)
+    sig_d, exp_d = c.eges.synth_sign_msg_dev(torch.from_numpy(sighash).to(c.dev), 0, stream=c.sp)
+    torch.cuda.synchronize()
+    sig_h, exp_h = sig_d.cpu().numpy(), exp_d.cpu().numpy()
+    r, s, v = txs.sender_rows(sig_h, txs.GEEC_CHAIN_ID)
+    iters = max(50, a.steps * 20)
+    lat = []
+    ok = True
+    for i in range(a.warmup + iters):
+        t0 = time.perf_counter()
+        addr, st = c.eges.sender_batch(sighash, r, s, v, None, SIGNER_EIP155, txs.GEEC_CHAIN_ID)
+        dt = time.perf_counter() - t0
+        if i >= a.warmup:
+            lat.append(dt)
+        if i == 0:
+            ok = bool((st == 0).all()) and np.array_equal(addr, exp_h)
+    lat = np.array(lat) * 1e3
+    cpu = None
+    if not a.no_cpu_baseline:
+        try:
+            from oracle import RefLib, have_ref
+            if have_ref():
+                ref = RefLib()
+                t0 = time.perf_counter()
+                ref.ecrecover_batch_mt(sighash, sig_h, 1)
+                dt = time.perf_counter() - t0
+                cpu = {"value": round(dt * 1e3, 3), "unit": "ms/block", "cores": 1, "kind": "reference",
+                       "sample": f"one {n}-tx block: the reference's serial per-tx ecrecover + Keccak address "
+                                 "(types.Sender inside StateProcessor.Process, state_processor.go:73-93), 1 core; "
+                                 "sighash RLP cost excluded on both sides"}
+        except Exception:
+            cpu = None
+    line = {"metric": "Geec block sender recovery latency (1000 EIP-155 txs, 100-byte payload)",
+            "value": round(float(np.median(lat)), 3), "unit": "ms/block", "p99_ms": round(float(np.percentile(lat, 99)), 3),
+            "sigs_per_s": round(n / (np.median(lat) / 1e3), 1), "n_gpus": 1, "steps": iters, "warmup": a.warmup,
+            "higher_is_better": False, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": "configs[2]: Geec block import, 1000 txns/block (txnSize 100), EIP155Signer(930412), "
+                                   "host buffers through eges_sender_batch (H2D + kernels + D2H)",
+                       "correct": ok}, "cpu_baseline": cpu}
+    c.finish(line, ok)
+
+
+# ------------------------------------------------------------------ c5: adversarial mix
+def run_adversarial(c):
+    import numpy as np
+    torch, a = c.torch, c.args
+    from eges_amd import txs, workloads
+    from eges_amd._lib import SIGNER_EIP155
+    B = a.batch or (1 << 20)
+    msg, sig, exp_addr = c.eges.synth_sign_dev(0, B, c.local, stream=c.sp)
+    torch.cuda.synchronize()
+    sig_h = sig.cpu().numpy()
+    kind = workloads.adversarial_mix(sig_h, frac=0.10)
+    exp_e = workloads.expected_status(kind, "ecrecover")
+    exp_s = workloads.expected_status(kind, "sender")
+    r, s, v = workloads.sender_rows_mixed(sig_h, kind, txs.GEEC_CHAIN_ID)
+    sig_m = torch.from_numpy(sig_h).to(c.dev)
+    rd, sd, vd = (torch.from_numpy(x).to(c.dev) for x in (r, s, v))
+    vf = torch.zeros(B, dtype=torch.uint8, device=c.dev)
+    addr = torch.empty((B, 20), dtype=torch.uint8, device=c.dev)
+    st = torch.empty((B,), dtype=torch.uint8, device=c.dev)
+    addr2 = torch.empty((B, 20), dtype=torch.uint8, device=c.dev)
+    st2 = torch.empty((B,), dtype=torch.uint8, device=c.dev)
+
+    def step_e():
+        c.eges.ecrecover_batch_dev(msg, sig_m, addr=addr, status=st, stream=c.sp)
+
+    def step_s():
+        c.eges.sender_batch_dev(msg, rd, sd, vd, vf, SIGNER_EIP155, txs.GEEC_CHAIN_ID, addr=addr2, status=st2,
+                                stream=c.sp)
+
+    el_e, k_e = c.timed(step_e)
+    el_s, k_s = c.timed(step_s)
+    got_e, got_s = st.cpu().numpy(), st2.cpu().numpy()
+    a_e, a_s, ex = addr.cpu().numpy(), addr2.cpu().numpy(), exp_addr.cpu().numpy()
+    okm_e = got_e == 0
+    okm_s = got_s == 0
+    ok = (np.array_equal(got_e, exp_e) and np.array_equal(got_s, exp_s) and np.array_equal(a_e[okm_e], ex[okm_e])
+          and np.array_equal(a_s[okm_s], ex[okm_s]) and not a_e[~okm_e].any() and not a_s[~okm_s].any())
+    counts = {workloads.KIND_NAMES[k]: int((kind == k).sum()) for k in range(len(workloads.KIND_NAMES))}
+    line = {"metric": "adversarial-mix sender recovery, bit-exact statuses", "value": round(B * a.steps / el_s, 1),
+            "unit": "sigs/s", "ecrecover_sigs_per_s": round(B * a.steps / el_e, 1), "n_gpus": 1, "steps": a.steps,
+            "warmup": a.warmup, "higher_is_better": True, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": "configs[4]: 10% invalid (high-s, bad recid / chain id, r>=n, s>=n, non-residue R, "
+                                   "zero r/s); types.Sender (EIP155Signer 930412) and crypto.Ecrecover semantics",
+                       "batch": B, "kinds": counts, "correct": ok,
+                       "mismatches": {"ecrecover": int((got_e != exp_e).sum()), "sender": int((got_s != exp_s).sum())}}}
+    c.finish(line, ok)
+
+
+# ------------------------------------------------------------------ verify mode
+def run_verify(c):
+    import numpy as np
+    torch, a = c.torch, c.args
+    from eges_amd import workloads
+    B = a.batch or (1 << 20)
+    msg, sig, _ = c.eges.synth_sign_dev(0, B, c.local, stream=c.sp)
+    pub = torch.empty((B, 65), dtype=torch.uint8, device=c.dev)
+    c.eges.ecrecover_batch_dev(msg, sig, pub=pub, stream=c.sp)
+    torch.cuda.synchronize()
+    pub_h, sig_h = pub.cpu().numpy(), sig.cpu().numpy()[:, :64].copy()
+    n_ = B
+    publen = np.full(n_, 65, np.uint8)
+    expect = np.ones(n_, np.uint8)
+    rng = np.random.default_rng(7)
+    # a quarter compressed (02/03 || X), 10% mutated: high-s, wrong key, hybrid 06/07 prefixes
+    comp = rng.random(n_) < 0.25
+    odd = (pub_h[:, 64] & 1).astype(np.uint8)
+    pub_c = pub_h.copy()
+    pub_c[comp, 0] = 2 + odd[comp]
+    pub_c[comp, 33:] = 0
+    publen[comp] = 33
+    mut = np.nonzero(rng.random(n_) < 0.10)[0]
+    cls = rng.integers(0, 3, len(mut))
+    for i, k in zip(mut.tolist(), cls.tolist()):
+        if k == 0:  # high-s: VerifySignature always rejects (secp256k1.c:293-308)
+            s_ = int.from_bytes(sig_h[i, 32:64].tobytes(), "big")
+            sig_h[i, 32:64] = np.frombuffer((workloads.N - s_).to_bytes(32, "big"), np.uint8)
+            expect[i] = 0
+        elif k == 1:  # wrong key
+            j = (i + 1) % n_
+            pub_c[i], publen[i] = pub_h[j], 65
+            expect[i] = 0
+        else:  # hybrid encoding with the right parity is accepted (eckey_impl.h:21-29)
+            pub_c[i], publen[i] = pub_h[i], 65
+            pub_c[i, 0] = 6 + odd[i]
+    pd, ld, sd = (torch.from_numpy(x).to(c.dev) for x in (pub_c, publen, sig_h))
+    ok_d = torch.empty((B,), dtype=torch.uint8, device=c.dev)
+
+    def step():
+        c.eges.verify_batch_dev(pd, ld, msg, sd, ok=ok_d, stream=c.sp)
+
+    elapsed, kern_ms = c.timed(step)
+    got = ok_d.cpu().numpy()
+    ok = bool(np.array_equal(got, expect))
+    line = {"metric": "crypto.VerifySignature/sec on 1 MI355X", "value": round(B * a.steps / elapsed, 1),
+            "unit": "sigs/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "higher_is_better": True,
+            "dtype": "u32", "data": "synthetic",
+            "config": {"workload": "VerifySignature over 1M signatures: 75% 65-byte / 25% 33-byte keys, 10% mutated "
+                                   "(high-s, wrong key, hybrid 06/07)", "batch": B, "correct": ok,
+                       "mismatches": int((got != expect).sum())},
+            "roofline": roofline(B / (kern_ms / 1e3), W_VERIFY65, None, kern_ms)}
+    c.finish(line, ok)
+
+
+def main():
+    args = parse()
+    c = Ctx(args)
+    if args.config == "c2":
+        run_throughput(c, strong=False)
+    elif args.config == "c4":
+        run_throughput(c, strong=True)
+    elif args.config == "c3":
+        run_block_latency(c)
+    elif args.config == "c5":
+        run_adversarial(c)
+    else:
+        run_verify(c)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,90 @@
+"""GPU tests of the BASELINE configs beyond C2, at reduced sizes, through the C-ABI:
+C3 (a Geec block of EIP-155 transactions via eges_sender_batch), C5 (the adversarial mix:
+every status bit-exact against its by-construction expectation, a sample against the oracle)
+and VerifySignature mode (33/65-byte and hybrid keys, high-s, wrong key)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_geec_block_sender_batch(engine, oracle):
+    import torch
+    from eges_amd import txs
+    from eges_amd._lib import SIGNER_EIP155
+    sighash = txs.geec_block(5000, 1000, payload=100)
+    sig_d, exp_d = engine.synth_sign_msg_dev(torch.from_numpy(sighash).to("cuda:0"), 5000)
+    torch.cuda.synchronize()
+    sig, exp = sig_d.cpu().numpy(), exp_d.cpu().numpy()
+    r, s, v = txs.sender_rows(sig, txs.GEEC_CHAIN_ID)
+    addr, st = engine.sender_batch(sighash, r, s, v, None, SIGNER_EIP155, txs.GEEC_CHAIN_ID)
+    assert (st == 0).all() and np.array_equal(addr, exp)
+    for i in (0, 499, 999):
+        ost, oaddr = oracle.sender(2, txs.GEEC_CHAIN_ID, sighash[i].tobytes(), r[i].tobytes(), s[i].tobytes(),
+                                   v[i].tobytes(), 0)
+        assert ost == 0 and oaddr == exp[i].tobytes()
+
+
+def test_adversarial_mix_bit_exact(engine, oracle):
+    import torch
+    from eges_amd import txs, workloads
+    from eges_amd._lib import SIGNER_EIP155
+    n = 20000 + 13
+    msg, sig, exp = engine.synth_sign_dev(0, n, 0)
+    torch.cuda.synchronize()
+    sig_h, msg_h, exp_h = sig.cpu().numpy(), msg.cpu().numpy(), exp.cpu().numpy()
+    kind = workloads.adversarial_mix(sig_h, frac=0.10, seed=99)
+    r, s, v = workloads.sender_rows_mixed(sig_h, kind, txs.GEEC_CHAIN_ID)
+    _, addr, st = engine.ecrecover_batch_dev(msg, torch.from_numpy(sig_h).cuda())
+    a2, st2 = engine.sender_batch_dev(msg, *(torch.from_numpy(x).cuda() for x in (r, s, v)),
+                                      torch.zeros(n, dtype=torch.uint8, device="cuda"), SIGNER_EIP155,
+                                      txs.GEEC_CHAIN_ID)
+    torch.cuda.synchronize()
+    st, st2, addr, a2 = st.cpu().numpy(), st2.cpu().numpy(), addr.cpu().numpy(), a2.cpu().numpy()
+    assert np.array_equal(st, workloads.expected_status(kind, "ecrecover"))
+    assert np.array_equal(st2, workloads.expected_status(kind, "sender"))
+    assert np.array_equal(addr[st == 0], exp_h[st == 0]) and not addr[st != 0].any()
+    assert np.array_equal(a2[st2 == 0], exp_h[st2 == 0]) and not a2[st2 != 0].any()
+    # every class against the oracle on a sample
+    for k in range(len(workloads.KIND_NAMES)):
+        for i in np.nonzero(kind == k)[0][:8]:
+            ost, _ = oracle.recover_pubkey(msg_h[i].tobytes(), sig_h[i].tobytes())
+            assert ost == st[i]
+            ost2, _ = oracle.sender(2, txs.GEEC_CHAIN_ID, msg_h[i].tobytes(), r[i].tobytes(), s[i].tobytes(),
+                                    v[i].tobytes(), 0)
+            assert ost2 == st2[i]
+
+
+def test_verify_mode_mix(engine, oracle):
+    import torch
+    from eges_amd import workloads
+    n = 4096 + 5
+    msg, sig, _ = engine.synth_sign_dev(777, n, 0)
+    pub = torch.empty((n, 65), dtype=torch.uint8, device="cuda")
+    engine.ecrecover_batch_dev(msg, sig, pub=pub)
+    torch.cuda.synchronize()
+    pub_h, sig_h, msg_h = pub.cpu().numpy(), sig.cpu().numpy()[:, :64].copy(), msg.cpu().numpy()
+    publen = np.full(n, 65, np.uint8)
+    exp = np.ones(n, np.uint8)
+    odd = pub_h[:, 64] & 1
+    P = pub_h.copy()
+    for i in range(n):
+        k = i % 5
+        if k == 1:
+            P[i, 0] = 2 + odd[i]
+            P[i, 33:] = 0
+            publen[i] = 33
+        elif k == 2:
+            s_ = int.from_bytes(sig_h[i, 32:64].tobytes(), "big")
+            sig_h[i, 32:64] = np.frombuffer((workloads.N - s_).to_bytes(32, "big"), np.uint8)
+            exp[i] = 0
+        elif k == 3:
+            P[i] = pub_h[(i + 1) % n]
+            exp[i] = 0
+        elif k == 4:
+            P[i, 0] = 6 + odd[i] if i % 2 else 7 - odd[i]  # right / wrong hybrid parity
+            exp[i] = 1 if i % 2 else 0
+    ok = engine.verify_batch(P, publen, msg_h, sig_h)
+    assert np.array_equal(ok, exp)
+    for i in range(0, 50):
+        assert oracle.verify(P[i, :publen[i]].tobytes(), msg_h[i].tobytes(), sig_h[i].tobytes()) == exp[i]
