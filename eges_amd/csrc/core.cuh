@@ -5,20 +5,19 @@
 //   parse (r, s, recid) ........... recovery/main_impl.h:38-58 (overflow => failure)
 //   x = r (+ n if recid & 2) ...... main_impl.h:101-109
 //   R = lift_x(x, recid & 1) ...... group_impl.h:216-237 via (p+1)/4 sqrt, field_impl.h:38-134
-//   r^-1 mod n .................... scalar_impl.h:262-281 -> workgroup Montgomery batch inversion
+//   r^-1 mod n .................... scalar_impl.h:262-281 -> per-thread Montgomery batch inversion
 //   u1 = -z/r, u2 = s/r ........... main_impl.h:114-117 (z = msg mod n, :183)
-//   Q = u2*R + u1*G ............... ecmult_impl.h:286-404 -> GLV + Strauss, fixed 4-bit signed
-//                                   windows for R / lambda*R (per-lane 8-entry affine table) and
-//                                   12-bit signed windows for G / lambda*G (2 x 2048-entry tables)
+//   Q = u2*R + u1*G ............... ecmult_impl.h:286-404 -> GLV split of u2 + 5-bit signed
+//                                   windows for R / lambda*R (per-lane 16-entry table on one
+//                                   global Z, built with co-Z additions); u1 split at 2^128 with
+//                                   20-bit signed windows against {1..2^19}*G and *2^128*G
 //   Q == infinity => failure ...... main_impl.h:120
 //   affine (batch inversion), serialize 04||X||Y (eckey_impl.h:36-52), Keccak-256 address
 //                                   (crypto.go:194-197, transaction_signing.go:245)
 //
-// Execution model: 256-thread workgroups (4 waves), one signature per lane, persistent
-// grid-stride over 256-signature tiles. Three workgroup-level Montgomery batch inversions
-// per tile (r mod n, the R-table Z's mod p, the final Z mod p) amortise each exponentiation
-// over 256 signatures. All control flow that depends on data is either per-lane selects or
-// wave-uniform (ballot) branches for the rare exceptional additions.
+// Execution model: see k_recover.hip (lane-serial batches, one thread per signature stream).
+// All control flow that depends on data is either per-lane selects or wave-uniform (ballot)
+// branches for the rare exceptional additions.
 #include <type_traits>
 
 #include "fe.cuh"
@@ -31,18 +30,24 @@ namespace eges {
 
 constexpr int WG = 256;
 constexpr int NWAVES = WG / 64;
-constexpr int RWIN = 33;    // 4-bit signed windows over |k| < 2^129 (132 bits)
+// R / lambda R: signed windows of RBITS bits over a GLV half (|k| < 2^129, plus one bit for
+// the recoding carry) against the per-lane table {1..2^(RBITS-1)}*R.
+#ifndef EGES_RBITS
+#define EGES_RBITS 5
+#endif
+constexpr int RBITS = EGES_RBITS;
+constexpr int RWIN = (130 + RBITS - 1) / RBITS;  // 26 windows of 5 bits (33 of 4)
+constexpr int PTAB = 1 << (RBITS - 1);           // {1..16}*R per lane
 // Fixed base: u_g = lo + 2^128 hi (libsecp's split_128, ecmult_impl.h:349), signed windows of
 // GBITS bits over each 128-bit half against the tables {1..GTAB}*G and {1..GTAB}*2^128*G.
 #ifndef EGES_GBITS
 #define EGES_GBITS 20
 #endif
-constexpr int GBITS = EGES_GBITS;                 // multiple of 4: aligned with the R windows
-constexpr int GSTEP = GBITS / 4;                  // R windows per G window
+constexpr int GBITS = EGES_GBITS;                 // multiple of RBITS: aligned with the R windows
+constexpr int GSTEP = GBITS / RBITS;              // R windows per G window
 constexpr int GWIN = (RWIN + GSTEP - 1) / GSTEP;  // G windows
 constexpr int GTAB = 1 << (GBITS - 1);
-constexpr int PTAB = 8;     // {1..8}*R per lane
-static_assert(GBITS % 4 == 0 && GWIN * GBITS >= 129, "G windows must cover a 128-bit half + carry");
+static_assert(GBITS % RBITS == 0 && GWIN * GBITS >= 129, "G windows must cover a 128-bit half + carry");
 using gdig_t = std::conditional_t<(GBITS > 16), int32_t, int16_t>;
 
 enum : uint32_t {
@@ -166,7 +171,8 @@ DEV typename Ops::T wg_batch_inv(const typename Ops::T& a, bool valid, uint32_t*
 
 // ------------------------------------------------------------------ digit recoding
 // Signed fixed-window recoding of a GLV half (|k| < 2^129) into NW digits of W bits,
-// digits in [-2^(W-1), 2^(W-1)], the half's sign folded in. Written to LDS [w][WG].
+// digits in [-(2^(W-1) - 1), 2^(W-1)] (table entries 1..2^(W-1)), the half's sign folded in.
+// Written to LDS [w][WG]. NW * W >= 130 leaves no carry out of the top window.
 template <int W, int NW, class D>
 DEV void recode(const glv_half& h, D* out /* [NW][WG] */) {
   uint32_t m[5];
@@ -177,7 +183,7 @@ DEV void recode(const glv_half& h, D* out /* [NW][WG] */) {
 #pragma unroll 1
   for (int w = 0; w < NW; ++w) {
     int v = (int)(m[0] & ((1u << W) - 1)) + carry;
-    carry = v >= (1 << (W - 1)) ? 1 : 0;
+    carry = v > (1 << (W - 1)) ? 1 : 0;
     v -= carry << W;
     out[w * WG + tid] = (D)(h.neg ? -v : v);
     // m >>= W
@@ -319,11 +325,13 @@ DEV void lds_get(uint32_t (*a)[WG], uint32_t* v) {
 }
 
 // Per-block workspace (global memory, this block's lanes only):
-//   [0, PTAB*WG*PT_WORDS)              table {1..8}*P, entry-major then lane
-//   [PTAB*WG*PT_WORDS, +(PTAB-1)*...)  Z ratios Z_{i+1}/Z_i while the table is built
+//   [0, PTAB*WG*PT_WORDS)              table {1..PTAB}*P, entry-major then lane
+//   [ZR_OFF, +(PTAB-1)*WG*ZR_WORDS)    Z ratios Z_{i+1}/Z_i while the table is built
 //   [PARK_OFF, +PARK_ROWS*WG)          per-thread registers parked across ecmult_core
+constexpr int ZR_WORDS = 12;  // one field element, three 16-byte accesses
 constexpr int PARK_ROWS = 18;
-constexpr size_t PARK_OFF = (size_t)(2 * PTAB - 1) * WG * PT_WORDS;
+constexpr size_t ZR_OFF = (size_t)PTAB * WG * PT_WORDS;
+constexpr size_t PARK_OFF = ZR_OFF + (size_t)(PTAB - 1) * WG * ZR_WORDS;
 constexpr size_t WS_WORDS = PARK_OFF + (size_t)PARK_ROWS * WG;
 
 // park / unpark N words of this thread at row offset r of the block's park area
@@ -345,6 +353,21 @@ DEV void store_fe2(uint32_t* dst, const fe& a, const fe& b) {
   p.x = a;
   p.y = b;
   store_pt(dst, p);
+}
+DEV void store_fe(uint32_t* dst, const fe& a) {
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  d[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+  d[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+  d[2] = make_uint4(a.v[8], 0u, 0u, 0u);
+}
+DEV fe load_fe(const uint32_t* src) {
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  const uint4 a = s[0], b = s[1], c = s[2];
+  fe r;
+  r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+  r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+  r.v[8] = c.x;
+  return r;
 }
 
 // Diagnostic phase stamps (EGES_PHASE_STAMPS builds only): per-wave s_memtime deltas.
@@ -371,7 +394,7 @@ struct Stamper {
 template <bool CHECKED>
 DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab, CoreLds& L) {
   const int tid = threadIdx.x;
-  // 33 windows of 4 bits (R, lambda R) interleaved with GWIN windows of GBITS bits
+  // RWIN windows of RBITS bits (R, lambda R) interleaved with GWIN windows of GBITS bits
   // (G, 2^128 G) every GSTEP-th window.
   inf = true;
   acc.x = fe_zero();
@@ -381,7 +404,7 @@ DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab
   for (int w = RWIN - 1; w >= 0; --w) {
     if (w != RWIN - 1) {
 #pragma unroll 1
-      for (int k = 0; k < 4; ++k) acc = gej_double(acc);
+      for (int k = 0; k < RBITS; ++k) acc = gej_double(acc);
     }
     const int nadd = (w % GSTEP) == 0 ? 4 : 2;
 #pragma unroll 1
@@ -415,13 +438,12 @@ DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& 
                      uint32_t* ws, CoreLds& L, ST* st = nullptr) {
   const int tid = threadIdx.x;
   uint32_t* const base = ws + (size_t)blockIdx.x * WS_WORDS;
-  uint32_t* const zp = base + (size_t)PTAB * WG * PT_WORDS;
   // --- digits
   {
     glv_half h1, h2;
     glv_split(h1, h2, u_r);
-    recode<4, RWIN, int8_t>(h1, &L.rdig[0][0][0]);
-    recode<4, RWIN, int8_t>(h2, &L.rdig[1][0][0]);
+    recode<RBITS, RWIN, int8_t>(h1, &L.rdig[0][0][0]);
+    recode<RBITS, RWIN, int8_t>(h2, &L.rdig[1][0][0]);
     glv_half g0, g1;  // u_g = lo + 2^128 hi, both non-negative
     g0.neg = false;
     g1.neg = false;
@@ -436,33 +458,34 @@ DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& 
     recode<GBITS, GWIN, gdig_t>(g1, &L.gdig[1][0][0]);
   }
   if (st) st->mark(2);
-  // --- per-lane table {1..8} * P with one global Z (ecmult_impl.h:52-110): T_1 = P,
-  //     T_2 = 2P, T_{i+1} = T_i + P in Jacobian, recording the ratios Z_{i+1}/Z_i; a backward
-  //     pass rescales every T_i to Z_8 = zeta. The entries are then affine points of the
-  //     isomorphic curve y^2 = x^3 + 7 zeta^6 — no field inversion.
+  // --- per-lane table {1..PTAB} * P with one global Z (the idea of ecmult_impl.h:52-110,
+  //     built with co-Z additions): T_2 = 2P and P share Z_2 = 2y (gej_dblu); each
+  //     T_{i+1} = T_i + P is a co-Z addition that also moves P onto the new Z (gej_zaddu),
+  //     recording the ratios Z_{i+1}/Z_i. A backward pass rescales every T_i to
+  //     Z_PTAB = zeta: the entries are affine points of the isomorphic curve
+  //     y^2 = x^3 + 7 zeta^6 — no field inversion. T_i == +-P never happens for 1 < i < n.
   fe zeta;
   {
     store_pt(base + (size_t)tid * PT_WORDS, P);
-    gej T;
-    T.x = P.x;
-    T.y = P.y;
-    T.z = fe_one();
-    T = gej_double(T);
-    store_fe2(base + (size_t)(1 * WG + tid) * PT_WORDS, T.x, T.y);
-    store_fe2(zp + (size_t)(0 * WG + tid) * PT_WORDS, T.z, T.z);  // Z_2 / Z_1 = Z_2
+    gej D;
+    ge B;
+    gej_dblu(D, B, P);
+    store_fe(base + ZR_OFF + (size_t)tid * ZR_WORDS, D.z);  // Z_2 / Z_1 = 2y
+    ge T;
+    T.x = D.x;
+    T.y = D.y;
+    store_pt(base + (size_t)(1 * WG + tid) * PT_WORDS, T);
 #pragma unroll 1
     for (int i = 2; i < PTAB; ++i) {
-      fe zr;
-      T = gej_add_ge_zr_fast(T, P, zr);  // i*P + P, never exceptional for i < 8 < n
-      store_fe2(base + (size_t)(i * WG + tid) * PT_WORDS, T.x, T.y);
-      store_fe2(zp + (size_t)((i - 1) * WG + tid) * PT_WORDS, zr, zr);
+      const fe zr = gej_zaddu(T, B);  // T = (i+1) P
+      store_pt(base + (size_t)(i * WG + tid) * PT_WORDS, T);
+      store_fe(base + ZR_OFF + (size_t)((i - 1) * WG + tid) * ZR_WORDS, zr);
     }
-    zeta = T.z;
     fe rho = fe_one();
 #pragma unroll 1
     for (int i = PTAB - 2; i >= 0; --i) {
-      const fe zr = load_pt(zp + (size_t)(i * WG + tid) * PT_WORDS).x;  // Z_{i+2} / Z_{i+1}
-      rho = i == PTAB - 2 ? zr : fe_mul(rho, zr);                        // Z_8 / Z_{i+1}
+      const fe zr = load_fe(base + ZR_OFF + (size_t)(i * WG + tid) * ZR_WORDS);  // Z_{i+2} / Z_{i+1}
+      rho = i == PTAB - 2 ? zr : fe_mul(rho, zr);                                // Z_PTAB / Z_{i+1}
       const ge J = load_pt(base + (size_t)(i * WG + tid) * PT_WORDS);
       const fe r2 = fe_sqr(rho);
       ge a;
@@ -470,6 +493,7 @@ DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& 
       a.y = fe_mul(J.y, fe_mul(r2, rho));
       store_pt(base + (size_t)(i * WG + tid) * PT_WORDS, a);
     }
+    zeta = rho;  // Z_PTAB / Z_1 with Z_1 = 1
     lds_put<FE_LIMBS>(L.zeta, zeta.v);
   }
   if (st) st->mark(3);

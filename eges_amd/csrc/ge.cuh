@@ -106,6 +106,42 @@ DEV gej gej_add_ge_zr_fast(const gej& a, const ge& b, fe& zr) {
   return gej_add_ge_t<ADD_ZR, false>(a, b, nullptr, h, r, &zr);
 }
 
+// ---- co-Z table building (Meloni, "New point addition formulae for ECC applications", 2007)
+// Start from affine p: d = 2p in Jacobian with Z = 2y, and p1 = p on that same Z
+// (p1 = (x (2y)^2, y (2y)^3) = (4xy^2, 8y^4), both by-products of the doubling). 1M + 5S.
+// p.x magnitude 1, p.y magnitude 1.
+DEV void gej_dblu(gej& d, ge& p1, const ge& p) {
+  const fe A = fe_sqr(p.x);
+  const fe B = fe_sqr(p.y);
+  const fe C = fe_sqr(B);                                     // y^4
+  const fe D = fe_sqr_sub<2>(fe_add(p.x, B), fe_add(A, C));   // 2 x y^2, 1
+  const fe E = fe_normalize_weak(fe_add(fe_add(A, A), A));    // 3 x^2, 1
+  d.x = fe_sqr_sub<1, 2>(E, D);                               // E^2 - 4D, 1
+  const fe D2 = fe_add(D, D);                                 // 4 x y^2, 2
+  d.y = fe_mul_sub<1, 3>(E, fe_sub<1>(D2, d.x), C);           // 1
+  d.z = fe_add(p.y, p.y);                                     // 2y, 2
+  p1.x = fe_normalize_weak(D2);                               // 1
+  // 8 y^4 in two carry passes (8 x a magnitude-1 limb can exceed 32 bits)
+  p1.y = fe_normalize_weak(fe_mul_small(fe_normalize_weak(fe_mul_small(C, 4)), 2));  // 1
+}
+
+// Co-Z addition with update (ZADDU): b and t share one Jacobian Z (only X, Y are held).
+// t <- t + b and b <- b, both on Z' = Z (X_t - X_b); returns zr = Z' / Z. 4M + 2S.
+// Exceptional (t == +-b) is the caller's to exclude. X, Y magnitude 1 in and out.
+DEV fe gej_zaddu(ge& t, ge& b) {
+  const fe dx = fe_normalize_weak(fe_sub<1>(t.x, b.x));      // 1
+  const fe dy = fe_normalize_weak(fe_sub<1>(t.y, b.y));      // 1
+  const fe A = fe_sqr(dx);
+  const fe B = fe_mul(b.x, A);                                // X_b on Z'
+  const fe C = fe_mul(t.x, A);
+  const fe E = fe_mul(b.y, fe_sub<1>(C, B));                  // Y_b on Z': 1 x 3
+  t.x = fe_sqr_sub<2>(dy, fe_add(B, C));                      // dy^2 - B - C, 1
+  t.y = fe_mul_sub<1>(dy, fe_sub<1>(B, t.x), E);              // dy (B - X3) - E, 1
+  b.x = B;
+  b.y = E;
+  return dx;
+}
+
 DEV gej gej_from_ge(const ge& b) {
   gej r;
   r.x = b.x;
