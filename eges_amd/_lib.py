@@ -18,6 +18,7 @@ EGES_INVALID_MSG_LEN = 3
 EGES_INVALID_SIG_LEN = 4
 EGES_INVALID_RECOVERY_ID = 5
 EGES_RECOVER_FAILED = 6
+EGES_DECODE_FAILED = 7
 
 EGES_SUCCESS = 0
 EGES_E_NULLPTR = -1
@@ -50,9 +51,11 @@ SIGNATURES = {
     "eges_ecdsa_verify": (_I, [_P, _P, _P, _SZ]),
     "eges_ecrecover_batch": (_I, [_P, _P, _SZ, _P, _P, _P]),
     "eges_sender_batch": (_I, [_P, _P, _P, _P, _P, _SZ, _I, _U64, _P, _P]),
+    "eges_sender_raw_batch": (_I, [_P, _P, _SZ, _I, _U64, _P, _P, _P]),
     "eges_verify_batch": (_I, [_P, _P, _P, _P, _SZ, _P]),
     "eges_ecrecover_batch_dev": (_I, [_I, _P, _P, _SZ, _P, _P, _P, _P]),
     "eges_sender_batch_dev": (_I, [_I, _P, _P, _P, _P, _P, _SZ, _I, _U64, _P, _P, _P]),
+    "eges_sender_raw_batch_dev": (_I, [_I, _P, _P, _SZ, _I, _U64, _P, _P, _P, _P]),
     "eges_verify_batch_dev": (_I, [_I, _P, _P, _P, _P, _SZ, _P, _P]),
     "eges_keccak256": (None, [_P, _SZ, _P]),
     "eges_synth_sign_dev": (_I, [_I, _U64, _SZ, _P, _P, _P, _P]),

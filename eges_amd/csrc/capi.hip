@@ -193,6 +193,35 @@ int run_sender_dev(Dev& d, const uint8_t* sighash, const uint8_t* r, const uint8
   return EGES_SUCCESS;
 }
 
+// Wire-format transactions: tx_rows_kernel (decode + sighash) writes the sender rows into device
+// scratch after the recovery records; then the sender pipeline runs unchanged.
+inline size_t tx_rows_bytes(size_t m) { return align_up(m * (4 * 32 + 1), 256); }
+
+int run_sender_raw_dev(Dev& d, const uint8_t* raw, const uint64_t* offsets, size_t n, int signer, uint64_t chain_id,
+                       uint8_t* addr, uint8_t* status, uint8_t* sighash_out, hipStream_t st) {
+  const size_t c = std::min(n, CHUNK);
+  const size_t n_pad = align_up(c, 64);
+  const size_t o_rows = align_up(recover_scratch_bytes(n_pad), 256);
+  int rc = dev_ensure_buf(d, o_rows + tx_rows_bytes(c));
+  if (rc) return rc;
+  uint32_t* rec = reinterpret_cast<uint32_t*>(d.buf);
+  uint8_t* rows = d.buf + o_rows;
+  Serial ser(d, st);
+  for (size_t off = 0; off < n; off += CHUNK) {
+    const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
+    uint8_t* hs = sighash_out ? sighash_out + off * 32 : rows;
+    uint8_t* rr = rows + (size_t)m * 32;
+    uint8_t* sr = rr + (size_t)m * 32;
+    uint8_t* vr = sr + (size_t)m * 32;
+    uint8_t* vf = vr + (size_t)m * 32;
+    HIPCHK(launch_tx_rows(raw, offsets, off, m, signer, chain_id, hs, rr, sr, vr, vf, st));
+    HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, m, (uint32_t)n_pad, signer, chain_id, rec, st));
+    RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr + off * 20, nullptr, d.gtab, d.ws};
+    HIPCHK(launch_recover(p, d.mb_recover, st));
+  }
+  return EGES_SUCCESS;
+}
+
 int run_verify_dev(Dev& d, const uint8_t* pub, const uint8_t* publen, const uint8_t* msg, const uint8_t* sig, size_t n,
                    uint8_t* ok, hipStream_t st) {
   Serial ser(d, st);
@@ -207,7 +236,9 @@ int run_verify_dev(Dev& d, const uint8_t* pub, const uint8_t* publen, const uint
 // ------------------------------------------------------------------ host-buffer pipelines
 // Copies the inputs of [off, off+cnt) to device scratch, runs, copies outputs back. Synchronous.
 struct HostJob {
-  enum Kind { RECOVER, SENDER, VERIFY } kind;
+  enum Kind { RECOVER, SENDER, VERIFY, SENDER_RAW } kind;
+  const uint64_t* offsets = nullptr;  // SENDER_RAW: n + 1 entries
+  uint8_t* sighash = nullptr;         // SENDER_RAW: optional output
   // inputs
   const uint8_t *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr, *e = nullptr;
   int signer = 0;
@@ -224,10 +255,16 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
     const size_t m_pad = align_up(m, 64);
     // layout: inputs | rec | outputs
     size_t in_bytes = 0;
+    size_t raw_lo = 0, raw_len = 0;
     switch (j.kind) {
       case HostJob::RECOVER: in_bytes = m * (32 + 65); break;
       case HostJob::SENDER: in_bytes = m * (32 * 4 + 1); break;
       case HostJob::VERIFY: in_bytes = m * (65 + 1 + 32 + 64); break;
+      case HostJob::SENDER_RAW:
+        raw_lo = j.offsets[base] - j.offsets[0];
+        raw_len = j.offsets[base + m] - j.offsets[base];
+        in_bytes = align_up(raw_len, 8) + 8 * (m + 1) + tx_rows_bytes(m);
+        break;
     }
     const size_t rec_bytes = (j.kind == HostJob::VERIFY) ? 0 : recover_scratch_bytes(m_pad);
     const size_t out_bytes = m * (65 + 20 + 1);
@@ -266,6 +303,22 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
                                 rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
       HIPCHK(launch_recover(p, d.mb_recover, st));
+    } else if (j.kind == HostJob::SENDER_RAW) {
+      uint8_t* draw = B + o_in;
+      uint64_t* doff = reinterpret_cast<uint64_t*>(draw + align_up(raw_len, 8));
+      uint8_t* hs = reinterpret_cast<uint8_t*>(doff + (m + 1));
+      uint8_t* rr = hs + m * 32;
+      uint8_t* sr = rr + m * 32;
+      uint8_t* vr = sr + m * 32;
+      uint8_t* vf = vr + m * 32;
+      if (raw_len) HIPCHK(hipMemcpyAsync(draw, j.a + raw_lo, raw_len, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(doff, j.offsets + base, 8 * (m + 1), hipMemcpyHostToDevice, st));
+      HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, vf, st));
+      uint32_t* rec = reinterpret_cast<uint32_t*>(B + o_rec);
+      HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, st));
+      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
+      HIPCHK(launch_recover(p, d.mb_recover, st));
+      if (j.sighash) HIPCHK(hipMemcpyAsync(j.sighash + base * 32, hs, m * 32, hipMemcpyDeviceToHost, st));
     } else {
       uint8_t* dp = B + o_in;
       uint8_t* dl = dp + m * 65;
@@ -444,6 +497,26 @@ int eges_sender_batch(const uint8_t* sighash, const uint8_t* r, const uint8_t* s
   return run_host(j, n);
 }
 
+int eges_sender_raw_batch(const uint8_t* raw, const uint64_t* offsets, size_t n, int signer, uint64_t chain_id,
+                          uint8_t* addr_out, uint8_t* status, uint8_t* sighash_out) {
+  if (n == 0) return EGES_SUCCESS;
+  if (!offsets || !addr_out || !status) return set_err(EGES_E_NULLPTR, "NULL argument");
+  if (signer < 0 || signer > 2) return set_err(EGES_E_INVALID_ARG, "bad signer %d", signer);
+  for (size_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i]) return set_err(EGES_E_INVALID_ARG, "offsets decrease at %zu", i);
+  if (!raw && offsets[n] != offsets[0]) return set_err(EGES_E_NULLPTR, "raw is NULL");
+  HostJob j;
+  j.kind = HostJob::SENDER_RAW;
+  j.a = raw;
+  j.offsets = offsets;
+  j.signer = signer;
+  j.chain_id = chain_id;
+  j.addr = addr_out;
+  j.status = status;
+  j.sighash = sighash_out;
+  return run_host(j, n);
+}
+
 int eges_verify_batch(const uint8_t* pub, const uint8_t* publen, const uint8_t* msg, const uint8_t* sig, size_t n,
                       uint8_t* ok_out) {
   if (n == 0) return EGES_SUCCESS;
@@ -507,6 +580,22 @@ int eges_sender_batch_dev(int device, const uint8_t* sighash, const uint8_t* r, 
   DevGuard g(device);
   return run_sender_dev(*d, sighash, r, s, v, vflags, n, signer, chain_id, addr_out, status,
                         (hipStream_t)stream);
+}
+
+int eges_sender_raw_batch_dev(int device, const uint8_t* raw, const uint64_t* offsets, size_t n, int signer,
+                              uint64_t chain_id, uint8_t* addr_out, uint8_t* status, uint8_t* sighash_out,
+                              void* stream) {
+  if (n == 0) return EGES_SUCCESS;
+  if (!raw || !offsets || !addr_out || !status) return set_err(EGES_E_NULLPTR, "NULL argument");
+  if (signer < 0 || signer > 2) return set_err(EGES_E_INVALID_ARG, "bad signer %d", signer);
+  int rc = ensure_init();
+  if (rc) return rc;
+  Dev* d = dev_by_id(device);
+  if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
+  std::lock_guard<std::mutex> lk(d->mu);
+  DevGuard g(device);
+  return run_sender_raw_dev(*d, raw, offsets, n, signer, chain_id, addr_out, status, sighash_out,
+                            (hipStream_t)stream);
 }
 
 int eges_verify_batch_dev(int device, const uint8_t* pub, const uint8_t* publen, const uint8_t* msg, const uint8_t* sig,

@@ -81,14 +81,15 @@ __global__ void __launch_bounds__(256) prep_sender_kernel(const uint8_t* __restr
   limbs_from_be32(v, vb + (size_t)i * 32);
   const uint32_t f = vflags ? vflags[i] : 0u;
   const bool v_wide = f & 1u, r_wide = f & 2u, s_wide = f & 4u;
-  uint32_t status = ST_OK;
+  // wire-format batches (k_txhash.hip): rlp.DecodeBytes failed, the tx never reaches Sender
+  uint32_t status = (f & VF_DECODE_ERR) ? ST_DECODE_FAILED : ST_OK;
   bool homestead = signer != 0;
   // Vb: the V handed to recoverPlain
   uint32_t vb8[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) vb8[k] = v[k];
   bool vb_wide = v_wide;
-  if (signer == 2) {
+  if (signer == 2 && status == ST_OK) {
     const int bl = v_wide ? 1000 : bitlen_limbs(v);
     const bool prot = bl <= 8 ? !(v[0] == 27u || v[0] == 28u) : true;
     if (prot) {

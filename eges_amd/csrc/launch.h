@@ -9,6 +9,9 @@ namespace eges {
 // Record layout produced by the prep kernels: 25 SoA rows of n_pad words
 // (z[8], r[8], s[8], meta) — see kernels.hip.
 constexpr int REC_ROWS = 25;
+// vflags bit set by tx_rows_kernel when the wire-format transaction failed to decode
+// (the public EGES_VF_* bits are 1, 2, 4: include/eges.h)
+constexpr uint8_t VF_DECODE_ERR = 0x8;
 // The recover kernel keeps per-signature state between its phases in SLOT_ROWS uint4 rows of
 // n_pad entries right after the record rows (k_recover.hip). A thread owns <= MAX_SLOTS.
 constexpr int SLOT_ROWS = 12;
@@ -56,6 +59,9 @@ hipError_t launch_prep_ecrecover(const uint8_t* msg, const uint8_t* sig, uint32_
 hipError_t launch_prep_sender(const uint8_t* sighash, const uint8_t* r, const uint8_t* s, const uint8_t* v,
                               const uint8_t* vflags, uint32_t n, uint32_t n_pad, int signer, uint64_t chain_id,
                               uint32_t* rec, hipStream_t st);
+hipError_t launch_tx_rows(const uint8_t* raw, const uint64_t* offsets, uint64_t first, uint32_t n, int signer,
+                          uint64_t chain_id, uint8_t* sighash, uint8_t* r, uint8_t* s, uint8_t* v, uint8_t* vflags,
+                          hipStream_t st);
 #ifdef EGES_PHASE_STAMPS
 hipError_t launch_recover_stamped(const RecoverParams& p, int max_blocks, hipStream_t st, uint64_t* stamps);
 #endif

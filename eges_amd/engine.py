@@ -61,6 +61,33 @@ def sender_batch(sighash, r, s, v, vflags, signer, chain_id):
     return addr, status
 
 
+def pack_raw(raws):
+    """List of per-transaction RLP byte strings -> (raw uint8 buffer, offsets uint64 (n+1,))."""
+    raws = [bytes(x) for x in raws]
+    offsets = np.zeros(len(raws) + 1, np.uint64)
+    if raws:
+        offsets[1:] = np.cumsum([len(x) for x in raws], dtype=np.uint64)
+    raw = np.frombuffer(b"".join(raws), np.uint8) if offsets[-1] else np.zeros(1, np.uint8)
+    return raw, offsets
+
+
+def sender_raw_batch(raws, signer, chain_id, want_sighash=False):
+    """types.Sender over wire-format transactions (a list of txdata RLP encodings, or a
+    (raw, offsets) pair as pack_raw returns) -> (addr (n,20), status (n,), sighash (n,32)|None).
+    Decoding, signing hash and recovery all run on the GPU (eges_sender_raw_batch)."""
+    raw, offsets = raws if isinstance(raws, tuple) else pack_raw(raws)
+    raw = np.ascontiguousarray(raw, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    n = offsets.shape[0] - 1
+    addr = np.zeros((n, 20), np.uint8)
+    status = np.zeros(n, np.uint8)
+    sighash = np.zeros((n, 32), np.uint8) if want_sighash else None
+    if n > 0:
+        check(lib.eges_sender_raw_batch(_p(raw), _p(offsets), n, int(signer), int(chain_id), _p(addr), _p(status),
+                                        _p(sighash)))
+    return addr, status, sighash
+
+
 def verify_batch(pub, publen, msg, sig):
     """crypto.VerifySignature over n items: pub (n,65) left-aligned, publen (n,), msg (n,32), sig (n,64) -> ok (n,)."""
     pub = _u8(pub, (65,), "pub")
@@ -156,4 +183,21 @@ def sender_batch_dev(sighash, r, s, v, vflags, signer, chain_id, addr=None, stat
     st = ctypes.c_void_p(stream) if stream is not None else _stream_of(sighash)
     check(lib.eges_sender_batch_dev(dev.index, _tp(sighash), _tp(r), _tp(s), _tp(v), _tp(vflags), n, int(signer),
                                     int(chain_id), _tp(addr), _tp(status), st))
+    return addr, status
+
+
+def sender_raw_batch_dev(raw, offsets, signer, chain_id, addr=None, status=None, sighash=None, stream=None):
+    """types.Sender over wire-format transactions resident on the device: raw uint8 tensor,
+    offsets int64/uint64 tensor (n+1,) (item i = raw[offsets[i]-offsets[0] : offsets[i+1]-offsets[0]])
+    -> (addr (n,20), status (n,)). Asynchronous on `stream`."""
+    import torch
+    n = offsets.shape[0] - 1
+    dev = raw.device
+    if addr is None:
+        addr = torch.empty((n, 20), dtype=torch.uint8, device=dev)
+    if status is None:
+        status = torch.empty((n,), dtype=torch.uint8, device=dev)
+    st = ctypes.c_void_p(stream) if stream is not None else _stream_of(raw)
+    check(lib.eges_sender_raw_batch_dev(dev.index, _tp(raw), _tp(offsets), n, int(signer), int(chain_id), _tp(addr),
+                                        _tp(status), _tp(sighash), st))
     return addr, status

@@ -111,6 +111,23 @@ def geec_block(first, n=1000, payload=100, chain_id=GEEC_CHAIN_ID):
     return out
 
 
+def geec_block_raw(first, sig65, payload=100, chain_id=GEEC_CHAIN_ID, is_geec=True):
+    """The transactions of geec_block(first, len(sig65), payload) as the wire carries them: the
+    10-field Geec txdata RLP [nonce, price, gas, to, value, payload, IsGeecTxn, V, R, S]
+    (core/types/transaction.go:59-76; the leader marks its filler txs with SetIsGeec,
+    consensus/geec/geec_api.go:35), signed with sig65 (R || S || recid) under EIP155Signer."""
+    coinbase = _keccak(b"eges-coinbase")[12:]
+    data = rlp_bytes(bytes(payload))
+    out = []
+    for i, sg in enumerate(np.ascontiguousarray(sig65, np.uint8)):
+        v = eip155_v(int(sg[64]), chain_id)
+        r = int.from_bytes(sg[:32].tobytes(), "big")
+        s = int.from_bytes(sg[32:64].tobytes(), "big")
+        out.append(rlp_list([rlp_uint(first + i), rlp_uint(0), rlp_uint(0), rlp_bytes(coinbase), rlp_uint(0), data,
+                             b"\x01" if is_geec else b"\x80", rlp_uint(v), rlp_uint(r), rlp_uint(s)]))
+    return out
+
+
 def sender_rows(sig65, chain_id=GEEC_CHAIN_ID):
     """R || S || recid signatures (n, 65) -> the r, s, v rows (n, 32) of eges_sender_batch for
     EIP-155-signed transactions (V = recid + 35 + 2 chainId)."""

@@ -39,7 +39,9 @@ typedef enum eges_status {
     EGES_INVALID_MSG_LEN = 3,     /* secp256k1.ErrInvalidMsgLen        crypto/secp256k1/secp256.go:55 */
     EGES_INVALID_SIG_LEN = 4,     /* secp256k1.ErrInvalidSignatureLen  secp256.go:56 */
     EGES_INVALID_RECOVERY_ID = 5, /* secp256k1.ErrInvalidRecoveryID    secp256.go:57 */
-    EGES_RECOVER_FAILED = 6       /* secp256k1.ErrRecoverFailed        secp256.go:61 */
+    EGES_RECOVER_FAILED = 6,      /* secp256k1.ErrRecoverFailed        secp256.go:61 */
+    EGES_DECODE_FAILED = 7        /* rlp.DecodeBytes(raw, tx) error (transaction.go:157-165, rlp/decode.go):
+                                     wire-format entries only; the reference never calls Sender */
 } eges_status;
 
 /* Call-level return codes. */
@@ -109,6 +111,19 @@ int eges_sender_batch(const uint8_t *sighash, const uint8_t *r, const uint8_t *s
                       const uint8_t *vflags, size_t n, int signer, uint64_t chain_id, uint8_t *addr_out,
                       uint8_t *status);
 
+/* types.Sender over a batch of wire-format transactions (SURVEY.md §8(f) N1 + N4): item i is the
+ * RLP encoding of one Geec txdata (core/types/transaction.go:59-76, 10 fields) at
+ * raw[offsets[i] - offsets[0], offsets[i+1] - offsets[0]) — offsets has n + 1 non-decreasing
+ * entries (a block body's or TxMsg's tx list split at item boundaries, or txs concatenated).
+ * On the GPU each item is decoded with the reference decoder's rules (rlp.DecodeBytes), its
+ * signing hash built and Keccak-256'd (EIP155Signer.Hash for protected V under an EIP155
+ * signer, else FrontierSigner.Hash: transaction_signing.go:127-137,155-165,207-216) and its
+ * sender recovered exactly as eges_sender_batch. Outputs: addr_out n*20, status n
+ * (EGES_DECODE_FAILED for items rlp.DecodeBytes rejects), sighash_out n*32 (nullable: the
+ * signing hash, zeros for undecodable items). */
+int eges_sender_raw_batch(const uint8_t *raw, const uint64_t *offsets, size_t n, int signer, uint64_t chain_id,
+                          uint8_t *addr_out, uint8_t *status, uint8_t *sighash_out);
+
 /* crypto.VerifySignature over a batch (signature_cgo.go:66 -> secp256.go:126-134).
  * pub: n*65 (each key left-aligned, publen[i] bytes valid: 33 or 65; 0 => false),
  * msg n*32, sig n*64. ok_out n bytes of 0/1. */
@@ -124,6 +139,10 @@ int eges_ecrecover_batch_dev(int device, const uint8_t *msg, const uint8_t *sig,
 int eges_sender_batch_dev(int device, const uint8_t *sighash, const uint8_t *r, const uint8_t *s,
                           const uint8_t *v, const uint8_t *vflags, size_t n, int signer, uint64_t chain_id,
                           uint8_t *addr_out, uint8_t *status, void *stream);
+/* offsets: device array of n + 1 entries, same meaning as above. */
+int eges_sender_raw_batch_dev(int device, const uint8_t *raw, const uint64_t *offsets, size_t n, int signer,
+                              uint64_t chain_id, uint8_t *addr_out, uint8_t *status, uint8_t *sighash_out,
+                              void *stream);
 int eges_verify_batch_dev(int device, const uint8_t *pub, const uint8_t *publen, const uint8_t *msg,
                           const uint8_t *sig, size_t n, uint8_t *ok_out, void *stream);
 

@@ -1,0 +1,180 @@
+"""GPU parity of the wire-format sender path (eges_sender_raw_batch / _dev, k_txhash.hip):
+RLP decode + signing hash + Keccak + recovery on the GPU, checked item by item (status, sighash,
+address) against oracle/txoracle.py — on the reference's own vectors (10-field Geec form, and
+the 9-field originals that the Geec struct rejects), the decode-rule table of test_txoracle.py,
+a seeded mutation fuzz over signed Geec transactions (truncations, byte flips, non-canonical
+items, nil `to` as 0xC0, IsGeecTxn values, unprotected / wide / mismatched V, multi-block
+payloads, 9-field lists, string headers) and a 1000-tx Geec block through the device entry."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import txoracle as T
+
+pytestmark = pytest.mark.gpu
+
+CHAIN = 930412  # genesis.json.template chainId
+SIGNERS = (0, 1, 2)
+
+
+def _check(engine, oracle, raws, signer, chain_id):
+    addr, st, sh = engine.sender_raw_batch(raws, signer, chain_id, want_sighash=True)
+    for i, raw in enumerate(raws):
+        ost, oaddr, oh = T.sender_raw(oracle, raw, signer, chain_id)
+        assert int(st[i]) == ost, (i, raw.hex(), int(st[i]), ost)
+        assert addr[i].tobytes() == oaddr, (i, raw.hex())
+        if ost != T.DECODE_FAILED:
+            assert sh[i].tobytes() == oh, (i, raw.hex())
+        else:
+            assert not sh[i].any()
+    return addr, st
+
+
+def test_reference_vectors(engine, oracle):
+    with open(os.path.join(GOLDEN, "vectors.json")) as f:
+        items = json.load(f)["items"]
+    vs = items["eip155_vitalik"]
+    raws = [T.to_geec10(bytes.fromhex(t["rlp"])) for t in vs["txs"]]
+    addr, st = _check(engine, oracle, raws, 2, vs["chain_id"])
+    assert (st == 0).all()
+    assert [a.tobytes().hex() for a in addr] == [t["addr"] for t in vs["txs"]]
+    nine = [bytes.fromhex(t["rlp"]) for t in vs["txs"]]
+    _, st9 = _check(engine, oracle, nine, 2, vs["chain_id"])
+    assert (st9 == T.DECODE_FAILED).all()
+    hv = items["homestead_recipients"]
+    for signer in SIGNERS:
+        addr, st = _check(engine, oracle, [T.to_geec10(bytes.fromhex(x)) for x in hv["txs"]], signer, CHAIN)
+        assert (st == 0).all() and all(a.tobytes().hex() == hv["addr"] for a in addr)
+
+
+def test_decode_rule_table(engine, oracle):
+    from test_txoracle import DECODE_CASES
+    raws = [raw for _, raw, _ in DECODE_CASES] + [b"", b"\x80", b"\xc0", b"\xf8"]
+    for signer in SIGNERS:
+        _, st = _check(engine, oracle, raws, signer, CHAIN)
+        for (name, _, ok), s in zip(DECODE_CASES, st):
+            assert (s != T.DECODE_FAILED) == ok, name
+
+
+def _geec_fields(i, rng, payload_len):
+    to = None if i % 7 == 0 else rng.bytes(20)
+    return dict(nonce=int(rng.integers(0, 1 << 62)) if i % 3 else i, price=int(rng.integers(0, 1 << 40)),
+                gas=21000 + i, to=to, value=int(rng.integers(0, 1 << 60)) if i % 4 else 0,
+                data=rng.bytes(payload_len), is_geec=bool(i % 2))
+
+
+def _encode(d, v, r, s, geec_item=None, to_item=None):
+    to_enc = to_item if to_item is not None else (T.enc_bytes(d["to"]) if d["to"] is not None else b"\x80")
+    items = [T.enc_uint(d["nonce"]), T.enc_uint(d["price"]), T.enc_uint(d["gas"]), to_enc, T.enc_uint(d["value"]),
+             T.enc_bytes(d["data"]), geec_item if geec_item is not None else (b"\x01" if d["is_geec"] else b"\x80"),
+             T.enc_uint(v), T.enc_uint(r), T.enc_uint(s)]
+    return T.enc_list(items)
+
+
+def _signed_txs(engine, first, n, payload_fn, rng, protected=True):
+    """n signed Geec transactions (EIP-155 V when `protected`, else V = 27/28), signed on the GPU
+    with the synthetic keys of indices first.. over the oracle's signing hash.
+    -> (raws, fields, sig (n,65), expected addr (n,20))."""
+    import torch
+    fields = [_geec_fields(first + i, rng, payload_fn(i)) for i in range(n)]
+    h = np.zeros((n, 32), np.uint8)
+    for i, d in enumerate(fields):
+        h[i] = np.frombuffer(engine.keccak256(T.signing_payload(dict(d, v=37 if protected else 27), 2, CHAIN)),
+                             np.uint8)
+    sig_d, exp_d = engine.synth_sign_msg_dev(torch.from_numpy(h).to("cuda:0"), first)
+    torch.cuda.synchronize()
+    sig, exp = sig_d.cpu().numpy(), exp_d.cpu().numpy()
+    raws = []
+    for i, d in enumerate(fields):
+        rec = int(sig[i, 64])
+        v = rec + 35 + 2 * CHAIN if protected else rec + 27
+        raws.append(_encode(d, v, int.from_bytes(sig[i, :32].tobytes(), "big"),
+                            int.from_bytes(sig[i, 32:64].tobytes(), "big")))
+    return raws, fields, sig, exp
+
+
+def _mutate(raw, d, sig, rng):
+    """One seeded mutation of a signed tx -> its new encoding (the oracle decides the outcome)."""
+    k = int(rng.integers(0, 14))
+    r = int.from_bytes(sig[:32].tobytes(), "big")
+    s = int.from_bytes(sig[32:64].tobytes(), "big")
+    v = int(sig[64]) + 35 + 2 * CHAIN
+    if k == 0:
+        return raw
+    if k == 1:  # one bit flipped anywhere
+        b = bytearray(raw)
+        j = int(rng.integers(0, len(b)))
+        b[j] ^= 1 << int(rng.integers(0, 8))
+        return bytes(b)
+    if k == 2:  # truncated
+        return raw[:int(rng.integers(0, len(raw)))]
+    if k == 3:  # trailing byte
+        return raw + bytes([int(rng.integers(0, 256))])
+    if k == 4:  # payload changed: the signature no longer matches (another sender or a failure)
+        return _encode(dict(d, data=d["data"] + b"\x00"), v, r, s)
+    if k == 5:
+        return _encode(d, v, r, s, geec_item=[b"\x01", b"\x00", b"\x02", b"\x81\x01", b"\x80", b"\xc0"][int(rng.integers(0, 6))])
+    if k == 6:  # unprotected V: Frontier hash
+        return _encode(d, int(sig[64]) + 27, r, s)
+    if k == 7:  # chain id mismatch
+        return _encode(d, v + 2, r, s)
+    if k == 8:  # V wider than 256 bits
+        return _encode(d, v + (1 << 300), r, s)
+    if k == 9:  # R wider than 256 bits
+        return _encode(d, v, r + (1 << 256), s)
+    if k == 10:  # high S
+        return _encode(d, v, r, (1 << 256) - 1 - s)
+    if k == 11:  # standard 9-field encoding
+        return T.enc_list([T.enc_uint(d["nonce"]), T.enc_uint(d["price"]), T.enc_uint(d["gas"]),
+                           T.enc_bytes(d["to"]) if d["to"] is not None else b"\x80", T.enc_uint(d["value"]),
+                           T.enc_bytes(d["data"]), T.enc_uint(v), T.enc_uint(r), T.enc_uint(s)])
+    if k == 12:  # the list body under a string header
+        body = raw[1:] if raw[0] < 0xf8 else raw[1 + raw[0] - 0xf7:]
+        return bytes([0xb9]) + len(body).to_bytes(2, "big") + body
+    # k == 13: nil `to` sent as an empty list (decodes as nil; the hash re-encodes it as 0x80)
+    return _encode(d, v, r, s, to_item=b"\xc0") if d["to"] is None else raw
+
+
+def test_mutation_fuzz(engine, oracle):
+    rng = np.random.default_rng(2024)
+    n = 1500
+    raws, fields, sig, exp = _signed_txs(engine, 10_000, n, lambda i: [0, 1, 55, 100, 135, 136, 300, 2000][i % 8], rng)
+    addr, st = _check(engine, oracle, raws, 2, CHAIN)  # unmutated: the synthetic keys' addresses
+    assert (st == 0).all() and np.array_equal(addr, exp)
+    mutated = [_mutate(raws[i], fields[i], sig[i], rng) for i in range(n)]
+    seen = set()
+    for signer in SIGNERS:
+        _, st = _check(engine, oracle, mutated, signer, CHAIN)
+        seen |= set(np.unique(st).tolist())
+    assert {0, 1, 2, T.DECODE_FAILED} <= seen, seen
+
+
+def test_unprotected_txs(engine, oracle):
+    rng = np.random.default_rng(5)
+    raws, _, _, exp = _signed_txs(engine, 50_000, 64, lambda i: 100, rng, protected=False)
+    for signer in SIGNERS:
+        addr, st = _check(engine, oracle, raws, signer, CHAIN)
+        assert (st == 0).all() and np.array_equal(addr, exp)
+
+
+def test_geec_block_device_entry(engine, oracle):
+    """C3's shape: 1000 EIP-155 transfers with a 100-byte payload, resident on the device."""
+    import torch
+    rng = np.random.default_rng(77)
+    raws, _, _, exp = _signed_txs(engine, 90_000, 1000, lambda i: 100, rng)
+    raw, off = engine.pack_raw(raws)
+    raw_d = torch.from_numpy(raw).to("cuda:0")
+    off_d = torch.from_numpy(off.astype(np.int64)).to("cuda:0")
+    addr_d, st_d = engine.sender_raw_batch_dev(raw_d, off_d, 2, CHAIN)
+    torch.cuda.synchronize()
+    assert (st_d.cpu().numpy() == 0).all() and np.array_equal(addr_d.cpu().numpy(), exp)
+    for i in (0, 511, 999):
+        ost, oaddr, _ = T.sender_raw(oracle, raws[i], 2, CHAIN)
+        assert ost == 0 and oaddr == exp[i].tobytes()
+    # offsets that are positions in a larger buffer: only differences from offsets[0] matter
+    a2, s2 = engine.sender_raw_batch_dev(raw_d, off_d + 37, 2, CHAIN)
+    torch.cuda.synchronize()
+    assert torch.equal(a2, addr_d) and torch.equal(s2, st_d)
