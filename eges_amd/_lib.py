@@ -52,10 +52,12 @@ SIGNATURES = {
     "eges_ecrecover_batch": (_I, [_P, _P, _SZ, _P, _P, _P]),
     "eges_sender_batch": (_I, [_P, _P, _P, _P, _P, _SZ, _I, _U64, _P, _P]),
     "eges_sender_raw_batch": (_I, [_P, _P, _SZ, _I, _U64, _P, _P, _P]),
+    "eges_ecrecover_precompile_batch": (_I, [_P, _P, _SZ, _P, _P]),
     "eges_verify_batch": (_I, [_P, _P, _P, _P, _SZ, _P]),
     "eges_ecrecover_batch_dev": (_I, [_I, _P, _P, _SZ, _P, _P, _P, _P]),
     "eges_sender_batch_dev": (_I, [_I, _P, _P, _P, _P, _P, _SZ, _I, _U64, _P, _P, _P]),
     "eges_sender_raw_batch_dev": (_I, [_I, _P, _P, _SZ, _I, _U64, _P, _P, _P, _P]),
+    "eges_ecrecover_precompile_batch_dev": (_I, [_I, _P, _P, _SZ, _P, _P, _P]),
     "eges_verify_batch_dev": (_I, [_I, _P, _P, _P, _P, _SZ, _P, _P]),
     "eges_keccak256": (None, [_P, _SZ, _P]),
     "eges_synth_sign_dev": (_I, [_I, _U64, _SZ, _P, _P, _P, _P]),

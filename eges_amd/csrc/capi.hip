@@ -222,6 +222,26 @@ int run_sender_raw_dev(Dev& d, const uint8_t* raw, const uint64_t* offsets, size
   return EGES_SUCCESS;
 }
 
+// EVM precompile: 32-byte output words (12 zero bytes + address) written in place by the
+// recover kernel (addr_stride 32) after the words are cleared.
+int run_precompile_dev(Dev& d, const uint8_t* input, const uint32_t* inlen, size_t n, uint8_t* out32, uint8_t* status,
+                       hipStream_t st) {
+  const size_t c = std::min(n, CHUNK);
+  const size_t n_pad = align_up(c, 64);
+  int rc = dev_ensure_buf(d, recover_scratch_bytes(n_pad));
+  if (rc) return rc;
+  uint32_t* rec = reinterpret_cast<uint32_t*>(d.buf);
+  Serial ser(d, st);
+  HIPCHK(hipMemsetAsync(out32, 0, n * 32, st));
+  for (size_t off = 0; off < n; off += CHUNK) {
+    const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
+    HIPCHK(launch_prep_precompile(input + off * 128, inlen ? inlen + off : nullptr, m, (uint32_t)n_pad, rec, st));
+    RecoverParams p{rec, m, (uint32_t)n_pad, status + off, out32 + off * 32 + 12, nullptr, d.gtab, d.ws, 32};
+    HIPCHK(launch_recover(p, d.mb_recover, st));
+  }
+  return EGES_SUCCESS;
+}
+
 int run_verify_dev(Dev& d, const uint8_t* pub, const uint8_t* publen, const uint8_t* msg, const uint8_t* sig, size_t n,
                    uint8_t* ok, hipStream_t st) {
   Serial ser(d, st);
@@ -236,7 +256,8 @@ int run_verify_dev(Dev& d, const uint8_t* pub, const uint8_t* publen, const uint
 // ------------------------------------------------------------------ host-buffer pipelines
 // Copies the inputs of [off, off+cnt) to device scratch, runs, copies outputs back. Synchronous.
 struct HostJob {
-  enum Kind { RECOVER, SENDER, VERIFY, SENDER_RAW } kind;
+  enum Kind { RECOVER, SENDER, VERIFY, SENDER_RAW, PRECOMPILE } kind;
+  const uint32_t* inlen = nullptr;  // PRECOMPILE: optional input lengths
   const uint64_t* offsets = nullptr;  // SENDER_RAW: n + 1 entries
   uint8_t* sighash = nullptr;         // SENDER_RAW: optional output
   // inputs
@@ -260,6 +281,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       case HostJob::RECOVER: in_bytes = m * (32 + 65); break;
       case HostJob::SENDER: in_bytes = m * (32 * 4 + 1); break;
       case HostJob::VERIFY: in_bytes = m * (65 + 1 + 32 + 64); break;
+      case HostJob::PRECOMPILE: in_bytes = m * (128 + 4); break;
       case HostJob::SENDER_RAW:
         raw_lo = j.offsets[base] - j.offsets[0];
         raw_len = j.offsets[base + m] - j.offsets[base];
@@ -267,7 +289,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
         break;
     }
     const size_t rec_bytes = (j.kind == HostJob::VERIFY) ? 0 : recover_scratch_bytes(m_pad);
-    const size_t out_bytes = m * (65 + 20 + 1);
+    const size_t out_bytes = m * (65 + 32 + 1);
     const size_t o_in = 0, o_rec = align_up(in_bytes, 256), o_out = o_rec + align_up(rec_bytes, 256);
     int rc = dev_ensure_buf(d, o_out + out_bytes);
     if (rc) return rc;
@@ -276,7 +298,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
     HIPCHK(hipStreamWaitEvent(st, d.last, 0));
     uint8_t* o_pub = B + o_out;
     uint8_t* o_addr = o_pub + m * 65;
-    uint8_t* o_st = o_addr + m * 20;
+    uint8_t* o_st = o_addr + m * 32;
     if (j.kind == HostJob::RECOVER) {
       uint8_t* dm = B + o_in;
       uint8_t* ds = dm + m * 32;
@@ -302,6 +324,16 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       HIPCHK(launch_prep_sender(dh, dr, dsv, dv, j.e ? df : nullptr, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id,
                                 rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
+      HIPCHK(launch_recover(p, d.mb_recover, st));
+    } else if (j.kind == HostJob::PRECOMPILE) {
+      uint8_t* din = B + o_in;
+      uint32_t* dlen = reinterpret_cast<uint32_t*>(din + m * 128);
+      HIPCHK(hipMemcpyAsync(din, j.a + base * 128, m * 128, hipMemcpyHostToDevice, st));
+      if (j.inlen) HIPCHK(hipMemcpyAsync(dlen, j.inlen + base, m * 4, hipMemcpyHostToDevice, st));
+      uint32_t* rec = reinterpret_cast<uint32_t*>(B + o_rec);
+      HIPCHK(hipMemsetAsync(o_addr, 0, m * 32, st));
+      HIPCHK(launch_prep_precompile(din, j.inlen ? dlen : nullptr, (uint32_t)m, (uint32_t)m_pad, rec, st));
+      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr + 12, nullptr, d.gtab, d.ws, 32};
       HIPCHK(launch_recover(p, d.mb_recover, st));
     } else if (j.kind == HostJob::SENDER_RAW) {
       uint8_t* draw = B + o_in;
@@ -333,7 +365,8 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
     }
     HIPCHK(hipEventRecord(d.last, st));
     if (j.pub) HIPCHK(hipMemcpyAsync(j.pub + base * 65, o_pub, m * 65, hipMemcpyDeviceToHost, st));
-    if (j.addr) HIPCHK(hipMemcpyAsync(j.addr + base * 20, o_addr, m * 20, hipMemcpyDeviceToHost, st));
+    const size_t astride = j.kind == HostJob::PRECOMPILE ? 32 : 20;
+    if (j.addr) HIPCHK(hipMemcpyAsync(j.addr + base * astride, o_addr, m * astride, hipMemcpyDeviceToHost, st));
     if (j.status) HIPCHK(hipMemcpyAsync(j.status + base, o_st, m, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
   }
@@ -517,6 +550,19 @@ int eges_sender_raw_batch(const uint8_t* raw, const uint64_t* offsets, size_t n,
   return run_host(j, n);
 }
 
+int eges_ecrecover_precompile_batch(const uint8_t* input, const uint32_t* inlen, size_t n, uint8_t* out32,
+                                    uint8_t* status) {
+  if (n == 0) return EGES_SUCCESS;
+  if (!input || !out32 || !status) return set_err(EGES_E_NULLPTR, "NULL argument");
+  HostJob j;
+  j.kind = HostJob::PRECOMPILE;
+  j.a = input;
+  j.inlen = inlen;
+  j.addr = out32;
+  j.status = status;
+  return run_host(j, n);
+}
+
 int eges_verify_batch(const uint8_t* pub, const uint8_t* publen, const uint8_t* msg, const uint8_t* sig, size_t n,
                       uint8_t* ok_out) {
   if (n == 0) return EGES_SUCCESS;
@@ -596,6 +642,19 @@ int eges_sender_raw_batch_dev(int device, const uint8_t* raw, const uint64_t* of
   DevGuard g(device);
   return run_sender_raw_dev(*d, raw, offsets, n, signer, chain_id, addr_out, status, sighash_out,
                             (hipStream_t)stream);
+}
+
+int eges_ecrecover_precompile_batch_dev(int device, const uint8_t* input, const uint32_t* inlen, size_t n,
+                                        uint8_t* out32, uint8_t* status, void* stream) {
+  if (n == 0) return EGES_SUCCESS;
+  if (!input || !out32 || !status) return set_err(EGES_E_NULLPTR, "NULL argument");
+  int rc = ensure_init();
+  if (rc) return rc;
+  Dev* d = dev_by_id(device);
+  if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
+  std::lock_guard<std::mutex> lk(d->mu);
+  DevGuard g(device);
+  return run_precompile_dev(*d, input, inlen, n, out32, status, (hipStream_t)stream);
 }
 
 int eges_verify_batch_dev(int device, const uint8_t* pub, const uint8_t* publen, const uint8_t* msg, const uint8_t* sig,

@@ -164,6 +164,41 @@ __global__ void __launch_bounds__(256) prep_sender_kernel(const uint8_t* __restr
   rec[(size_t)24 * n_pad + i] = recid | (status << 8);
 }
 
+// EVM ECRECOVER precompile (core/vm/contracts.go:77-101): input (hash, v, r, s), each 32 bytes,
+// right-padded to 128 (common.RightPadBytes: bytes at or past inlen[i] read as zero). Rejected
+// before the C call (-> nil output): input[32:63] not all zero, or ValidateSignatureValues(v =
+// input[63] - 27 as a byte, r, s, homestead = false) fails (crypto.go:181-192).
+__global__ void __launch_bounds__(256) prep_precompile_kernel(const uint8_t* __restrict__ input,
+                                                              const uint32_t* __restrict__ inlen, uint32_t n,
+                                                              uint32_t n_pad, uint32_t* __restrict__ rec) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* in = input + (size_t)i * 128;
+  const uint32_t len = inlen ? inlen[i] : 128u;
+  uint8_t b[128];
+#pragma unroll
+  for (int k = 0; k < 128; ++k) b[k] = (uint32_t)k < len ? in[k] : (uint8_t)0;
+  uint32_t z[8], r[8], s[8];
+  limbs_from_be32(z, b);
+  limbs_from_be32(r, b + 64);
+  limbs_from_be32(s, b + 96);
+  uint32_t nz = 0;
+#pragma unroll
+  for (int k = 32; k < 63; ++k) nz |= b[k];
+  const uint32_t v = (uint32_t)(uint8_t)(b[63] - 27u);
+  bool r_zero = true, s_zero = true;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { r_zero = r_zero && r[k] == 0; s_zero = s_zero && s[k] == 0; }
+  const bool bad = nz != 0 || r_zero || s_zero || u256_ge(r, SC_N) || u256_ge(s, SC_N) || v > 1u;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    rec[(size_t)k * n_pad + i] = z[k];
+    rec[(size_t)(8 + k) * n_pad + i] = r[k];
+    rec[(size_t)(16 + k) * n_pad + i] = s[k];
+  }
+  rec[(size_t)24 * n_pad + i] = bad ? (ST_INVALID_SIG << 8) : v;
+}
+
 // ------------------------------------------------------------------ launchers
 hipError_t launch_init_gtab(uint32_t* gtab, hipStream_t st) {
   hipLaunchKernelGGL(init_gtab_kernel, dim3((2 * GTAB + 255) / 256), dim3(256), 0, st, gtab);
@@ -181,6 +216,12 @@ hipError_t launch_prep_sender(const uint8_t* sighash, const uint8_t* r, const ui
                               uint32_t* rec, hipStream_t st) {
   hipLaunchKernelGGL(prep_sender_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sighash, r, s, v, vflags, n, n_pad,
                      signer, chain_id, rec);
+  return hipGetLastError();
+}
+
+hipError_t launch_prep_precompile(const uint8_t* input, const uint32_t* inlen, uint32_t n, uint32_t n_pad,
+                                  uint32_t* rec, hipStream_t st) {
+  hipLaunchKernelGGL(prep_precompile_kernel, dim3((n + 255) / 256), dim3(256), 0, st, input, inlen, n, n_pad, rec);
   return hipGetLastError();
 }
 

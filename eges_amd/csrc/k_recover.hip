@@ -197,7 +197,7 @@ DEV void recover_body(const RecoverParams& prm, uint64_t* stamps) {
     if (prm.addr) {
       uint32_t a[5];
       pub_address(a, X, Y);
-      uint32_t* dst = reinterpret_cast<uint32_t*>(prm.addr + (size_t)idx * 20);
+      uint32_t* dst = reinterpret_cast<uint32_t*>(prm.addr + (size_t)idx * prm.addr_stride);
 #pragma unroll
       for (int i = 0; i < 5; ++i) dst[i] = ok ? a[i] : 0u;
     }

@@ -29,6 +29,7 @@ struct RecoverParams {
   uint8_t* pub;   // nullable, n*65
   const uint32_t* gtab;
   uint32_t* ws;
+  uint32_t addr_stride = 20;  // bytes between consecutive addresses (32 for the EVM precompile's word)
 };
 
 struct VerifyParams {
@@ -59,6 +60,8 @@ hipError_t launch_prep_ecrecover(const uint8_t* msg, const uint8_t* sig, uint32_
 hipError_t launch_prep_sender(const uint8_t* sighash, const uint8_t* r, const uint8_t* s, const uint8_t* v,
                               const uint8_t* vflags, uint32_t n, uint32_t n_pad, int signer, uint64_t chain_id,
                               uint32_t* rec, hipStream_t st);
+hipError_t launch_prep_precompile(const uint8_t* input, const uint32_t* inlen, uint32_t n, uint32_t n_pad,
+                                  uint32_t* rec, hipStream_t st);
 hipError_t launch_tx_rows(const uint8_t* raw, const uint64_t* offsets, uint64_t first, uint32_t n, int signer,
                           uint64_t chain_id, uint8_t* sighash, uint8_t* r, uint8_t* s, uint8_t* v, uint8_t* vflags,
                           hipStream_t st);

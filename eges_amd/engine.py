@@ -67,7 +67,7 @@ def pack_raw(raws):
     offsets = np.zeros(len(raws) + 1, np.uint64)
     if raws:
         offsets[1:] = np.cumsum([len(x) for x in raws], dtype=np.uint64)
-    raw = np.frombuffer(b"".join(raws), np.uint8) if offsets[-1] else np.zeros(1, np.uint8)
+    raw = np.frombuffer(b"".join(raws), np.uint8).copy() if offsets[-1] else np.zeros(1, np.uint8)
     return raw, offsets
 
 
@@ -86,6 +86,24 @@ def sender_raw_batch(raws, signer, chain_id, want_sighash=False):
         check(lib.eges_sender_raw_batch(_p(raw), _p(offsets), n, int(signer), int(chain_id), _p(addr), _p(status),
                                         _p(sighash)))
     return addr, status, sighash
+
+
+def ecrecover_precompile_batch(inputs):
+    """The EVM ECRECOVER precompile (core/vm/contracts.go:77-101) over a list of call inputs
+    (bytes of any length) -> (out (n,32), status (n,)); item i returns out[i] when status[i] == 0
+    and nil otherwise."""
+    n = len(inputs)
+    buf = np.zeros((n, 128), np.uint8)
+    inlen = np.zeros(n, np.uint32)
+    for i, x in enumerate(inputs):
+        x = bytes(x)[:128]
+        buf[i, :len(x)] = np.frombuffer(x, np.uint8)
+        inlen[i] = len(x)
+    out = np.zeros((n, 32), np.uint8)
+    status = np.zeros(n, np.uint8)
+    if n:
+        check(lib.eges_ecrecover_precompile_batch(_p(buf), _p(inlen), n, _p(out), _p(status)))
+    return out, status
 
 
 def verify_batch(pub, publen, msg, sig):
@@ -201,3 +219,18 @@ def sender_raw_batch_dev(raw, offsets, signer, chain_id, addr=None, status=None,
     check(lib.eges_sender_raw_batch_dev(dev.index, _tp(raw), _tp(offsets), n, int(signer), int(chain_id), _tp(addr),
                                         _tp(status), _tp(sighash), st))
     return addr, status
+
+
+def ecrecover_precompile_batch_dev(input, inlen=None, out=None, status=None, stream=None):
+    """The ECRECOVER precompile over device tensors: input (n,128) uint8, inlen (n,) int32 or None
+    -> (out (n,32), status (n,)). Asynchronous on `stream`."""
+    import torch
+    n = input.shape[0]
+    dev = input.device
+    if out is None:
+        out = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    if status is None:
+        status = torch.empty((n,), dtype=torch.uint8, device=dev)
+    st = ctypes.c_void_p(stream) if stream is not None else _stream_of(input)
+    check(lib.eges_ecrecover_precompile_batch_dev(dev.index, _tp(input), _tp(inlen), n, _tp(out), _tp(status), st))
+    return out, status

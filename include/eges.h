@@ -124,6 +124,16 @@ int eges_sender_batch(const uint8_t *sighash, const uint8_t *r, const uint8_t *s
 int eges_sender_raw_batch(const uint8_t *raw, const uint64_t *offsets, size_t n, int signer, uint64_t chain_id,
                           uint8_t *addr_out, uint8_t *status, uint8_t *sighash_out);
 
+/* The EVM ECRECOVER precompile (core/vm/contracts.go:77-101, address 0x01) over a batch: input
+ * n*128 (hash, v, r, s as 32-byte words); inlen n (nullable = all 128): bytes at or past
+ * inlen[i] read as zero, which is the RightPadBytes of :82 (a longer input passes its first 128
+ * bytes, as Run reads no further). out32 n*32: 12 zero bytes + the address when status[i] ==
+ * EGES_OK, all zero when Run returns nil — status EGES_INVALID_SIG for its pre-checks
+ * (input[32:63] not zero, ValidateSignatureValues(input[63] - 27, r, s, homestead = false)) or
+ * EGES_RECOVER_FAILED when crypto.Ecrecover fails. */
+int eges_ecrecover_precompile_batch(const uint8_t *input, const uint32_t *inlen, size_t n, uint8_t *out32,
+                                    uint8_t *status);
+
 /* crypto.VerifySignature over a batch (signature_cgo.go:66 -> secp256.go:126-134).
  * pub: n*65 (each key left-aligned, publen[i] bytes valid: 33 or 65; 0 => false),
  * msg n*32, sig n*64. ok_out n bytes of 0/1. */
@@ -143,6 +153,8 @@ int eges_sender_batch_dev(int device, const uint8_t *sighash, const uint8_t *r, 
 int eges_sender_raw_batch_dev(int device, const uint8_t *raw, const uint64_t *offsets, size_t n, int signer,
                               uint64_t chain_id, uint8_t *addr_out, uint8_t *status, uint8_t *sighash_out,
                               void *stream);
+int eges_ecrecover_precompile_batch_dev(int device, const uint8_t *input, const uint32_t *inlen, size_t n,
+                                        uint8_t *out32, uint8_t *status, void *stream);
 int eges_verify_batch_dev(int device, const uint8_t *pub, const uint8_t *publen, const uint8_t *msg,
                           const uint8_t *sig, size_t n, uint8_t *ok_out, void *stream);
 

@@ -16,7 +16,9 @@ Pure-Python restatement of what the reference does from raw transaction bytes to
     :155-165) re-encoded with rlp/encode.go's rules and Keccak-256'd (rlpHash, block.go:134-139);
     EIP155Signer.Sender (:127-137) picks the Frontier hash for unprotected V (isProtectedV,
     transaction.go:142-149);
-  - the sender itself through the C oracle's Sender (oracle.c, pinned by oracle/_ref).
+  - the sender itself through the C oracle's Sender (oracle.c, pinned by oracle/_ref);
+  - the EVM ECRECOVER precompile's Run (core/vm/contracts.go:77-101), pinned by the reference's
+    own sample (contracts_test.go:390-395).
 Pinned by: the reference's Vitalik EIP-155 vectors (transaction_signing_test.go:79-116) and the
 Homestead recipient vectors (transaction_test.go:82-127), re-encoded in the 10-field Geec form;
 the 9-field originals must fail to decode under the Geec struct.
@@ -230,6 +232,25 @@ def sender_raw(oracle, raw, signer, chain_id):
     flags = (1 if vw else 0) | (2 if rw else 0) | (4 if sw else 0)
     st, addr = oracle.sender(signer, chain_id, h, rb, sb, vb, flags)
     return st, (addr if st == 0 else bytes(20)), h
+
+
+def precompile_ecrecover(oracle, inp):
+    """ECRECOVER precompile Run (core/vm/contracts.go:77-101) -> (status, 32-byte output or None).
+    status: 0 ok, 2 rejected by the pre-checks (input[32:63] / ValidateSignatureValues with
+    homestead = false), 6 crypto.Ecrecover failed."""
+    inp = bytes(inp)
+    if len(inp) < 128:
+        inp = inp + bytes(128 - len(inp))  # common.RightPadBytes
+    r = int.from_bytes(inp[64:96], "big")
+    s = int.from_bytes(inp[96:128], "big")
+    v = (inp[63] - 27) & 0xff
+    N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+    if any(inp[32:63]) or not (1 <= r < N and 1 <= s < N and v in (0, 1)):
+        return 2, None
+    st, pub = oracle.recover_pubkey(inp[:32], inp[64:128] + bytes([v]))
+    if st != 0:
+        return 6, None
+    return 0, bytes(12) + oracle.keccak256(pub[1:])[12:]
 
 
 def to_geec10(raw9):

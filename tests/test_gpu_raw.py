@@ -4,7 +4,8 @@ address) against oracle/txoracle.py — on the reference's own vectors (10-field
 the 9-field originals that the Geec struct rejects), the decode-rule table of test_txoracle.py,
 a seeded mutation fuzz over signed Geec transactions (truncations, byte flips, non-canonical
 items, nil `to` as 0xC0, IsGeecTxn values, unprotected / wide / mismatched V, multi-block
-payloads, 9-field lists, string headers) and a 1000-tx Geec block through the device entry."""
+payloads, 9-field lists, string headers) and a 1000-tx Geec block through the device entry;
+plus the EVM ECRECOVER precompile batch (eges_ecrecover_precompile_batch / _dev)."""
 import json
 import os
 
@@ -178,3 +179,47 @@ def test_geec_block_device_entry(engine, oracle):
     a2, s2 = engine.sender_raw_batch_dev(raw_d, off_d + 37, 2, CHAIN)
     torch.cuda.synchronize()
     assert torch.equal(a2, addr_d) and torch.equal(s2, st_d)
+
+
+def test_ecrecover_precompile(engine, oracle):
+    """EVM ECRECOVER precompile (core/vm/contracts.go:77-101) through eges_ecrecover_precompile_batch:
+    the reference's sample (contracts_test.go:390-395), the pre-check cases, and synthetic
+    signatures with seeded mutations, every output word and status against the oracle."""
+    import torch
+    from test_txoracle import PRECOMPILE_VECTOR, precompile_cases
+    inputs = [bytes.fromhex(PRECOMPILE_VECTOR[0])] + [c for c, _ in precompile_cases()]
+    msg, sig, exp = engine.synth_sign_dev(123_000, 600, 0)
+    torch.cuda.synchronize()
+    msg, sig, exp = msg.cpu().numpy(), sig.cpu().numpy(), exp.cpu().numpy()
+    rng = np.random.default_rng(31)
+    for i in range(600):
+        word = bytes(31) + bytes([27 + int(sig[i, 64])])
+        x = msg[i].tobytes() + word + sig[i, :64].tobytes()
+        k = i % 6
+        if k == 1:
+            j = int(rng.integers(0, 128))
+            x = x[:j] + bytes([x[j] ^ (1 << int(rng.integers(0, 8)))]) + x[j + 1:]
+        elif k == 2:
+            x = x[:int(rng.integers(0, 129))]
+        elif k == 3:
+            x = x + rng.bytes(int(rng.integers(1, 64)))
+        inputs.append(x)
+    out, st = engine.ecrecover_precompile_batch(inputs)
+    for i, x in enumerate(inputs):
+        ost, oout = T.precompile_ecrecover(oracle, x)
+        assert int(st[i]) == ost, (i, x.hex())
+        assert out[i].tobytes() == (oout if oout is not None else bytes(32)), (i, x.hex())
+    assert out[0].tobytes().hex() == PRECOMPILE_VECTOR[1]
+    base = len(inputs) - 600
+    for i in range(0, 600, 6):  # unmutated synthetic items: the signer's address
+        assert st[base + i] == 0 and out[base + i, 12:].tobytes() == exp[i].tobytes()
+    # device entry, fixed 128-byte records
+    buf = np.zeros((len(inputs), 128), np.uint8)
+    ln = np.zeros(len(inputs), np.int32)
+    for i, x in enumerate(inputs):
+        x = x[:128]
+        buf[i, :len(x)] = np.frombuffer(x, np.uint8)
+        ln[i] = len(x)
+    o2, s2 = engine.ecrecover_precompile_batch_dev(torch.from_numpy(buf).cuda(), torch.from_numpy(ln).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(o2.cpu().numpy(), out) and np.array_equal(s2.cpu().numpy(), st)

@@ -138,3 +138,39 @@ def test_signing_payload_matches_host_helpers():
     assert h == txs.eip155_sighash(d["nonce"], d["price"], d["gas"], d["to"], d["value"], d["data"], txs.GEEC_CHAIN_ID)
     h0 = keccak256(T.signing_payload(d, 0, txs.GEEC_CHAIN_ID))
     assert h0 == txs.frontier_sighash(d["nonce"], d["price"], d["gas"], d["to"], d["value"], d["data"])
+
+
+# core/vm/contracts_test.go:390-395 (BenchmarkPrecompiledEcrecover sample)
+PRECOMPILE_VECTOR = ("38d18acb67d25c8bb9942764b62f18e17054f66a817bd4295423adf9ed98873e"
+                     "000000000000000000000000000000000000000000000000000000000000001b"
+                     "38d18acb67d25c8bb9942764b62f18e17054f66a817bd4295423adf9ed98873e"
+                     "789d1dd423d25f0772d2748d60f7e4b81bb14d086eba8e8e8efb6dcff8a4ae02",
+                     "000000000000000000000000ceaccac640adf55b2028469bd36ba501f28b699d")
+
+
+def precompile_cases():
+    """(input, expected status) around the reference vector: the pre-checks of Run and padding."""
+    good = bytes.fromhex(PRECOMPILE_VECTOR[0])
+    N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+    flip = lambda b, i, x: b[:i] + bytes([x]) + b[i + 1:]
+    cases = [(good, 0), (good + b"\x99" * 40, 0),                      # longer input: first 128 bytes
+             (flip(good, 40, 1), 2),                                   # input[32:63] not zero
+             (flip(good, 63, 0x1c), None),                             # v = 1: another key or failure
+             (flip(good, 63, 0x1d), 2), (flip(good, 63, 0x00), 2),     # v not 27/28 (byte wrap)
+             (good[:64] + bytes(32) + good[96:], 2),                   # r = 0
+             (good[:96] + bytes(32), 2),                               # s = 0
+             (good[:64] + N.to_bytes(32, "big") + good[96:], 2),       # r = N
+             (good[:96] + (N - 1).to_bytes(32, "big"), 0),             # high s allowed (homestead = false)
+             (good[:64] + (5).to_bytes(32, "big") + good[96:], 6),     # x = 5: not on the curve
+             (good[:100], None), (b"", 2), (good[:127], None), (good[:64], 2)]  # right-padded short inputs
+    return cases
+
+
+def test_precompile_reference_vector(oracle):
+    st, out = T.precompile_ecrecover(oracle, bytes.fromhex(PRECOMPILE_VECTOR[0]))
+    assert st == 0 and out.hex() == PRECOMPILE_VECTOR[1]
+    for inp, exp in precompile_cases():
+        st, out = T.precompile_ecrecover(oracle, inp)
+        if exp is not None:
+            assert st == exp, inp.hex()
+        assert (out is None) == (st != 0)
