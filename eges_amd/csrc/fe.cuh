@@ -91,19 +91,61 @@ DEV void fe_to_u256(uint32_t x[8], const fe& a) {
 
 // ------------------------------------------------------------------ reduction of 17 columns
 // S[0..16]: column sums (each < 2^63.9). Returns magnitude-1 limbs (limb 2 carries < 2^15 slack).
+#ifndef EGES_FOLD
+#define EGES_FOLD 1
+#endif
 DEV fe fe_reduce_cols(uint64_t S[17]) {
-  const uint32_t f8 = opaque_u32(1u << 8), f11 = opaque_u32(1u << 11), fhi = opaque_u32(FOLD0 << 3);
-  // fold columns 16..9, descending (column 16 spills into column 9, folded afterwards).
-  // S_k 2^(29k) = (hi 2^32 + lo) 2^(29(k-9)) (2^37 + 31264)
+  const uint32_t f8 = opaque_u32(1u << 8), f3 = opaque_u32(1u << 3);
+  // Fold columns 9..16 into 0..8 with 2^261 == 2^37 + 31264 (mod p). S_k = hi 2^32 + lo:
+  //   lo 2^(29k) = lo 2^(29(k-9)) (2^37 + 31264): two MADs into columns k-9, k-8;
+  //   hi 2^32 2^(29k) either folds the same way (hi 8 31264 into k-8, hi 2^11 into k-7: two
+  //   MADs) or moves up as 8 hi into column k+1 (one MAD) before that column is folded.
+  // EGES_FOLD 1 (default) pushes up from every column: 26 MADs, measured 6 % faster end to end
+  // than EGES_FOLD 0 (32 MADs, every hi folded down) and 2.5 % faster than EGES_FOLD 2 (push
+  // from odd columns only: 29 MADs) on the same box — the serial chain costs nothing visible.
+  // (The same push in the carry pass below, one MAD + 32-bit carry-in instead of a 64-bit
+  // shift + add, measured 1 % slower.)
+  // Column 9 holds 8 products (< 2^63.7), so every pushed 8 hi < 2^35 keeps columns < 2^64.
+#if EGES_FOLD == 0
 #pragma unroll
   for (int k = 16; k >= 9; --k) {
     const uint32_t lo = (uint32_t)S[k];
     const uint32_t hi = (uint32_t)(S[k] >> 32);
     S[k - 9] = mad64(lo, FOLD0, S[k - 9]);
     S[k - 8] = mad64(lo, f8, S[k - 8]);
-    S[k - 8] = mad64(hi, fhi, S[k - 8]);
-    S[k - 7] = mad64(hi, f11, S[k - 7]);
+    S[k - 8] = mad64(hi, opaque_u32(FOLD0 << 3), S[k - 8]);
+    S[k - 7] = mad64(hi, opaque_u32(1u << 11), S[k - 7]);
   }
+#else
+#pragma unroll
+  for (int k = 9; k <= 15; ++k) {
+    if (EGES_FOLD == 1 || (k & 1)) {  // push hi up
+      S[k + 1] = mad64((uint32_t)(S[k] >> 32), f3, S[k + 1]);
+    }
+  }
+#pragma unroll
+  for (int k = 9; k <= 15; ++k) {
+    const uint32_t lo = (uint32_t)S[k];
+    S[k - 9] = mad64(lo, FOLD0, S[k - 9]);
+    S[k - 8] = mad64(lo, f8, S[k - 8]);
+    if (EGES_FOLD == 2 && !(k & 1)) {  // fold hi down
+      const uint32_t hi = (uint32_t)(S[k] >> 32);
+      S[k - 8] = mad64(hi, opaque_u32(FOLD0 << 3), S[k - 8]);
+      S[k - 7] = mad64(hi, opaque_u32(1u << 11), S[k - 7]);
+    }
+  }
+  {
+    // column 16: hi 2^32 2^(29*16) = 8 hi 2^(29*17), and
+    // 2^(29*17) = 2^(29*8) 2^261 == 31264 2^(29*8) + 2^16 2^29 + 2^8 31264  (mod p)
+    const uint32_t lo = (uint32_t)S[16];
+    const uint32_t hi = (uint32_t)(S[16] >> 32);  // < 2^29
+    S[7] = mad64(lo, FOLD0, S[7]);
+    S[8] = mad64(lo, f8, S[8]);
+    S[8] = mad64(hi, opaque_u32(FOLD0 << 3), S[8]);
+    S[1] = mad64(hi, opaque_u32(1u << 19), S[1]);
+    S[0] = mad64(hi, opaque_u32(FOLD0 << 11), S[0]);
+  }
+#endif
   fe r;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -115,7 +157,7 @@ DEV fe fe_reduce_cols(uint64_t S[17]) {
   const uint32_t cl = (uint32_t)c, ch = (uint32_t)(c >> 32);
   const uint64_t t0 = mad64(cl, FOLD0, r.v[0]);
   uint64_t t1 = mad64(cl, f8, r.v[1]);
-  t1 = mad64(ch, fhi, t1);
+  t1 = mad64(ch, opaque_u32(FOLD0 << 3), t1);
   r.v[0] = (uint32_t)t0 & M29;
   t1 += t0 >> 29;
   r.v[1] = (uint32_t)t1 & M29;
