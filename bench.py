@@ -109,8 +109,13 @@ class Ctx:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        # rehearsal knobs for a 1-GPU box (tools/rehearse_dist.sh): every rank on one device,
+        # gloo for the timing collectives. The driver's multi-GPU runs leave both unset.
+        if "EGES_BENCH_DEVICE" in os.environ:
+            self.local = int(os.environ["EGES_BENCH_DEVICE"])
         if self.world > 1:
-            dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
+            backend = os.environ.get("EGES_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+            dist.init_process_group(backend=backend)
         torch.cuda.set_device(self.local)
         import eges_amd
         self.eges = eges_amd

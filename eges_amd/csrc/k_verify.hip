@@ -5,13 +5,37 @@ namespace eges {
 // ------------------------------------------------------------------ verify kernel
 // crypto.VerifySignature: ext.h:58-75 -> secp256k1.c:228-247 (parse_compact), :150-163 and
 // eckey_impl.h:17-34 (pubkey parse), :293-308 (low-s), ecdsa_impl.h:203-271 (sig_verify).
+//
+// Only 33-byte keys need the (p+1)/4 square root (a third of a signature's work). Each tile of
+// WG signatures is first partitioned in LDS — compressed keys first — so at most one wave of
+// the tile mixes the two key types and every other wave skips the root (wave-uniform branch).
 __global__ void __launch_bounds__(WG, 2) verify_kernel(VerifyParams prm) {
   __shared__ CoreLds L;
-  const int tid = threadIdx.x;
+  __shared__ uint32_t perm[WG];
+  __shared__ uint32_t wcnt[NWAVES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t ntiles = (prm.n + WG - 1) / WG;
 #pragma unroll 1
   for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const uint32_t idx = tile * WG + tid;
+    {
+      const uint32_t i0 = tile * WG + tid;
+      const bool comp = i0 < prm.n && prm.publen[i0] == 33;
+      const uint64_t b = __ballot(comp);
+      const uint64_t below = (1ull << lane) - 1ull;
+      if (lane == 0) wcnt[wave] = (uint32_t)__popcll(b);
+      __syncthreads();
+      uint32_t before = 0, total = 0;
+#pragma unroll
+      for (int w = 0; w < NWAVES; ++w) {
+        before += w < wave ? wcnt[w] : 0u;
+        total += wcnt[w];
+      }
+      const uint32_t pos = comp ? before + (uint32_t)__popcll(b & below)
+                                : total + ((uint32_t)wave * 64u - before) + (uint32_t)__popcll(~b & below);
+      perm[pos] = i0;
+      __syncthreads();
+    }
+    const uint32_t idx = perm[tid];
     const bool in = idx < prm.n;
     uint32_t zl[8], rl[8], sl[8], px[8], py[8];
     uint32_t plen = 0, pfx = 0;
@@ -43,7 +67,9 @@ __global__ void __launch_bounds__(WG, 2) verify_kernel(VerifyParams prm) {
     bool pk_ok;
     {
       ge lifted;
-      const bool lo = ge_set_xo(lifted, X, pfx == 3);
+      lifted.y = Y;
+      bool lo = false;
+      if (__any(c33)) lo = ge_set_xo(lifted, X, pfx == 3);
       ge full;
       full.x = X;
       full.y = Y;
