@@ -244,10 +244,14 @@ int run_precompile_dev(Dev& d, const uint8_t* input, const uint32_t* inlen, size
 
 int run_verify_dev(Dev& d, const uint8_t* pub, const uint8_t* publen, const uint8_t* msg, const uint8_t* sig, size_t n,
                    uint8_t* ok, hipStream_t st) {
+  const size_t n_pad = align_up(std::min(n, CHUNK), 64);
+  int rc = dev_ensure_buf(d, verify_scratch_bytes(n_pad));
+  if (rc) return rc;
   Serial ser(d, st);
   for (size_t off = 0; off < n; off += CHUNK) {
     const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
     VerifyParams p{pub + off * 65, publen + off, msg + off * 32, sig + off * 64, m, ok + off, d.gtab, d.ws};
+    verify_scratch_bind(p, d.buf, n_pad);
     HIPCHK(launch_verify(p, d.mb_verify, st));
   }
   return EGES_SUCCESS;
@@ -288,7 +292,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
         in_bytes = align_up(raw_len, 8) + 8 * (m + 1) + tx_rows_bytes(m);
         break;
     }
-    const size_t rec_bytes = (j.kind == HostJob::VERIFY) ? 0 : recover_scratch_bytes(m_pad);
+    const size_t rec_bytes = (j.kind == HostJob::VERIFY) ? verify_scratch_bytes(m_pad) : recover_scratch_bytes(m_pad);
     const size_t out_bytes = m * (65 + 32 + 1);
     const size_t o_in = 0, o_rec = align_up(in_bytes, 256), o_out = o_rec + align_up(rec_bytes, 256);
     int rc = dev_ensure_buf(d, o_out + out_bytes);
@@ -361,6 +365,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       HIPCHK(hipMemcpyAsync(dm, j.c + base * 32, m * 32, hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(ds, j.d + base * 64, m * 64, hipMemcpyHostToDevice, st));
       VerifyParams p{dp, dl, dm, ds, (uint32_t)m, o_st, d.gtab, d.ws};
+      verify_scratch_bind(p, B + o_rec, m_pad);
       HIPCHK(launch_verify(p, d.mb_verify, st));
     }
     HIPCHK(hipEventRecord(d.last, st));

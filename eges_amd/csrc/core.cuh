@@ -510,6 +510,75 @@ DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& 
   if (st) st->mark(4);
 }
 
+// ------------------------------------------------------------------ lane-serial kernels
+// Per-item state between the phases of the recover / verify kernels lives in uint4 slot rows of
+// n_pad entries (recover: 0-4 R then Q.x/Q.y, 5-6 prefix product of r, 7-11 Q.z and the prefix
+// product of Z; verify: 0-4 P, 5-6 prefix product of s).
+DEV void slot_put_pt(uint4* slot, uint32_t n_pad, int row, uint32_t idx, const ge& p) {
+  uint32_t w[PT_WORDS];
+  pt_pack(w, p.x, p.y);
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+    slot[(size_t)(row + q) * n_pad + idx] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+DEV ge slot_get_pt(const uint4* slot, uint32_t n_pad, int row, uint32_t idx) {
+  uint32_t w[PT_WORDS];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const uint4 u = slot[(size_t)(row + q) * n_pad + idx];
+    w[4 * q] = u.x;
+    w[4 * q + 1] = u.y;
+    w[4 * q + 2] = u.z;
+    w[4 * q + 3] = u.w;
+  }
+  ge p;
+  pt_unpack(w, p.x, p.y);
+  return p;
+}
+DEV void slot_put_sc(uint4* slot, uint32_t n_pad, int row, uint32_t idx, const sc& a) {
+  slot[(size_t)row * n_pad + idx] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+  slot[(size_t)(row + 1) * n_pad + idx] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+}
+DEV sc slot_get_sc(const uint4* slot, uint32_t n_pad, int row, uint32_t idx) {
+  const uint4 a = slot[(size_t)row * n_pad + idx], b = slot[(size_t)(row + 1) * n_pad + idx];
+  sc r;
+  r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+  r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+  return r;
+}
+DEV void rec_get(const RecoverParams& prm, int row, uint32_t idx, uint32_t out[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) out[k] = prm.rec[(size_t)(row + k) * prm.n_pad + idx];
+}
+
+// Progress-balanced issue priority. Co-resident waves of a SIMD are otherwise arbitrated by
+// age: the older wave finishes far ahead and the younger one then runs alone at a fraction
+// of the issue rate (measured: per-wave lifetimes spread 1.8x). A wave lowers its priority
+// as it advances (units: 1 per lift, 4 per ecmult), so lagging waves catch up and the SIMD
+// keeps two waves busy to the end. p must be wave-uniform.
+DEV void balance_prio(uint32_t done, uint32_t total) {
+#ifndef EGES_NO_PRIO
+  const uint32_t q = __builtin_amdgcn_readfirstlane(total ? (4u * done) / total : 0u);
+  switch (q) {
+    case 0: __builtin_amdgcn_s_setprio(3); break;
+    case 1: __builtin_amdgcn_s_setprio(2); break;
+    case 2: __builtin_amdgcn_s_setprio(1); break;
+    default: __builtin_amdgcn_s_setprio(0); break;
+  }
+#endif
+}
+
+
+// One signature per thread up to a full resident grid, then K = ceil(n / threads) per thread;
+// more blocks than resident when that would exceed MAX_SLOTS signatures per thread.
+inline int grid_for_lane_serial(uint32_t n, int max_blocks) {
+  const uint32_t tiles = (n + WG - 1) / WG;
+  uint32_t g = tiles < (uint32_t)max_blocks ? tiles : (uint32_t)max_blocks;
+  const uint32_t min_g = (n + (uint32_t)WG * MAX_SLOTS - 1) / ((uint32_t)WG * MAX_SLOTS);
+  return (int)(g > min_g ? g : min_g);
+}
+
+
 // ------------------------------------------------------------------ byte helpers
 DEV void limbs_from_be32(uint32_t out[8], const uint8_t* b) {
 #pragma unroll

@@ -15,62 +15,6 @@ namespace eges {
 // Phase marks (diagnostic build only): 0 parse + sqrt, 1 r^-1 + u1/u2, 2 GLV + digits,
 // 3 R table, 4 Strauss loop, 5 Z^-1, 6 affine + Keccak + stores.
 //
-// Slot rows (uint4, n_pad each): 0-4 R (affine, store_pt) then Q.x/Q.y, 5-6 prefix prod r,
-// 7-11 Q.z and prefix prod Z (store_fe2).
-DEV void slot_put_pt(uint4* slot, uint32_t n_pad, int row, uint32_t idx, const ge& p) {
-  uint32_t w[PT_WORDS];
-  pt_pack(w, p.x, p.y);
-#pragma unroll
-  for (int q = 0; q < 5; ++q)
-    slot[(size_t)(row + q) * n_pad + idx] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-}
-DEV ge slot_get_pt(const uint4* slot, uint32_t n_pad, int row, uint32_t idx) {
-  uint32_t w[PT_WORDS];
-#pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    const uint4 u = slot[(size_t)(row + q) * n_pad + idx];
-    w[4 * q] = u.x;
-    w[4 * q + 1] = u.y;
-    w[4 * q + 2] = u.z;
-    w[4 * q + 3] = u.w;
-  }
-  ge p;
-  pt_unpack(w, p.x, p.y);
-  return p;
-}
-DEV void slot_put_sc(uint4* slot, uint32_t n_pad, int row, uint32_t idx, const sc& a) {
-  slot[(size_t)row * n_pad + idx] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
-  slot[(size_t)(row + 1) * n_pad + idx] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
-}
-DEV sc slot_get_sc(const uint4* slot, uint32_t n_pad, int row, uint32_t idx) {
-  const uint4 a = slot[(size_t)row * n_pad + idx], b = slot[(size_t)(row + 1) * n_pad + idx];
-  sc r;
-  r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
-  r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
-  return r;
-}
-DEV void rec_get(const RecoverParams& prm, int row, uint32_t idx, uint32_t out[8]) {
-#pragma unroll
-  for (int k = 0; k < 8; ++k) out[k] = prm.rec[(size_t)(row + k) * prm.n_pad + idx];
-}
-
-// Progress-balanced issue priority. Co-resident waves of a SIMD are otherwise arbitrated by
-// age: the older wave finishes far ahead and the younger one then runs alone at a fraction
-// of the issue rate (measured: per-wave lifetimes spread 1.8x). A wave lowers its priority
-// as it advances (units: 1 per lift, 4 per ecmult), so lagging waves catch up and the SIMD
-// keeps two waves busy to the end. p must be wave-uniform.
-DEV void balance_prio(uint32_t done, uint32_t total) {
-#ifndef EGES_NO_PRIO
-  const uint32_t q = __builtin_amdgcn_readfirstlane(total ? (4u * done) / total : 0u);
-  switch (q) {
-    case 0: __builtin_amdgcn_s_setprio(3); break;
-    case 1: __builtin_amdgcn_s_setprio(2); break;
-    case 2: __builtin_amdgcn_s_setprio(1); break;
-    default: __builtin_amdgcn_s_setprio(0); break;
-  }
-#endif
-}
-
 template <class ST>
 DEV void recover_body(const RecoverParams& prm, uint64_t* stamps) {
   __shared__ CoreLds L;
@@ -234,25 +178,16 @@ __global__ void __launch_bounds__(WG, 2) recover_kernel_stamped(RecoverParams pr
 #endif
 
 // ------------------------------------------------------------------ launcher
-// One signature per thread up to a full resident grid, then K = ceil(n / threads) per thread;
-// more blocks than resident when that would exceed MAX_SLOTS signatures per thread.
-static int grid_for(uint32_t n, int max_blocks) {
-  const uint32_t tiles = (n + WG - 1) / WG;
-  uint32_t g = tiles < (uint32_t)max_blocks ? tiles : (uint32_t)max_blocks;
-  const uint32_t min_g = (n + (uint32_t)WG * MAX_SLOTS - 1) / ((uint32_t)WG * MAX_SLOTS);
-  return (int)(g > min_g ? g : min_g);
-}
-
 hipError_t launch_recover(const RecoverParams& p, int max_blocks, hipStream_t st) {
   if (p.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(recover_kernel, dim3(grid_for(p.n, max_blocks)), dim3(WG), 0, st, p);
+  hipLaunchKernelGGL(recover_kernel, dim3(grid_for_lane_serial(p.n, max_blocks)), dim3(WG), 0, st, p);
   return hipGetLastError();
 }
 
 #ifdef EGES_PHASE_STAMPS
 hipError_t launch_recover_stamped(const RecoverParams& p, int max_blocks, hipStream_t st, uint64_t* stamps) {
   if (p.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(recover_kernel_stamped, dim3(grid_for(p.n, max_blocks)), dim3(WG), 0, st, p, stamps);
+  hipLaunchKernelGGL(recover_kernel_stamped, dim3(grid_for_lane_serial(p.n, max_blocks)), dim3(WG), 0, st, p, stamps);
   return hipGetLastError();
 }
 #endif

@@ -41,7 +41,20 @@ struct VerifyParams {
   uint8_t* ok;
   const uint32_t* gtab;
   uint32_t* ws;
+  uint32_t n_pad;
+  uint4* slot;        // VERIFY_SLOT_ROWS rows of n_pad
+  uint32_t* order;    // n_pad: processing order (compressed keys first)
+  uint32_t* counts;   // 2 counters for the order kernel
 };
+// Verify scratch: slot rows (P affine, prefix product of s), the order, the two counters.
+constexpr int VERIFY_SLOT_ROWS = 7;
+inline size_t verify_scratch_bytes(size_t n_pad) { return n_pad * ((size_t)VERIFY_SLOT_ROWS * 16 + 4) + 256; }
+inline void verify_scratch_bind(VerifyParams& p, uint8_t* scratch, size_t n_pad) {
+  p.n_pad = (uint32_t)n_pad;
+  p.slot = reinterpret_cast<uint4*>(scratch);
+  p.order = reinterpret_cast<uint32_t*>(scratch + n_pad * (size_t)VERIFY_SLOT_ROWS * 16);
+  p.counts = p.order + n_pad;
+}
 
 struct SynthParams {
   uint64_t first;

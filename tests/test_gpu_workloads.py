@@ -88,3 +88,42 @@ def test_verify_mode_mix(engine, oracle):
     assert np.array_equal(ok, exp)
     for i in range(0, 50):
         assert oracle.verify(P[i, :publen[i]].tobytes(), msg_h[i].tobytes(), sig_h[i].tobytes()) == exp[i]
+
+
+@pytest.mark.gpu
+def test_verify_lane_serial_multi_item(engine):
+    """verify_kernel with several items per thread (n > one resident grid of 131,072 threads),
+    33-byte keys scattered at random (the order kernel groups them), and mutations whose
+    expected result follows from the reference rules (secp256k1.c:293-308, eckey_impl.h:17-34)."""
+    import torch
+    from eges_amd import workloads
+    n = 300_003
+    msg, sig, _ = engine.synth_sign_dev(4242, n, 0)
+    pub = torch.empty((n, 65), dtype=torch.uint8, device="cuda")
+    engine.ecrecover_batch_dev(msg, sig, pub=pub)
+    torch.cuda.synchronize()
+    pub_h, sig_h = pub.cpu().numpy(), sig.cpu().numpy()[:, :64].copy()
+    rng = np.random.default_rng(11)
+    odd = (pub_h[:, 64] & 1).astype(np.uint8)
+    P = pub_h.copy()
+    publen = np.full(n, 65, np.uint8)
+    comp = rng.random(n) < 0.3
+    P[comp, 0] = 2 + odd[comp]
+    P[comp, 33:] = 0
+    publen[comp] = 33
+    exp = np.ones(n, np.uint8)
+    mut = np.nonzero(rng.random(n) < 0.02)[0]
+    for i, k in zip(mut.tolist(), rng.integers(0, 2, len(mut)).tolist()):
+        if k == 0:  # high s
+            s_ = int.from_bytes(sig_h[i, 32:64].tobytes(), "big")
+            sig_h[i, 32:64] = np.frombuffer((workloads.N - s_).to_bytes(32, "big"), np.uint8)
+        else:  # another signer's key
+            P[i], publen[i] = pub_h[(i + 7) % n], 65
+        exp[i] = 0
+    dev = torch.device("cuda")
+    ok = torch.empty((n,), dtype=torch.uint8, device=dev)
+    engine.verify_batch_dev(torch.from_numpy(P).to(dev), torch.from_numpy(publen).to(dev), msg,
+                            torch.from_numpy(sig_h).to(dev), ok=ok)
+    torch.cuda.synchronize()
+    got = ok.cpu().numpy()
+    assert int((got != exp).sum()) == 0
