@@ -20,6 +20,8 @@ Metric (BASELINE.json): "secp256k1 ecrecover+address/sec at 1/8 MI355X; % of INT
   non-residue R, zero r / s) through crypto.Ecrecover and types.Sender semantics, statuses
   checked bit-exact against their by-construction expectation, plus VerifySignature mode.
 --config verify: crypto.VerifySignature throughput (65-byte and 33-byte keys).
+--config c2host: configs[1]'s batch handed over as host (pageable) buffers through
+  eges_ecrecover_batch — the PCIe-inclusive rate a Go caller sees (never `value` of the c2 line).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config c2|c3|c4|c5|verify]
 """
@@ -52,7 +54,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=None, help="c2: signatures per GPU; c4: total signatures")
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c3raw", "c4", "c5", "verify"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c2host", "c3", "c3raw", "c4", "c5", "verify"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -381,6 +383,37 @@ def run_verify(c):
     c.finish(line, ok)
 
 
+# ------------------------------------------------------------------ c2host: host buffers
+def run_host_throughput(c):
+    import numpy as np
+    torch, a = c.torch, c.args
+    B = a.batch or (1 << 20)
+    msg, sig, exp_addr = c.eges.synth_sign_dev(0, B, c.local)
+    torch.cuda.synchronize()
+    msg_h, sig_h, exp_h = msg.cpu().numpy(), sig.cpu().numpy(), exp_addr.cpu().numpy()
+    out = {}
+
+    def step():
+        out["r"] = c.eges.ecrecover_batch(msg_h, sig_h, want_pub=False)
+
+    for _ in range(a.warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    elapsed = time.perf_counter() - t0
+    _, addr, st = out["r"]
+    ok = bool((st == 0).all()) and np.array_equal(addr, exp_h)
+    line = {"metric": "secp256k1 ecrecover+address/sec, host buffers (PCIe-inclusive)", "value": round(B * a.steps / elapsed, 1),
+            "unit": "sigs/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed * 1e3 / a.steps, 3), "higher_is_better": True, "dtype": "u32",
+            "data": "synthetic",
+            "config": {"workload": "configs[1] batch through eges_ecrecover_batch: pageable host msg/sig in, host "
+                                   "addresses + statuses out (H2D + prep + recover + D2H, synchronous call)",
+                       "batch": B, "correct": ok}}
+    c.finish(line, ok)
+
+
 def main():
     args = parse()
     c = Ctx(args)
@@ -390,6 +423,8 @@ def main():
         run_throughput(c, strong=True)
     elif args.config in ("c3", "c3raw"):
         run_block_latency(c)
+    elif args.config == "c2host":
+        run_host_throughput(c)
     elif args.config == "c5":
         run_adversarial(c)
     else:

@@ -22,6 +22,11 @@ namespace {
 using namespace eges;
 
 constexpr size_t CHUNK = size_t(1) << 21;  // signatures per device pass (bounds scratch memory)
+// host-buffer shards of at least 2 * PIPE_MIN items are split into >= 2 pipelined chunks
+constexpr size_t PIPE_MIN = size_t(1) << 18;
+#ifndef EGES_PIPE_PARTS
+#define EGES_PIPE_PARTS 4
+#endif
 
 thread_local std::string t_err;
 
@@ -45,7 +50,9 @@ struct Dev {
   int id = -1;
   int cus = 0;
   hipStream_t stream = nullptr;
+  hipStream_t copy = nullptr;  // host-buffer pipeline: H2D / D2H while `stream` computes
   hipEvent_t last = nullptr;  // completion of the last engine work (workspace users serialise on it)
+  hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_k[2] = {nullptr, nullptr};  // per pipeline region
   uint32_t* gtab = nullptr;
   uint32_t* ws = nullptr;
   int mb_recover = 0, mb_verify = 0, mb_synth = 0;
@@ -97,6 +104,11 @@ int init_device(int id, Dev** out) {
   d->cus = prop.multiProcessorCount;
   HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&d->last, hipEventDisableTiming));
+  HIPCHK(hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking));
+  for (int r = 0; r < 2; ++r) {
+    HIPCHK(hipEventCreateWithFlags(&d->ev_in[r], hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&d->ev_k[r], hipEventDisableTiming));
+  }
   d->mb_recover = occupancy_recover() * d->cus;
   d->mb_verify = occupancy_verify() * d->cus;
   d->mb_synth = occupancy_synth() * d->cus;
@@ -272,109 +284,170 @@ struct HostJob {
   uint8_t *pub = nullptr, *addr = nullptr, *status = nullptr;
 };
 
+// Device bytes of one pipeline region for a chunk of m items: inputs | scratch | outputs.
+struct Region {
+  size_t in_bytes = 0, raw_lo = 0, raw_len = 0, o_rec = 0, o_out = 0, total = 0;
+};
+Region region_for(const HostJob& j, size_t base, size_t m) {
+  Region g;
+  const size_t m_pad = align_up(m, 64);
+  switch (j.kind) {
+    case HostJob::RECOVER: g.in_bytes = m * (32 + 65); break;
+    case HostJob::SENDER: g.in_bytes = m * (32 * 4 + 1); break;
+    case HostJob::VERIFY: g.in_bytes = m * (65 + 1 + 32 + 64); break;
+    case HostJob::PRECOMPILE: g.in_bytes = m * (128 + 4); break;
+    case HostJob::SENDER_RAW:
+      g.raw_lo = j.offsets[base] - j.offsets[0];
+      g.raw_len = j.offsets[base + m] - j.offsets[base];
+      g.in_bytes = align_up(g.raw_len, 8) + 8 * (m + 1) + tx_rows_bytes(m);
+      break;
+  }
+  const size_t rec_bytes = (j.kind == HostJob::VERIFY) ? verify_scratch_bytes(m_pad) : recover_scratch_bytes(m_pad);
+  g.o_rec = align_up(g.in_bytes, 256);
+  g.o_out = g.o_rec + align_up(rec_bytes, 256);
+  g.total = align_up(g.o_out + m * (65 + 32 + 1), 256);
+  return g;
+}
+
+// Host-buffer pipeline over chunks of one shard. Two device regions alternate: while the
+// compute stream runs chunk i, the copy stream stages chunk i+1's inputs and returns chunk
+// i-1's outputs (host order H2D(i+1), K(i+1), D2H(i): the pageable D2H blocks this thread
+// until K(i) is done, by which time K(i+1) is queued behind it). Synchronous overall.
 int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
   std::lock_guard<std::mutex> lk(d.mu);
   DevGuard g(d.id);
-  for (size_t base = off; base < off + cnt; base += CHUNK) {
-    const size_t m = std::min(CHUNK, off + cnt - base);
-    const size_t m_pad = align_up(m, 64);
-    // layout: inputs | rec | outputs
-    size_t in_bytes = 0;
-    size_t raw_lo = 0, raw_len = 0;
-    switch (j.kind) {
-      case HostJob::RECOVER: in_bytes = m * (32 + 65); break;
-      case HostJob::SENDER: in_bytes = m * (32 * 4 + 1); break;
-      case HostJob::VERIFY: in_bytes = m * (65 + 1 + 32 + 64); break;
-      case HostJob::PRECOMPILE: in_bytes = m * (128 + 4); break;
-      case HostJob::SENDER_RAW:
-        raw_lo = j.offsets[base] - j.offsets[0];
-        raw_len = j.offsets[base + m] - j.offsets[base];
-        in_bytes = align_up(raw_len, 8) + 8 * (m + 1) + tx_rows_bytes(m);
-        break;
+  // a shard big enough to pipeline runs as >= 2 chunks (each still a full resident grid)
+  size_t c = std::min(CHUNK, cnt);
+  if (cnt >= 2 * PIPE_MIN && c > cnt / 2) c = align_up((cnt + EGES_PIPE_PARTS - 1) / EGES_PIPE_PARTS, 64);
+  size_t worst = 0;  // region size: SENDER_RAW depends on the bytes of each chunk
+  for (size_t base = off; base < off + cnt; base += c) worst = std::max(worst, region_for(j, base, std::min(c, off + cnt - base)).total);
+  const int nreg = cnt > c ? 2 : 1;
+  int rc = dev_ensure_buf(d, worst * nreg);
+  if (rc) return rc;
+  // a single chunk has nothing to overlap: one stream, no cross-stream waits (C3 latency)
+  hipStream_t st = d.stream, sx = nreg > 1 ? d.copy : d.stream;
+  HIPCHK(hipStreamWaitEvent(st, d.last, 0));
+  HIPCHK(hipStreamWaitEvent(sx, d.last, 0));
+  struct Pending {
+    size_t base, m;
+    int r;
+    uint8_t* B;
+    Region g;
+  };
+  auto outputs = [&](const Pending& q) -> int {  // D2H of one chunk, on the copy stream
+    uint8_t* o_pub = q.B + q.g.o_out;
+    uint8_t* o_addr = o_pub + q.m * 65;
+    uint8_t* o_st = o_addr + q.m * 32;
+    HIPCHK(hipStreamWaitEvent(sx, d.ev_k[q.r], 0));
+    if (j.pub) HIPCHK(hipMemcpyAsync(j.pub + q.base * 65, o_pub, q.m * 65, hipMemcpyDeviceToHost, sx));
+    const size_t astride = j.kind == HostJob::PRECOMPILE ? 32 : 20;
+    if (j.addr) HIPCHK(hipMemcpyAsync(j.addr + q.base * astride, o_addr, q.m * astride, hipMemcpyDeviceToHost, sx));
+    if (j.status) HIPCHK(hipMemcpyAsync(j.status + q.base, o_st, q.m, hipMemcpyDeviceToHost, sx));
+    if (j.kind == HostJob::SENDER_RAW && j.sighash) {
+      const uint8_t* hs = q.B + align_up(q.g.raw_len, 8) + 8 * (q.m + 1);
+      HIPCHK(hipMemcpyAsync(j.sighash + q.base * 32, hs, q.m * 32, hipMemcpyDeviceToHost, sx));
     }
-    const size_t rec_bytes = (j.kind == HostJob::VERIFY) ? verify_scratch_bytes(m_pad) : recover_scratch_bytes(m_pad);
-    const size_t out_bytes = m * (65 + 32 + 1);
-    const size_t o_in = 0, o_rec = align_up(in_bytes, 256), o_out = o_rec + align_up(rec_bytes, 256);
-    int rc = dev_ensure_buf(d, o_out + out_bytes);
-    if (rc) return rc;
-    uint8_t* B = d.buf;
-    hipStream_t st = d.stream;
-    HIPCHK(hipStreamWaitEvent(st, d.last, 0));
-    uint8_t* o_pub = B + o_out;
+    return EGES_SUCCESS;
+  };
+  Pending prev{};
+  bool have_prev = false;
+  int ci = 0;
+  for (size_t base = off; base < off + cnt; base += c, ++ci) {
+    const size_t m = std::min(c, off + cnt - base);
+    const size_t m_pad = align_up(m, 64);
+    const int r = ci % nreg;
+    const Region rg = region_for(j, base, m);
+    uint8_t* B = d.buf + (size_t)r * worst;
+    uint8_t* o_pub = B + rg.o_out;
     uint8_t* o_addr = o_pub + m * 65;
     uint8_t* o_st = o_addr + m * 32;
+    uint32_t* rec = reinterpret_cast<uint32_t*>(B + rg.o_rec);
+    // --- inputs (copy stream), then the kernels (compute stream)
     if (j.kind == HostJob::RECOVER) {
-      uint8_t* dm = B + o_in;
+      uint8_t* dm = B;
       uint8_t* ds = dm + m * 32;
-      HIPCHK(hipMemcpyAsync(dm, j.a + base * 32, m * 32, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(ds, j.b + base * 65, m * 65, hipMemcpyHostToDevice, st));
-      uint32_t* rec = reinterpret_cast<uint32_t*>(B + o_rec);
+      HIPCHK(hipMemcpyAsync(dm, j.a + base * 32, m * 32, hipMemcpyHostToDevice, sx));
+      HIPCHK(hipMemcpyAsync(ds, j.b + base * 65, m * 65, hipMemcpyHostToDevice, sx));
+      HIPCHK(hipEventRecord(d.ev_in[r], sx));
+      HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
       HIPCHK(launch_prep_ecrecover(dm, ds, (uint32_t)m, (uint32_t)m_pad, rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, j.addr ? o_addr : nullptr, j.pub ? o_pub : nullptr,
                       d.gtab, d.ws};
       HIPCHK(launch_recover(p, d.mb_recover, st));
     } else if (j.kind == HostJob::SENDER) {
-      uint8_t* dh = B + o_in;
+      uint8_t* dh = B;
       uint8_t* dr = dh + m * 32;
       uint8_t* dsv = dr + m * 32;
       uint8_t* dv = dsv + m * 32;
       uint8_t* df = dv + m * 32;
-      HIPCHK(hipMemcpyAsync(dh, j.a + base * 32, m * 32, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(dr, j.b + base * 32, m * 32, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(dsv, j.c + base * 32, m * 32, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(dv, j.d + base * 32, m * 32, hipMemcpyHostToDevice, st));
-      if (j.e) HIPCHK(hipMemcpyAsync(df, j.e + base, m, hipMemcpyHostToDevice, st));
-      uint32_t* rec = reinterpret_cast<uint32_t*>(B + o_rec);
+      HIPCHK(hipMemcpyAsync(dh, j.a + base * 32, m * 32, hipMemcpyHostToDevice, sx));
+      HIPCHK(hipMemcpyAsync(dr, j.b + base * 32, m * 32, hipMemcpyHostToDevice, sx));
+      HIPCHK(hipMemcpyAsync(dsv, j.c + base * 32, m * 32, hipMemcpyHostToDevice, sx));
+      HIPCHK(hipMemcpyAsync(dv, j.d + base * 32, m * 32, hipMemcpyHostToDevice, sx));
+      if (j.e) HIPCHK(hipMemcpyAsync(df, j.e + base, m, hipMemcpyHostToDevice, sx));
+      HIPCHK(hipEventRecord(d.ev_in[r], sx));
+      HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
       HIPCHK(launch_prep_sender(dh, dr, dsv, dv, j.e ? df : nullptr, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id,
                                 rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
       HIPCHK(launch_recover(p, d.mb_recover, st));
     } else if (j.kind == HostJob::PRECOMPILE) {
-      uint8_t* din = B + o_in;
+      uint8_t* din = B;
       uint32_t* dlen = reinterpret_cast<uint32_t*>(din + m * 128);
-      HIPCHK(hipMemcpyAsync(din, j.a + base * 128, m * 128, hipMemcpyHostToDevice, st));
-      if (j.inlen) HIPCHK(hipMemcpyAsync(dlen, j.inlen + base, m * 4, hipMemcpyHostToDevice, st));
-      uint32_t* rec = reinterpret_cast<uint32_t*>(B + o_rec);
+      HIPCHK(hipMemcpyAsync(din, j.a + base * 128, m * 128, hipMemcpyHostToDevice, sx));
+      if (j.inlen) HIPCHK(hipMemcpyAsync(dlen, j.inlen + base, m * 4, hipMemcpyHostToDevice, sx));
+      HIPCHK(hipEventRecord(d.ev_in[r], sx));
+      HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
       HIPCHK(hipMemsetAsync(o_addr, 0, m * 32, st));
       HIPCHK(launch_prep_precompile(din, j.inlen ? dlen : nullptr, (uint32_t)m, (uint32_t)m_pad, rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr + 12, nullptr, d.gtab, d.ws, 32};
       HIPCHK(launch_recover(p, d.mb_recover, st));
     } else if (j.kind == HostJob::SENDER_RAW) {
-      uint8_t* draw = B + o_in;
-      uint64_t* doff = reinterpret_cast<uint64_t*>(draw + align_up(raw_len, 8));
+      uint8_t* draw = B;
+      uint64_t* doff = reinterpret_cast<uint64_t*>(draw + align_up(rg.raw_len, 8));
       uint8_t* hs = reinterpret_cast<uint8_t*>(doff + (m + 1));
       uint8_t* rr = hs + m * 32;
       uint8_t* sr = rr + m * 32;
       uint8_t* vr = sr + m * 32;
       uint8_t* vf = vr + m * 32;
-      if (raw_len) HIPCHK(hipMemcpyAsync(draw, j.a + raw_lo, raw_len, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(doff, j.offsets + base, 8 * (m + 1), hipMemcpyHostToDevice, st));
+      if (rg.raw_len) HIPCHK(hipMemcpyAsync(draw, j.a + rg.raw_lo, rg.raw_len, hipMemcpyHostToDevice, sx));
+      HIPCHK(hipMemcpyAsync(doff, j.offsets + base, 8 * (m + 1), hipMemcpyHostToDevice, sx));
+      HIPCHK(hipEventRecord(d.ev_in[r], sx));
+      HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
       HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, vf, st));
-      uint32_t* rec = reinterpret_cast<uint32_t*>(B + o_rec);
       HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
       HIPCHK(launch_recover(p, d.mb_recover, st));
-      if (j.sighash) HIPCHK(hipMemcpyAsync(j.sighash + base * 32, hs, m * 32, hipMemcpyDeviceToHost, st));
     } else {
-      uint8_t* dp = B + o_in;
+      uint8_t* dp = B;
       uint8_t* dl = dp + m * 65;
       uint8_t* dm = dl + m;
       uint8_t* ds = dm + m * 32;
-      HIPCHK(hipMemcpyAsync(dp, j.a + base * 65, m * 65, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(dl, j.b + base, m, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(dm, j.c + base * 32, m * 32, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(ds, j.d + base * 64, m * 64, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(dp, j.a + base * 65, m * 65, hipMemcpyHostToDevice, sx));
+      HIPCHK(hipMemcpyAsync(dl, j.b + base, m, hipMemcpyHostToDevice, sx));
+      HIPCHK(hipMemcpyAsync(dm, j.c + base * 32, m * 32, hipMemcpyHostToDevice, sx));
+      HIPCHK(hipMemcpyAsync(ds, j.d + base * 64, m * 64, hipMemcpyHostToDevice, sx));
+      HIPCHK(hipEventRecord(d.ev_in[r], sx));
+      HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
       VerifyParams p{dp, dl, dm, ds, (uint32_t)m, o_st, d.gtab, d.ws};
-      verify_scratch_bind(p, B + o_rec, m_pad);
+      verify_scratch_bind(p, B + rg.o_rec, m_pad);
       HIPCHK(launch_verify(p, d.mb_verify, st));
     }
-    HIPCHK(hipEventRecord(d.last, st));
-    if (j.pub) HIPCHK(hipMemcpyAsync(j.pub + base * 65, o_pub, m * 65, hipMemcpyDeviceToHost, st));
-    const size_t astride = j.kind == HostJob::PRECOMPILE ? 32 : 20;
-    if (j.addr) HIPCHK(hipMemcpyAsync(j.addr + base * astride, o_addr, m * astride, hipMemcpyDeviceToHost, st));
-    if (j.status) HIPCHK(hipMemcpyAsync(j.status + base, o_st, m, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipEventRecord(d.ev_k[r], st));
+    // --- the previous chunk's outputs, while this chunk computes
+    if (have_prev) {
+      rc = outputs(prev);
+      if (rc) return rc;
+    }
+    prev = Pending{base, m, r, B, rg};
+    have_prev = true;
   }
+  if (have_prev) {
+    rc = outputs(prev);
+    if (rc) return rc;
+  }
+  HIPCHK(hipEventRecord(d.last, sx));
+  HIPCHK(hipStreamSynchronize(sx));
   return EGES_SUCCESS;
 }
 
@@ -485,6 +558,11 @@ void eges_shutdown(void) {
     (void)hipFree(d->ws);
     if (d->buf) (void)hipFree(d->buf);
     (void)hipEventDestroy(d->last);
+    for (int r = 0; r < 2; ++r) {
+      (void)hipEventDestroy(d->ev_in[r]);
+      (void)hipEventDestroy(d->ev_k[r]);
+    }
+    (void)hipStreamDestroy(d->copy);
     (void)hipStreamDestroy(d->stream);
   }
   for (Dev* d : g_devs) delete d;
