@@ -1,0 +1,59 @@
+"""Concurrent callers through the C-ABI (SURVEY §8(b) threading contract).
+
+The reference calls one read-only libsecp256k1 context from any goroutine with no locks
+(crypto/secp256k1/secp256.go:45-52). libeges must give the same answers when several host
+threads call its batch and single-item entries at once (ctypes releases the GIL for the
+call). Every result is checked bit-exactly against the golden fixtures.
+"""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def test_concurrent_batch_and_single_item_callers(engine):
+    from eges_amd._lib import lib
+    g = load_golden("recover.npz")
+    msg, sig, exp_pub, exp_st = g["msg"], g["sig"], g["pub"], g["status"]
+    n = msg.shape[0]
+    errors = []
+
+    def batch_worker(t):
+        try:
+            for rep in range(3):
+                lo = (t * 397 + rep * 131) % n
+                sel = np.arange(lo, lo + 700) % n  # ragged, wraps around the fixture
+                pub, _, st = engine.ecrecover_batch(msg[sel], sig[sel])
+                if not np.array_equal(st, exp_st[sel]) or not np.array_equal(pub, exp_pub[sel]):
+                    errors.append(("batch", t, rep))
+        except Exception as e:  # surfaced in the main thread
+            errors.append(("batch-exc", t, repr(e)))
+
+    def single_worker(t):
+        try:
+            out = (ctypes.c_ubyte * 65)()
+            for i in range(t, n, 97):
+                m = msg[i].tobytes()
+                s = sig[i].tobytes()
+                if s[64] >= 4:
+                    continue  # checkSignature rejects these before the C call (secp256.go:171-179)
+                rc = lib.eges_ecdsa_recover(out, s, m)
+                want = 1 if exp_st[i] == 0 else 0
+                if rc != want or (rc == 1 and bytes(out) != exp_pub[i].tobytes()):
+                    errors.append(("single", t, i, rc))
+        except Exception as e:
+            errors.append(("single-exc", t, repr(e)))
+
+    threads = [threading.Thread(target=batch_worker, args=(t,)) for t in range(4)]
+    threads += [threading.Thread(target=single_worker, args=(t,)) for t in range(4)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=100)
+    assert not any(th.is_alive() for th in threads), "a caller thread did not return"
+    assert not errors, errors[:10]
