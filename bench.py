@@ -19,11 +19,14 @@ Metric (BASELINE.json): "secp256k1 ecrecover+address/sec at 1/8 MI355X; % of INT
 --config c5 (configs[4]): 10% invalid signatures (high-s, bad recid / chain id, r >= n, s >= n,
   non-residue R, zero r / s) through crypto.Ecrecover and types.Sender semantics, statuses
   checked bit-exact against their by-construction expectation, plus VerifySignature mode.
+--config c1 (configs[0]): types.Sender over 10k EIP-155 transfers (SURVEY.md §8(d) C1 shape:
+  nonce i, gasPrice 1, gas 21000, value 1, empty data, chainId 930412) handed over as wire bytes
+  through eges_sender_raw_batch -> txs/s, next to the reference libsecp256k1 on all host cores.
 --config verify: crypto.VerifySignature throughput (65-byte and 33-byte keys).
 --config c2host: configs[1]'s batch handed over as host (pageable) buffers through
   eges_ecrecover_batch — the PCIe-inclusive rate a Go caller sees (never `value` of the c2 line).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config c2|c3|c4|c5|verify]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config c1|c2|c2host|c3|c3raw|c4|c5|verify]
 """
 import argparse
 import ctypes
@@ -54,7 +57,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=None, help="c2: signatures per GPU; c4: total signatures")
-    ap.add_argument("--config", default="c2", choices=["c2", "c2host", "c3", "c3raw", "c4", "c5", "verify"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2host", "c3", "c3raw", "c4", "c5", "verify"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -280,6 +283,63 @@ def run_block_latency(c):
     c.finish(line, ok)
 
 
+# ------------------------------------------------------------------ c1: 10k EIP-155 transfers
+def run_c1(c):
+    import numpy as np
+    torch, a = c.torch, c.args
+    from eges_amd import txs
+    from eges_amd._lib import SIGNER_EIP155
+    n = a.batch or 10000
+    sighash = txs.c1_sighashes(0, n)
+    # the GPU synthetic signer uses C1's keys (tests/test_c1.py pins them against the reference's
+    # pubkey_create); its nonces are not RFC6979, which does not change what recovery computes
+    sig_d, exp_d = c.eges.synth_sign_msg_dev(torch.from_numpy(sighash).to(c.dev), 0, stream=c.sp)
+    torch.cuda.synchronize()
+    sig_h, exp_h = sig_d.cpu().numpy(), exp_d.cpu().numpy()
+    packed = c.eges.pack_raw(txs.c1_raw(0, sig_h))
+    iters = max(20, a.steps * 4)
+    lat = []
+    ok = True
+    for i in range(a.warmup + iters):
+        t0 = time.perf_counter()
+        addr, st, _ = c.eges.sender_raw_batch(packed, SIGNER_EIP155, txs.GEEC_CHAIN_ID)
+        dt = time.perf_counter() - t0
+        if i >= a.warmup:
+            lat.append(dt)
+        if i == 0:
+            ok = bool((st == 0).all()) and np.array_equal(addr, exp_h)
+    med = float(np.median(lat))
+    cpu = None
+    if not a.no_cpu_baseline:
+        try:
+            from oracle import RefLib, have_ref
+            if have_ref():
+                ref = RefLib()
+                threads = min(16, os.cpu_count() or 1)
+                t0 = time.perf_counter()
+                ref.ecrecover_batch_mt(sighash, sig_h, 1)
+                dt1 = time.perf_counter() - t0
+                t0 = time.perf_counter()
+                _, _, ret = ref.ecrecover_batch_mt(sighash, sig_h, threads)
+                dtn = time.perf_counter() - t0
+                assert (ret == 1).all()
+                cpu = {"value": round(n / dtn, 1), "unit": "txs/s", "cores": threads, "kind": "reference",
+                       "single_core_txs_per_s": round(n / dt1, 1),
+                       "sample": f"the same {n} transfers: reference libsecp256k1 ecrecover (cgo build flags) + Keccak "
+                                 f"address, {threads} pthreads ({dtn:.2f} s; 1 core {dt1:.2f} s); sighash RLP + Keccak "
+                                 "excluded on the CPU side only (the GPU value includes decode and sighash)"}
+        except Exception:
+            cpu = None
+    line = {"metric": "types.Sender over 10k synthetic EIP-155-signed transfers (configs[0]), from wire bytes",
+            "value": round(n / med, 1), "unit": "txs/s", "ms_per_batch": round(med * 1e3, 3), "n_gpus": 1,
+            "steps": iters, "warmup": a.warmup, "higher_is_better": True, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": f"configs[0]: {n} EIP-155 transfers (nonce i, gasPrice 1, gas 21000, value 1, "
+                                   "empty data, chainId 930412) as 10-field txdata RLP through eges_sender_raw_batch "
+                                   "(pageable host buffers: H2D + GPU decode + sighash RLP/Keccak + recovery + D2H)",
+                       "correct": ok}, "cpu_baseline": cpu}
+    c.finish(line, ok)
+
+
 # ------------------------------------------------------------------ c5: adversarial mix
 def run_adversarial(c):
     import numpy as np
@@ -417,7 +477,9 @@ def run_host_throughput(c):
 def main():
     args = parse()
     c = Ctx(args)
-    if args.config == "c2":
+    if args.config == "c1":
+        run_c1(c)
+    elif args.config == "c2":
         run_throughput(c, strong=False)
     elif args.config == "c4":
         run_throughput(c, strong=True)

@@ -128,6 +128,50 @@ def geec_block_raw(first, sig65, payload=100, chain_id=GEEC_CHAIN_ID, is_geec=Tr
     return out
 
 
+def encode_geec_tx(nonce, price, gas, to, value, data, is_geec, v, r, s):
+    """One transaction in the 10-field Geec txdata wire form (core/types/transaction.go:59-76)."""
+    return rlp_list([rlp_uint(nonce), rlp_uint(price), rlp_uint(gas), rlp_bytes(to or b""), rlp_uint(value),
+                     rlp_bytes(data), b"\x01" if is_geec else b"\x80", rlp_uint(v), rlp_uint(r), rlp_uint(s)])
+
+
+# ------------------------------------------------------------------ C1: 10k EIP-155 transfers
+C1_PRICE, C1_GAS, C1_VALUE = 1, 21000, 1
+
+
+def c1_key(i):
+    """SURVEY.md §8(d) C1 key of transfer i: Keccak256("eges-key" || u64le(i)) mod n, skipping 0
+    (the same derivation as the GPU synthetic signer, k_synth.hip)."""
+    from .workloads import N
+    k = int.from_bytes(_keccak(b"eges-key" + int(i).to_bytes(8, "little")), "big") % N
+    return k or 1
+
+
+def c1_to(i):
+    """Recipient of transfer i: Keccak256("eges-to" || u64le(i))[12:]."""
+    return _keccak(b"eges-to" + int(i).to_bytes(8, "little"))[12:]
+
+
+def c1_sighashes(first, n, chain_id=GEEC_CHAIN_ID):
+    """EIP155Signer(chain_id).Hash of C1 transfers first..first+n-1: nonce i, gasPrice 1,
+    gas 21000, value 1, empty data (BASELINE.json configs[0]). Returns (n, 32) uint8."""
+    out = np.zeros((n, 32), np.uint8)
+    for j in range(n):
+        i = first + j
+        out[j] = np.frombuffer(eip155_sighash(i, C1_PRICE, C1_GAS, c1_to(i), C1_VALUE, b"", chain_id), np.uint8)
+    return out
+
+
+def c1_raw(first, sig65, chain_id=GEEC_CHAIN_ID):
+    """C1 transfers signed with sig65 (R || S || recid) under EIP155Signer, as wire bytes
+    (10-field txdata, IsGeecTxn false: ordinary user transfers)."""
+    out = []
+    for j, sg in enumerate(np.ascontiguousarray(sig65, np.uint8)):
+        i = first + j
+        out.append(encode_geec_tx(i, C1_PRICE, C1_GAS, c1_to(i), C1_VALUE, b"", False, eip155_v(int(sg[64]), chain_id),
+                                  int.from_bytes(sg[:32].tobytes(), "big"), int.from_bytes(sg[32:64].tobytes(), "big")))
+    return out
+
+
 def sender_rows(sig65, chain_id=GEEC_CHAIN_ID):
     """R || S || recid signatures (n, 65) -> the r, s, v rows (n, 32) of eges_sender_batch for
     EIP-155-signed transactions (V = recid + 35 + 2 chainId)."""
