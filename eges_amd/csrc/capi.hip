@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -58,8 +59,23 @@ struct Dev {
   int mb_recover = 0, mb_verify = 0, mb_synth = 0;
   uint8_t* buf = nullptr;  // per-call device scratch, grown on demand
   size_t buf_cap = 0;
+  // overlapped recover launches (EGES_OVERLAP): a second stream, workspace and its events
+  hipStream_t aux = nullptr;
+  uint32_t* ws2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::mutex mu;
 };
+
+// EGES_OVERLAP=S (S >= 2): a device-resident recover batch runs as S launches alternating
+// between two streams with their own workspaces, so each launch's tail (its slowest waves)
+// overlaps the next launch's start. 0/1 = one launch per CHUNK (default).
+static int overlap_parts() {
+  static const int v = [] {
+    const char* e = std::getenv("EGES_OVERLAP");
+    return e ? std::max(0, std::atoi(e)) : 0;
+  }();
+  return v;
+}
 
 std::mutex g_mu;
 std::vector<Dev*> g_devs;
@@ -161,8 +177,43 @@ extern "C" size_t eges_diag_read_stamps(uint64_t* out, size_t max_waves) {
 }
 #endif
 
+int run_recover_dev_overlap(Dev& d, const uint8_t* msg, const uint8_t* sig, size_t n, uint8_t* pub, uint8_t* addr,
+                            uint8_t* status, hipStream_t st, int parts) {
+  const size_t per = std::min(CHUNK, (n + parts - 1) / parts);
+  const size_t n_pad = align_up(per, 64);
+  const size_t region = align_up(recover_scratch_bytes(n_pad), 256);
+  int rc = dev_ensure_buf(d, 2 * region);
+  if (rc) return rc;
+  if (!d.aux) {
+    HIPCHK(hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&d.ev_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&d.ev_join, hipEventDisableTiming));
+    const int mb = std::max(d.mb_recover, std::max(d.mb_verify, d.mb_synth));
+    HIPCHK(hipMalloc(&d.ws2, ws_bytes_per_block() * (size_t)mb));
+  }
+  Serial ser(d, st);
+  HIPCHK(hipEventRecord(d.ev_fork, st));
+  HIPCHK(hipStreamWaitEvent(d.aux, d.ev_fork, 0));
+  int j = 0;
+  for (size_t off = 0; off < n; off += per, ++j) {
+    const uint32_t m = (uint32_t)std::min(per, n - off);
+    hipStream_t sj = (j & 1) ? d.aux : st;
+    uint32_t* rec = reinterpret_cast<uint32_t*>(d.buf + (j & 1) * region);
+    HIPCHK(launch_prep_ecrecover(msg + off * 32, sig + off * 65, m, (uint32_t)n_pad, rec, sj));
+    RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr ? addr + off * 20 : nullptr, pub ? pub + off * 65 : nullptr,
+                    d.gtab, (j & 1) ? d.ws2 : d.ws};
+    HIPCHK(launch_recover(p, d.mb_recover, sj));
+  }
+  HIPCHK(hipEventRecord(d.ev_join, d.aux));
+  HIPCHK(hipStreamWaitEvent(st, d.ev_join, 0));
+  return EGES_SUCCESS;
+}
+
 int run_recover_dev(Dev& d, const uint8_t* msg, const uint8_t* sig, size_t n, uint8_t* pub, uint8_t* addr,
                     uint8_t* status, hipStream_t st) {
+  const int parts = overlap_parts();
+  if (parts >= 2 && n >= (size_t)parts * 64 * 1024)
+    return run_recover_dev_overlap(d, msg, sig, n, pub, addr, status, st, parts);
   const size_t c = std::min(n, CHUNK);
   const size_t n_pad = align_up(c, 64);
   int rc = dev_ensure_buf(d, recover_scratch_bytes(n_pad));
@@ -554,6 +605,7 @@ void eges_shutdown(void) {
     std::lock_guard<std::mutex> dl(d->mu);
     DevGuard g(d->id);
     (void)hipStreamSynchronize(d->stream);
+    (void)hipEventSynchronize(d->last);  // the last engine work, on whichever stream the caller gave
     (void)hipFree(d->gtab);
     (void)hipFree(d->ws);
     if (d->buf) (void)hipFree(d->buf);
@@ -563,6 +615,12 @@ void eges_shutdown(void) {
       (void)hipEventDestroy(d->ev_k[r]);
     }
     (void)hipStreamDestroy(d->copy);
+    if (d->aux) {
+      (void)hipStreamDestroy(d->aux);
+      (void)hipEventDestroy(d->ev_fork);
+      (void)hipEventDestroy(d->ev_join);
+      (void)hipFree(d->ws2);
+    }
     (void)hipStreamDestroy(d->stream);
   }
   for (Dev* d : g_devs) delete d;
