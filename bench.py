@@ -118,10 +118,11 @@ class Ctx:
         # gloo for the timing collectives. The driver's multi-GPU runs leave both unset.
         if "EGES_BENCH_DEVICE" in os.environ:
             self.local = int(os.environ["EGES_BENCH_DEVICE"])
+        # bind the rank's GPU before the process group exists, so RCCL's barrier uses it
+        torch.cuda.set_device(self.local)
         if self.world > 1:
             backend = os.environ.get("EGES_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
             dist.init_process_group(backend=backend)
-        torch.cuda.set_device(self.local)
         import eges_amd
         self.eges = eges_amd
         eges_amd.init(1 << self.local)
