@@ -62,3 +62,16 @@ def test_synth_roundtrip(engine, oracle):
         ost, pub = oracle.recover_pubkey(m[i].tobytes(), s[i].tobytes())
         assert ost == 0
         assert oracle.pub_to_addr(pub) == e[i].tobytes()
+
+
+def test_multi_chunk_overlapped_launches(engine):
+    """A device batch larger than one pass (2^21 signatures) runs as launches alternating between
+    two streams with separate workspaces (capi.hip run_recover_dev_overlap): every address of a
+    ragged 2^21 + 4099 batch must still equal the synthetic signer's expectation."""
+    import torch
+    n = (1 << 21) + 4099
+    msg, sig, exp = engine.synth_sign_dev(1 << 30, n, 0)
+    _, addr, st = engine.ecrecover_batch_dev(msg, sig)
+    torch.cuda.synchronize()
+    assert bool((st == 0).all().item())
+    assert torch.equal(addr, exp)
