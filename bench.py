@@ -48,6 +48,12 @@ W_VERIFY65 = 242_216
 # v_mad_u64_u32 / v_add_co / v_addc at 4.4-4.9 cyc per wave64 instruction per SIMD, i.e. this
 # rate; only v_add_u32/v_bitop3 issue at the 2x rate).
 PEAK_INT32_OPS = 256 * 64 * 2.4e9  # 3.93e13 lane-ops/s
+# The same achieved rate against two other named denominators (bench line "peaks_T"):
+#  - the guide (MI355X_MICROARCH.md): one wave64 VALU instruction per 2 cycles per SIMD,
+#    1024 SIMDs x 32 lane-ops/clk x 2.4 GHz = 7.86e13 (full-rate 32-bit ops);
+#  - measured: v_mad_u64_u32 at 4 waves/SIMD, 31.6e12 lane-ops/s (profiles/r01/ubench_valu.txt).
+PEAK_GUIDE_VALU = 1024 * 32 * 2.4e9
+PEAK_MEASURED_MAD = 31.61e12
 C4_TOTAL = 64 << 20
 
 
@@ -63,15 +69,38 @@ def parse():
     return ap.parse_args()
 
 
+def host_cpus():
+    """CPUs granted to this process on the box: nproc (os.cpu_count()), affinity
+    (len(sched_getaffinity)), the cgroup CPU quota (None when unset) and the threads the
+    baseline uses: one pthread per granted CPU, i.e. the affinity count, capped by a cgroup
+    quota when one is set (more threads than the quota would only time-share)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except Exception:
+        quota = None
+    threads = aff if quota is None else max(1, min(aff, int(quota + 0.999)))
+    return {"nproc": nproc, "affinity": aff, "cgroup_cpus": quota, "threads": threads}
+
+
 def cpu_baseline(msg_h, sig_h, target_s):
     """Reference libsecp256k1 (compiled in place, oracle/_ref) on the host cores: the
-    goroutine-parallel types.Sender/Ecrecover path restated as one pthread per core.
+    goroutine-parallel types.Sender/Ecrecover path restated as one pthread per granted CPU.
     Returns the cpu_baseline object or None."""
     try:
         from oracle import Oracle, RefLib, have_ref
     except Exception:
         return None
-    threads = min(16, os.cpu_count() or 1)  # the GPU box grants 16 CPUs per GPU
+    host = host_cpus()
+    threads = int(os.environ.get("EGES_CPU_THREADS", host["threads"]))
     if have_ref():
         ref = RefLib()
         # calibrate on a small slice, then size the sample to ~target_s
@@ -85,6 +114,9 @@ def cpu_baseline(msg_h, sig_h, target_s):
         dt = time.perf_counter() - t0
         assert (ret == 1).all()
         return {"value": round(n / dt, 1), "unit": "sigs/s", "cores": threads, "kind": "reference",
+                "host": dict(host, threads=threads),
+                "ratio_basis": "the GPU/CPU ratio is per granted CPU set of the host (all threads above), "
+                               "not per core",
                 "sample": f"first {n} signatures of the same synthetic batch: reference libsecp256k1 ecrecover "
                           f"(cgo build flags) + Keccak address, {threads} pthreads, {dt:.1f} s"}
     o = Oracle()
@@ -92,18 +124,41 @@ def cpu_baseline(msg_h, sig_h, target_s):
     t0 = time.perf_counter()
     o.recover_batch(msg_h[:n], sig_h[:n])
     dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 1), "unit": "sigs/s", "cores": 1, "kind": "port",
+    return {"value": round(n / dt, 1), "unit": "sigs/s", "cores": 1, "kind": "port", "host": dict(host, threads=1),
             "sample": f"first {n} of the batch, oracle restatement, 1 thread"}
 
 
-def read_traffic(batch):
+def kernel_src_hash():
+    """SHA-256 over the kernel sources and headers libeges.so is built from. The GPU box gets no
+    .git, so a PMC summary is tied to the sources it was collected from, not to a commit id."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "eges_amd", "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cuh"))
+                   + glob.glob(os.path.join(csrc, "*.h"))) + [os.path.join(ROOT, "include", "eges.h")]
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def read_pmc(kernel, batch):
+    """Counter summary of `kernel` at `batch` from profiles/pmc_traffic.json (tools/pmc.sh +
+    tools/pmc_summary.py), only when it was collected from the same kernel sources; else None."""
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(tf) as f:
             tj = json.load(f)
-        return tj.get("bytes_per_launch") if tj.get("batch") == batch else None
     except Exception:
         return None
+    if tj.get("src_sha256") != kernel_src_hash():
+        return None
+    ent = tj.get("kernels", {}).get(kernel)
+    if not ent or ent.get("batch") != batch:
+        return None
+    return ent
 
 
 class Ctx:
@@ -131,13 +186,18 @@ class Ctx:
         self.stream = torch.cuda.Stream(self.dev)
         self.sp = self.stream.cuda_stream
 
-    def timed(self, step):
+    def timed(self, step, reset=None):
         """W untimed steps, then K steps between barrier + synchronize on both sides; returns
-        (max elapsed over ranks, mean per-step time from HIP events on the engine's stream)."""
+        (max elapsed over ranks, mean per-step time from HIP events on the engine's stream).
+        `reset` (untimed) clears the outputs after the warmup, so the check that follows reads
+        what the timed steps wrote."""
         torch, dist, a = self.torch, self.dist, self.args
         for _ in range(a.warmup):
             step()
         torch.cuda.synchronize()
+        if reset is not None:
+            reset()
+            torch.cuda.synchronize()
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
         if self.world > 1:
             dist.barrier()
@@ -170,12 +230,34 @@ class Ctx:
             sys.exit(1)
 
 
-def roofline(per_gpu_rate, work, batch, kern_ms):
-    achieved = per_gpu_rate * work / 1e12
-    peak = PEAK_INT32_OPS / 1e12
-    return {"bound": "valu", "achieved": round(achieved, 3), "peak": round(peak, 2),
-            "unit": "T INT32 lane-ops/s (reference-algorithm accounting, SURVEY.md 8(d))",
-            "frac": round(achieved / peak, 4), "traffic": read_traffic(batch), "kernel_ms": round(kern_ms, 3)}
+def roofline(per_gpu_rate, work, batch, kern_ms, kernel="eges::recover_kernel"):
+    """Roofline object of the dominant kernel. `frac` keeps the SURVEY.md 8(d) contract
+    denominator; the same achieved rate is also given against the guide's VALU issue rate and
+    the measured v_mad_u64_u32 rate, each named. With a PMC summary of the same kernel sources:
+    HBM-side traffic and the counter-derived VALU utilisation."""
+    achieved = per_gpu_rate * work
+    r = {"bound": "valu", "achieved": round(achieved / 1e12, 3), "peak": round(PEAK_INT32_OPS / 1e12, 2),
+         "unit": "T INT32 lane-ops/s (reference-algorithm accounting, SURVEY.md 8(d))",
+         "frac": round(achieved / PEAK_INT32_OPS, 4),
+         "frac_vs_guide_valu_issue": round(achieved / PEAK_GUIDE_VALU, 4),
+         "frac_vs_measured_mad_rate": round(achieved / PEAK_MEASURED_MAD, 4),
+         "peaks_T": {"contract": round(PEAK_INT32_OPS / 1e12, 2), "guide_valu_issue": round(PEAK_GUIDE_VALU / 1e12, 2),
+                     "measured_v_mad_u64_u32": round(PEAK_MEASURED_MAD / 1e12, 2)},
+         "traffic": None, "kernel_ms": round(kern_ms, 3)}
+    pmc = read_pmc(kernel, batch)
+    if pmc:
+        # FETCH_SIZE (KB, x2: gfx950 correction) + WRITE_SIZE (KB): L2 <-> fabric (MALL / HBM) bytes
+        r["traffic"] = pmc.get("bytes_per_launch")
+        insts = pmc.get("SQ_INSTS_VALU")
+        if insts and batch:
+            lane_insts = insts * 64
+            r["counters"] = {
+                "source": "profiles/pmc_traffic.json (PMC passes of the same kernel sources, src_sha256)",
+                "valu_lane_insts_per_sig": round(lane_insts / batch),
+                "int64_class_share": round(pmc.get("SQ_INSTS_VALU_INT64", 0) / insts, 4),
+                "valu_util_vs_contract": round(lane_insts / (kern_ms / 1e3) / PEAK_INT32_OPS, 4),
+                "valu_util_vs_guide": round(lane_insts / (kern_ms / 1e3) / PEAK_GUIDE_VALU, 4)}
+    return r
 
 
 # ------------------------------------------------------------------ c2 / c4: throughput
@@ -202,11 +284,14 @@ def run_throughput(c, strong):
                                            None, ctypes.c_void_p(addr.data_ptr()), ctypes.c_void_p(status.data_ptr()),
                                            ctypes.c_void_p(c.sp)))
 
-    step()
-    torch.cuda.synchronize()
-    # correctness of the measured path: every address equals the signer's (by construction)
+    def reset():
+        addr.zero_()
+        status.fill_(0xFF)
+
+    elapsed, kern_ms = c.timed(step, reset)
+    # correctness of the measured launches: every address the timed steps wrote equals the
+    # signer's (by construction)
     ok = bool((status == 0).all().item()) and bool(torch.equal(addr, exp_addr))
-    elapsed, kern_ms = c.timed(step)
     elapsed, kern_ms, bad = c.reduce_max(elapsed, kern_ms, 0.0 if ok else 1.0)
     ok = bad == 0.0
     value = total * a.steps / elapsed
@@ -316,7 +401,7 @@ def run_c1(c):
             from oracle import RefLib, have_ref
             if have_ref():
                 ref = RefLib()
-                threads = min(16, os.cpu_count() or 1)
+                threads = int(os.environ.get("EGES_CPU_THREADS", host_cpus()["threads"]))
                 t0 = time.perf_counter()
                 ref.ecrecover_batch_mt(sighash, sig_h, 1)
                 dt1 = time.perf_counter() - t0
@@ -370,8 +455,16 @@ def run_adversarial(c):
         c.eges.sender_batch_dev(msg, rd, sd, vd, vf, SIGNER_EIP155, txs.GEEC_CHAIN_ID, addr=addr2, status=st2,
                                 stream=c.sp)
 
-    el_e, k_e = c.timed(step_e)
-    el_s, k_s = c.timed(step_s)
+    def reset_e():
+        addr.fill_(0xAB)
+        st.fill_(0xFF)
+
+    def reset_s():
+        addr2.fill_(0xAB)
+        st2.fill_(0xFF)
+
+    el_e, k_e = c.timed(step_e, reset_e)
+    el_s, k_s = c.timed(step_s, reset_s)
     got_e, got_s = st.cpu().numpy(), st2.cpu().numpy()
     a_e, a_s, ex = addr.cpu().numpy(), addr2.cpu().numpy(), exp_addr.cpu().numpy()
     okm_e = got_e == 0
@@ -431,7 +524,7 @@ def run_verify(c):
     def step():
         c.eges.verify_batch_dev(pd, ld, msg, sd, ok=ok_d, stream=c.sp)
 
-    elapsed, kern_ms = c.timed(step)
+    elapsed, kern_ms = c.timed(step, lambda: ok_d.fill_(0xFF))
     got = ok_d.cpu().numpy()
     ok = bool(np.array_equal(got, expect))
     line = {"metric": "crypto.VerifySignature/sec on 1 MI355X", "value": round(B * a.steps / elapsed, 1),
@@ -440,7 +533,7 @@ def run_verify(c):
             "config": {"workload": "VerifySignature over 1M signatures: 75% 65-byte / 25% 33-byte keys, 10% mutated "
                                    "(high-s, wrong key, hybrid 06/07)", "batch": B, "correct": ok,
                        "mismatches": int((got != expect).sum())},
-            "roofline": roofline(B / (kern_ms / 1e3), W_VERIFY65, None, kern_ms)}
+            "roofline": roofline(B / (kern_ms / 1e3), W_VERIFY65, B, kern_ms, kernel="eges::verify_kernel")}
     c.finish(line, ok)
 
 

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -22,7 +23,7 @@ namespace {
 
 using namespace eges;
 
-constexpr size_t CHUNK = size_t(1) << 21;  // signatures per device pass (bounds scratch memory)
+constexpr size_t CHUNK = PASS_MAX;  // signatures per device pass (bounds scratch memory)
 // host-buffer shards of at least 2 * PIPE_MIN items are split into >= 2 pipelined chunks
 constexpr size_t PIPE_MIN = size_t(1) << 18;
 #ifndef EGES_PIPE_PARTS
@@ -41,6 +42,11 @@ int set_err(int rc, const char* fmt, ...) {
   return rc;
 }
 
+int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e && *e ? std::atoi(e) : dflt;
+}
+
 #define HIPCHK(expr)                                                                                \
   do {                                                                                              \
     hipError_t e_ = (expr);                                                                         \
@@ -57,6 +63,7 @@ struct Dev {
   uint32_t* gtab = nullptr;
   uint32_t* ws = nullptr;
   int mb_recover = 0, mb_verify = 0, mb_synth = 0;
+  int ws_blocks = 0;  // blocks ws (and ws2) hold: every launch's grid is checked against it
   uint8_t* buf = nullptr;  // per-call device scratch, grown on demand
   size_t buf_cap = 0;
   // overlapped recover launches (EGES_OVERLAP): a second stream, workspace and its events
@@ -64,7 +71,9 @@ struct Dev {
   uint32_t* ws2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::mutex mu;
+  ~Dev();
 };
+using DevPtr = std::shared_ptr<Dev>;
 
 // Overlapped launches: a device-resident recover batch runs as launches alternating between
 // two streams with their own workspaces, so each launch's tail (its slowest waves) overlaps the
@@ -81,7 +90,7 @@ static int overlap_parts(size_t n) {
 }
 
 std::mutex g_mu;
-std::vector<Dev*> g_devs;
+std::vector<DevPtr> g_devs;
 bool g_inited = false;
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -112,13 +121,13 @@ int dev_ensure_buf(Dev& d, size_t bytes) {
   return EGES_SUCCESS;
 }
 
-int init_device(int id, Dev** out) {
+int init_device(int id, DevPtr* out) {
   hipDeviceProp_t prop;
   HIPCHK(hipGetDeviceProperties(&prop, id));
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
     return set_err(EGES_E_NODEVICE, "device %d is %s, the engine is built for gfx950 only", id, prop.gcnArchName);
   DevGuard g(id);
-  Dev* d = new Dev();
+  DevPtr d = std::make_shared<Dev>();
   d->id = id;
   d->cus = prop.multiProcessorCount;
   HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
@@ -131,14 +140,47 @@ int init_device(int id, Dev** out) {
   d->mb_recover = occupancy_recover() * d->cus;
   d->mb_verify = occupancy_verify() * d->cus;
   d->mb_synth = occupancy_synth() * d->cus;
+  if (const int cap = env_int("EGES_TEST_MAX_BLOCKS", 0); cap > 0) {  // tests: a small device
+    d->mb_recover = std::min(d->mb_recover, cap);
+    d->mb_verify = std::min(d->mb_verify, cap);
+    d->mb_synth = std::min(d->mb_synth, cap);
+  }
+  // A full pass may need more blocks than are resident (grid_for_lane_serial caps the
+  // signatures per thread at MAX_SLOTS): the workspace covers the larger of the two.
   const int mb = std::max(d->mb_recover, std::max(d->mb_verify, d->mb_synth));
+  d->ws_blocks = std::max(mb, std::max(lane_serial_grid((uint32_t)CHUNK, d->mb_recover),
+                                       lane_serial_grid((uint32_t)CHUNK, d->mb_verify)));
   HIPCHK(hipMalloc(&d->gtab, gtab_bytes()));
-  HIPCHK(hipMalloc(&d->ws, ws_bytes_per_block() * (size_t)mb));
+  HIPCHK(hipMalloc(&d->ws, ws_bytes_per_block() * (size_t)d->ws_blocks));
   HIPCHK(launch_init_gtab(d->gtab, d->stream));
   HIPCHK(hipEventRecord(d->last, d->stream));
   HIPCHK(hipStreamSynchronize(d->stream));
-  *out = d;
+  *out = std::move(d);
   return EGES_SUCCESS;
+}
+
+// Resources go when the last reference does: eges_shutdown drops the registry's references,
+// and a call still in flight keeps its device alive until it returns.
+Dev::~Dev() {
+  DevGuard g(id);
+  if (stream) (void)hipStreamSynchronize(stream);
+  if (last) (void)hipEventSynchronize(last);  // the last engine work, on whichever stream the caller gave
+  if (gtab) (void)hipFree(gtab);
+  if (ws) (void)hipFree(ws);
+  if (buf) (void)hipFree(buf);
+  if (last) (void)hipEventDestroy(last);
+  for (int r = 0; r < 2; ++r) {
+    if (ev_in[r]) (void)hipEventDestroy(ev_in[r]);
+    if (ev_k[r]) (void)hipEventDestroy(ev_k[r]);
+  }
+  if (copy) (void)hipStreamDestroy(copy);
+  if (aux) {
+    (void)hipStreamDestroy(aux);
+    (void)hipEventDestroy(ev_fork);
+    (void)hipEventDestroy(ev_join);
+    (void)hipFree(ws2);
+  }
+  if (stream) (void)hipStreamDestroy(stream);
 }
 
 int ensure_init() {
@@ -150,8 +192,9 @@ int ensure_init() {
   return rc;
 }
 
-Dev* dev_by_id(int id) {
-  for (Dev* d : g_devs)
+DevPtr dev_by_id(int id) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (const DevPtr& d : g_devs)
     if (d->id == id) return d;
   return nullptr;
 }
@@ -191,8 +234,7 @@ int run_recover_dev_overlap(Dev& d, const uint8_t* msg, const uint8_t* sig, size
     HIPCHK(hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&d.ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&d.ev_join, hipEventDisableTiming));
-    const int mb = std::max(d.mb_recover, std::max(d.mb_verify, d.mb_synth));
-    HIPCHK(hipMalloc(&d.ws2, ws_bytes_per_block() * (size_t)mb));
+    HIPCHK(hipMalloc(&d.ws2, ws_bytes_per_block() * (size_t)d.ws_blocks));
   }
   Serial ser(d, st);
   HIPCHK(hipEventRecord(d.ev_fork, st));
@@ -205,7 +247,7 @@ int run_recover_dev_overlap(Dev& d, const uint8_t* msg, const uint8_t* sig, size
     HIPCHK(launch_prep_ecrecover(msg + off * 32, sig + off * 65, m, (uint32_t)n_pad, rec, sj));
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr ? addr + off * 20 : nullptr, pub ? pub + off * 65 : nullptr,
                     d.gtab, (j & 1) ? d.ws2 : d.ws};
-    HIPCHK(launch_recover(p, d.mb_recover, sj));
+    HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, sj));
   }
   HIPCHK(hipEventRecord(d.ev_join, d.aux));
   HIPCHK(hipStreamWaitEvent(st, d.ev_join, 0));
@@ -232,9 +274,9 @@ int run_recover_dev(Dev& d, const uint8_t* msg, const uint8_t* sig, size_t n, ui
     if (!g_stamps) HIPCHK(hipMalloc(&g_stamps, (size_t)d.mb_recover * 4 /* waves per block */ * 8 * sizeof(uint64_t)));
     g_stamp_waves = (size_t)d.mb_recover * 4 /* waves per block */;
     HIPCHK(hipMemsetAsync(g_stamps, 0, g_stamp_waves * 8 * sizeof(uint64_t), st));
-    HIPCHK(launch_recover_stamped(p, d.mb_recover, st, g_stamps));
+    HIPCHK(launch_recover_stamped(p, d.mb_recover, d.ws_blocks, st, g_stamps));
 #else
-    HIPCHK(launch_recover(p, d.mb_recover, st));
+    HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, st));
 #endif
   }
   return EGES_SUCCESS;
@@ -254,7 +296,7 @@ int run_sender_dev(Dev& d, const uint8_t* sighash, const uint8_t* r, const uint8
     HIPCHK(launch_prep_sender(sighash + off * 32, r + off * 32, s + off * 32, v + off * 32, vflags ? vflags + off : nullptr,
                               m, (uint32_t)n_pad, signer, chain_id, rec, st));
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr + off * 20, nullptr, d.gtab, d.ws};
-    HIPCHK(launch_recover(p, d.mb_recover, st));
+    HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, st));
   }
   return EGES_SUCCESS;
 }
@@ -283,7 +325,7 @@ int run_sender_raw_dev(Dev& d, const uint8_t* raw, const uint64_t* offsets, size
     HIPCHK(launch_tx_rows(raw, offsets, off, m, signer, chain_id, hs, rr, sr, vr, vf, st));
     HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, m, (uint32_t)n_pad, signer, chain_id, rec, st));
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr + off * 20, nullptr, d.gtab, d.ws};
-    HIPCHK(launch_recover(p, d.mb_recover, st));
+    HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, st));
   }
   return EGES_SUCCESS;
 }
@@ -303,7 +345,7 @@ int run_precompile_dev(Dev& d, const uint8_t* input, const uint32_t* inlen, size
     const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
     HIPCHK(launch_prep_precompile(input + off * 128, inlen ? inlen + off : nullptr, m, (uint32_t)n_pad, rec, st));
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, out32 + off * 32 + 12, nullptr, d.gtab, d.ws, 32};
-    HIPCHK(launch_recover(p, d.mb_recover, st));
+    HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, st));
   }
   return EGES_SUCCESS;
 }
@@ -318,7 +360,7 @@ int run_verify_dev(Dev& d, const uint8_t* pub, const uint8_t* publen, const uint
     const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
     VerifyParams p{pub + off * 65, publen + off, msg + off * 32, sig + off * 64, m, ok + off, d.gtab, d.ws};
     verify_scratch_bind(p, d.buf, n_pad);
-    HIPCHK(launch_verify(p, d.mb_verify, st));
+    HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
   }
   return EGES_SUCCESS;
 }
@@ -427,7 +469,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       HIPCHK(launch_prep_ecrecover(dm, ds, (uint32_t)m, (uint32_t)m_pad, rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, j.addr ? o_addr : nullptr, j.pub ? o_pub : nullptr,
                       d.gtab, d.ws};
-      HIPCHK(launch_recover(p, d.mb_recover, st));
+      HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, st));
     } else if (j.kind == HostJob::SENDER) {
       uint8_t* dh = B;
       uint8_t* dr = dh + m * 32;
@@ -444,7 +486,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       HIPCHK(launch_prep_sender(dh, dr, dsv, dv, j.e ? df : nullptr, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id,
                                 rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
-      HIPCHK(launch_recover(p, d.mb_recover, st));
+      HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, st));
     } else if (j.kind == HostJob::PRECOMPILE) {
       uint8_t* din = B;
       uint32_t* dlen = reinterpret_cast<uint32_t*>(din + m * 128);
@@ -455,7 +497,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       HIPCHK(hipMemsetAsync(o_addr, 0, m * 32, st));
       HIPCHK(launch_prep_precompile(din, j.inlen ? dlen : nullptr, (uint32_t)m, (uint32_t)m_pad, rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr + 12, nullptr, d.gtab, d.ws, 32};
-      HIPCHK(launch_recover(p, d.mb_recover, st));
+      HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, st));
     } else if (j.kind == HostJob::SENDER_RAW) {
       uint8_t* draw = B;
       uint64_t* doff = reinterpret_cast<uint64_t*>(draw + align_up(rg.raw_len, 8));
@@ -471,7 +513,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, vf, st));
       HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
-      HIPCHK(launch_recover(p, d.mb_recover, st));
+      HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, st));
     } else {
       uint8_t* dp = B;
       uint8_t* dl = dp + m * 65;
@@ -485,7 +527,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
       VerifyParams p{dp, dl, dm, ds, (uint32_t)m, o_st, d.gtab, d.ws};
       verify_scratch_bind(p, B + rg.o_rec, m_pad);
-      HIPCHK(launch_verify(p, d.mb_verify, st));
+      HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
     }
     HIPCHK(hipEventRecord(d.ev_k[r], st));
     // --- the previous chunk's outputs, while this chunk computes
@@ -510,7 +552,7 @@ int run_host(const HostJob& j, size_t n) {
   if (n == 0) return EGES_SUCCESS;
   int rc = ensure_init();
   if (rc) return rc;
-  std::vector<Dev*> devs;
+  std::vector<DevPtr> devs;
   {
     std::lock_guard<std::mutex> lk(g_mu);
     devs = g_devs;
@@ -590,12 +632,17 @@ int eges_init(uint32_t device_mask, uint32_t flags) {
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
     return set_err(EGES_E_NODEVICE, "no HIP device visible");
   std::string errs;
+  // tests only: register every device k times (independent streams / workspaces), so the
+  // multi-device shard path of run_host runs on a one-GPU box
+  const int logical = std::max(1, std::min(8, env_int("EGES_TEST_LOGICAL_DEVICES", 1)));
   for (int i = 0; i < count && i < 32; ++i) {
     if (device_mask && !((device_mask >> i) & 1u)) continue;
-    Dev* d = nullptr;
-    int rc = init_device(i, &d);
-    if (rc == EGES_SUCCESS) g_devs.push_back(d);
-    else errs += t_err + "; ";
+    for (int k = 0; k < logical; ++k) {
+      DevPtr d;
+      int rc = init_device(i, &d);
+      if (rc == EGES_SUCCESS) g_devs.push_back(std::move(d));
+      else errs += t_err + "; ";
+    }
   }
   if (g_devs.empty()) return set_err(EGES_E_NODEVICE, "no usable gfx950 device (%s)", errs.c_str());
   g_inited = true;
@@ -603,32 +650,17 @@ int eges_init(uint32_t device_mask, uint32_t flags) {
 }
 
 void eges_shutdown(void) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  for (Dev* d : g_devs) {
-    std::lock_guard<std::mutex> dl(d->mu);
-    DevGuard g(d->id);
-    (void)hipStreamSynchronize(d->stream);
-    (void)hipEventSynchronize(d->last);  // the last engine work, on whichever stream the caller gave
-    (void)hipFree(d->gtab);
-    (void)hipFree(d->ws);
-    if (d->buf) (void)hipFree(d->buf);
-    (void)hipEventDestroy(d->last);
-    for (int r = 0; r < 2; ++r) {
-      (void)hipEventDestroy(d->ev_in[r]);
-      (void)hipEventDestroy(d->ev_k[r]);
-    }
-    (void)hipStreamDestroy(d->copy);
-    if (d->aux) {
-      (void)hipStreamDestroy(d->aux);
-      (void)hipEventDestroy(d->ev_fork);
-      (void)hipEventDestroy(d->ev_join);
-      (void)hipFree(d->ws2);
-    }
-    (void)hipStreamDestroy(d->stream);
+  std::vector<DevPtr> devs;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    devs.swap(g_devs);
+    g_inited = false;
   }
-  for (Dev* d : g_devs) delete d;
-  g_devs.clear();
-  g_inited = false;
+  // each device is released once its in-flight calls (which hold references) have returned
+  for (DevPtr& d : devs) {
+    { std::lock_guard<std::mutex> dl(d->mu); }
+    d.reset();
+  }
 }
 
 int eges_device_count(void) {
@@ -749,7 +781,7 @@ int eges_ecrecover_batch_dev(int device, const uint8_t* msg, const uint8_t* sig,
   if (!msg || !sig || !status) return set_err(EGES_E_NULLPTR, "NULL argument");
   int rc = ensure_init();
   if (rc) return rc;
-  Dev* d = dev_by_id(device);
+  DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
@@ -764,7 +796,7 @@ int eges_sender_batch_dev(int device, const uint8_t* sighash, const uint8_t* r, 
   if (signer < 0 || signer > 2) return set_err(EGES_E_INVALID_ARG, "bad signer %d", signer);
   int rc = ensure_init();
   if (rc) return rc;
-  Dev* d = dev_by_id(device);
+  DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
@@ -780,7 +812,7 @@ int eges_sender_raw_batch_dev(int device, const uint8_t* raw, const uint64_t* of
   if (signer < 0 || signer > 2) return set_err(EGES_E_INVALID_ARG, "bad signer %d", signer);
   int rc = ensure_init();
   if (rc) return rc;
-  Dev* d = dev_by_id(device);
+  DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
@@ -794,7 +826,7 @@ int eges_ecrecover_precompile_batch_dev(int device, const uint8_t* input, const 
   if (!input || !out32 || !status) return set_err(EGES_E_NULLPTR, "NULL argument");
   int rc = ensure_init();
   if (rc) return rc;
-  Dev* d = dev_by_id(device);
+  DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
@@ -807,7 +839,7 @@ int eges_verify_batch_dev(int device, const uint8_t* pub, const uint8_t* publen,
   if (!pub || !publen || !msg || !sig || !ok_out) return set_err(EGES_E_NULLPTR, "NULL argument");
   int rc = ensure_init();
   if (rc) return rc;
-  Dev* d = dev_by_id(device);
+  DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
@@ -818,7 +850,7 @@ static int synth_common(int device, uint64_t first_index, size_t n, const uint8_
                         uint8_t* addr_expected, void* stream) {
   int rc = ensure_init();
   if (rc) return rc;
-  Dev* d = dev_by_id(device);
+  DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);

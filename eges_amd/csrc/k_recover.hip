@@ -178,19 +178,25 @@ __global__ void __launch_bounds__(WG, 2) recover_kernel_stamped(RecoverParams pr
 #endif
 
 // ------------------------------------------------------------------ launcher
-hipError_t launch_recover(const RecoverParams& p, int max_blocks, hipStream_t st) {
+hipError_t launch_recover(const RecoverParams& p, int max_blocks, int ws_blocks, hipStream_t st) {
   if (p.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(recover_kernel, dim3(grid_for_lane_serial(p.n, max_blocks)), dim3(WG), 0, st, p);
+  const int grid = grid_for_lane_serial(p.n, max_blocks);
+  if (grid > ws_blocks) return hipErrorInvalidValue;  // the kernel indexes ws by blockIdx.x
+  hipLaunchKernelGGL(recover_kernel, dim3(grid), dim3(WG), 0, st, p);
   return hipGetLastError();
 }
 
 #ifdef EGES_PHASE_STAMPS
-hipError_t launch_recover_stamped(const RecoverParams& p, int max_blocks, hipStream_t st, uint64_t* stamps) {
+hipError_t launch_recover_stamped(const RecoverParams& p, int max_blocks, int ws_blocks, hipStream_t st, uint64_t* stamps) {
   if (p.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(recover_kernel_stamped, dim3(grid_for_lane_serial(p.n, max_blocks)), dim3(WG), 0, st, p, stamps);
+  const int grid = grid_for_lane_serial(p.n, max_blocks);
+  if (grid > ws_blocks) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(recover_kernel_stamped, dim3(grid), dim3(WG), 0, st, p, stamps);
   return hipGetLastError();
 }
 #endif
+
+int lane_serial_grid(uint32_t n, int max_blocks) { return grid_for_lane_serial(n, max_blocks); }
 
 int occupancy_recover() {
   int b = 0;

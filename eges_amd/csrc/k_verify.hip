@@ -147,14 +147,16 @@ __global__ void __launch_bounds__(WG, 2) verify_kernel(VerifyParams prm) {
 }
 
 // ------------------------------------------------------------------ launcher
-hipError_t launch_verify(const VerifyParams& p, int max_blocks, hipStream_t st) {
+hipError_t launch_verify(const VerifyParams& p, int max_blocks, int ws_blocks, hipStream_t st) {
   if (p.n == 0) return hipSuccess;
+  const int grid = grid_for_lane_serial(p.n, max_blocks);
+  if (grid > ws_blocks) return hipErrorInvalidValue;  // the kernel indexes ws by blockIdx.x
   hipError_t e = hipMemsetAsync(p.counts, 0, 2 * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(verify_order_kernel, dim3((p.n + WG - 1) / WG), dim3(WG), 0, st, p.publen, p.n, p.order, p.counts);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(verify_kernel, dim3(grid_for_lane_serial(p.n, max_blocks)), dim3(WG), 0, st, p);
+  hipLaunchKernelGGL(verify_kernel, dim3(grid), dim3(WG), 0, st, p);
   return hipGetLastError();
 }
 

@@ -16,6 +16,8 @@ constexpr uint8_t VF_DECODE_ERR = 0x8;
 // n_pad entries right after the record rows (k_recover.hip). A thread owns <= MAX_SLOTS.
 constexpr int SLOT_ROWS = 12;
 constexpr uint32_t MAX_SLOTS = 32;
+// Signatures per device pass of the batch entries (bounds the per-call scratch memory).
+constexpr size_t PASS_MAX = size_t(1) << 21;
 inline size_t recover_scratch_bytes(size_t n_pad) { return n_pad * ((size_t)REC_ROWS * 4 + (size_t)SLOT_ROWS * 16); }
 __host__ __device__ inline uint4* recover_slots(const uint32_t* rec, uint32_t n_pad) {
   return reinterpret_cast<uint4*>(const_cast<uint32_t*>(rec) + (size_t)REC_ROWS * n_pad);
@@ -79,10 +81,15 @@ hipError_t launch_tx_rows(const uint8_t* raw, const uint64_t* offsets, uint64_t 
                           uint64_t chain_id, uint8_t* sighash, uint8_t* r, uint8_t* s, uint8_t* v, uint8_t* vflags,
                           hipStream_t st);
 #ifdef EGES_PHASE_STAMPS
-hipError_t launch_recover_stamped(const RecoverParams& p, int max_blocks, hipStream_t st, uint64_t* stamps);
+hipError_t launch_recover_stamped(const RecoverParams& p, int max_blocks, int ws_blocks, hipStream_t st, uint64_t* stamps);
 #endif
-hipError_t launch_recover(const RecoverParams& p, int max_blocks, hipStream_t st);
-hipError_t launch_verify(const VerifyParams& p, int max_blocks, hipStream_t st);
+// max_blocks: the resident grid; ws_blocks: blocks the workspace p.ws was allocated for. A
+// launch whose grid would exceed ws_blocks is refused (hipErrorInvalidValue), never run.
+hipError_t launch_recover(const RecoverParams& p, int max_blocks, int ws_blocks, hipStream_t st);
+hipError_t launch_verify(const VerifyParams& p, int max_blocks, int ws_blocks, hipStream_t st);
+// Blocks the lane-serial kernels may need for a pass of n signatures at a resident grid of
+// max_blocks (grid_for_lane_serial: more than resident when n > max_blocks * WG * MAX_SLOTS).
+int lane_serial_grid(uint32_t n, int max_blocks);
 hipError_t launch_synth(const SynthParams& p, int max_blocks, hipStream_t st);
 int occupancy_recover();
 int occupancy_verify();

@@ -12,6 +12,12 @@
 // inversion", TCHES 2019), in the zeta = -(delta + 1/2) form: state (zeta, f, g, d, e) with
 // f = M, g = x, d = 0, e = 1. 590 divsteps suffice for 256-bit inputs; 20 x 30 = 600 are run.
 // Afterwards g = 0, f = +-1 and x^-1 = +-d (mod M). Numbers are signed radix-2^30, 9 limbs.
+//
+// Attribution: divsteps_30 and update_de_30 below follow the structure of upstream
+// libsecp256k1's src/modinv32_impl.h (secp256k1_modinv32_divsteps_30 / _update_de_30: the
+// c1/c2 masks, the u/v/q/r transition matrix and the md/me correction by M^-1 mod 2^30),
+// Copyright (c) 2020 Peter Dettman, Pieter Wuille, MIT License. That file is not part of the
+// vendored reference snapshot (which predates it); the code here is written for gfx950.
 #pragma once
 #include <stdint.h>
 

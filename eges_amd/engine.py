@@ -132,6 +132,29 @@ def _tp(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+def _dchk(t, tail, name, n, dev, dtype=None, optional=False):
+    """Validate a device tensor handed to a *_dev entry: dtype (uint8 unless given), C-contiguous,
+    shape (n, *tail), on `dev`. The C-ABI takes raw pointers and sizes, so a sliced, short or
+    foreign-device tensor would otherwise be read or written out of bounds."""
+    import torch
+    if t is None:
+        if optional:
+            return None
+        raise ValueError(f"{name}: required")
+    want = dtype or torch.uint8
+    dts = want if isinstance(want, tuple) else (want,)
+    if t.dtype not in dts:
+        raise ValueError(f"{name}: dtype {t.dtype}, expected {' or '.join(map(str, dts))}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if t.device != dev:
+        raise ValueError(f"{name}: on {t.device}, expected {dev}")
+    shape = (n,) + tuple(tail)
+    if tuple(t.shape) != shape:
+        raise ValueError(f"{name}: shape {tuple(t.shape)}, expected {shape}")
+    return t
+
+
 def _stream_of(t):
     import torch
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
@@ -147,6 +170,11 @@ def ecrecover_batch_dev(msg, sig, pub=None, addr=None, status=None, stream=None)
         addr = torch.empty((n, 20), dtype=torch.uint8, device=dev)
     if status is None:
         status = torch.empty((n,), dtype=torch.uint8, device=dev)
+    _dchk(msg, (32,), "msg", n, dev)
+    _dchk(sig, (65,), "sig", n, dev)
+    _dchk(pub, (65,), "pub", n, dev, optional=True)
+    _dchk(addr, (20,), "addr", n, dev)
+    _dchk(status, (), "status", n, dev)
     st = ctypes.c_void_p(stream) if stream is not None else _stream_of(msg)
     check(lib.eges_ecrecover_batch_dev(dev.index, _tp(msg), _tp(sig), n, _tp(pub), _tp(addr), _tp(status), st))
     return pub, addr, status
@@ -172,6 +200,7 @@ def synth_sign_msg_dev(msg, first_index=0, stream=None):
     dev = msg.device
     sig = torch.empty((n, 65), dtype=torch.uint8, device=dev)
     addr = torch.empty((n, 20), dtype=torch.uint8, device=dev)
+    _dchk(msg, (32,), "msg", n, dev)
     st = ctypes.c_void_p(stream) if stream is not None else _stream_of(msg)
     check(lib.eges_synth_sign_msg_dev(dev.index, int(first_index), n, _tp(msg), _tp(sig), _tp(addr), st))
     return sig, addr
@@ -184,6 +213,12 @@ def verify_batch_dev(pub, publen, msg, sig, ok=None, stream=None):
     n = msg.shape[0]
     if ok is None:
         ok = torch.empty((n,), dtype=torch.uint8, device=msg.device)
+    dev = msg.device
+    _dchk(pub, (65,), "pub", n, dev)
+    _dchk(publen, (), "publen", n, dev)
+    _dchk(msg, (32,), "msg", n, dev)
+    _dchk(sig, (64,), "sig", n, dev)
+    _dchk(ok, (), "ok", n, dev)
     st = ctypes.c_void_p(stream) if stream is not None else _stream_of(msg)
     check(lib.eges_verify_batch_dev(msg.device.index, _tp(pub), _tp(publen), _tp(msg), _tp(sig), n, _tp(ok), st))
     return ok
@@ -198,6 +233,11 @@ def sender_batch_dev(sighash, r, s, v, vflags, signer, chain_id, addr=None, stat
         addr = torch.empty((n, 20), dtype=torch.uint8, device=dev)
     if status is None:
         status = torch.empty((n,), dtype=torch.uint8, device=dev)
+    for t, name in ((sighash, "sighash"), (r, "r"), (s, "s"), (v, "v")):
+        _dchk(t, (32,), name, n, dev)
+    _dchk(vflags, (), "vflags", n, dev, optional=True)
+    _dchk(addr, (20,), "addr", n, dev)
+    _dchk(status, (), "status", n, dev)
     st = ctypes.c_void_p(stream) if stream is not None else _stream_of(sighash)
     check(lib.eges_sender_batch_dev(dev.index, _tp(sighash), _tp(r), _tp(s), _tp(v), _tp(vflags), n, int(signer),
                                     int(chain_id), _tp(addr), _tp(status), st))
@@ -215,6 +255,12 @@ def sender_raw_batch_dev(raw, offsets, signer, chain_id, addr=None, status=None,
         addr = torch.empty((n, 20), dtype=torch.uint8, device=dev)
     if status is None:
         status = torch.empty((n,), dtype=torch.uint8, device=dev)
+    if raw.dtype != torch.uint8 or raw.dim() != 1 or not raw.is_contiguous() or raw.device != dev:
+        raise ValueError("raw: expected a contiguous 1-D uint8 tensor on the device")
+    _dchk(offsets, (), "offsets", n + 1, dev, dtype=(torch.int64, torch.uint64))
+    _dchk(addr, (20,), "addr", n, dev)
+    _dchk(status, (), "status", n, dev)
+    _dchk(sighash, (32,), "sighash", n, dev, optional=True)
     st = ctypes.c_void_p(stream) if stream is not None else _stream_of(raw)
     check(lib.eges_sender_raw_batch_dev(dev.index, _tp(raw), _tp(offsets), n, int(signer), int(chain_id), _tp(addr),
                                         _tp(status), _tp(sighash), st))
@@ -231,6 +277,10 @@ def ecrecover_precompile_batch_dev(input, inlen=None, out=None, status=None, str
         out = torch.empty((n, 32), dtype=torch.uint8, device=dev)
     if status is None:
         status = torch.empty((n,), dtype=torch.uint8, device=dev)
+    _dchk(input, (128,), "input", n, dev)
+    _dchk(inlen, (), "inlen", n, dev, dtype=(torch.int32, torch.uint32), optional=True)
+    _dchk(out, (32,), "out", n, dev)
+    _dchk(status, (), "status", n, dev)
     st = ctypes.c_void_p(stream) if stream is not None else _stream_of(input)
     check(lib.eges_ecrecover_precompile_batch_dev(dev.index, _tp(input), _tp(inlen), n, _tp(out), _tp(status), st))
     return out, status

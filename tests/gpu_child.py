@@ -1,0 +1,75 @@
+"""Child process for GPU tests that need the engine initialised under test-only knobs
+(EGES_TEST_MAX_BLOCKS, EGES_TEST_LOGICAL_DEVICES), which are read once at eges_init. Run by
+tests/test_gpu_c4.py as `python tests/gpu_child.py <mode>`; prints one JSON line."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def tiled_golden(n):
+    """The golden recover fixture tiled to n items: (msg, sig, pub, status)."""
+    import numpy as np
+    from conftest import load_golden
+    g = load_golden("recover.npz")
+    idx = np.arange(n) % g["msg"].shape[0]
+    return g["msg"][idx], g["sig"][idx], g["pub"][idx], g["status"][idx]
+
+
+def small_grid():
+    """A device whose resident grid is far below the blocks a full pass needs: a multi-pass
+    device batch and a multi-pass verify batch must still be bit-exact (the workspace is sized
+    for the larger grid, capi.hip init_device)."""
+    import numpy as np
+    import torch
+    import eges_amd
+    from eges_amd._lib import lib
+    eges_amd.init(1)
+    n = (1 << 21) + 3001  # two passes of the device entry
+    msg, sig, pub, st = tiled_golden(n)
+    dev = torch.device("cuda", 0)
+    pd = torch.empty((n, 65), dtype=torch.uint8, device=dev)
+    _, _, sd = eges_amd.ecrecover_batch_dev(torch.from_numpy(msg).to(dev), torch.from_numpy(sig).to(dev), pub=pd)
+    torch.cuda.synchronize()
+    ok_dev = bool(np.array_equal(sd.cpu().numpy(), st) and np.array_equal(pd.cpu().numpy(), pub))
+    # host-buffer entry (pipelined chunks) on the same small grid
+    m2 = 300_001
+    p2, _, s2 = eges_amd.ecrecover_batch(msg[:m2], sig[:m2])
+    ok_host = bool(np.array_equal(s2, st[:m2]) and np.array_equal(p2, pub[:m2]))
+    return {"ok_dev": ok_dev, "ok_host": ok_host, "devices": int(lib.eges_device_count())}
+
+
+def logical_devices():
+    """Two logical devices on one GPU: run_host splits a host-buffer batch into two contiguous
+    shards on two threads (capi.hip run_host); the result must equal the device-resident
+    single-device result byte for byte, and the synthetic signer's addresses."""
+    import numpy as np
+    import torch
+    import eges_amd
+    from eges_amd._lib import lib
+    eges_amd.init(1)
+    ndev = int(lib.eges_device_count())
+    n = 400_003
+    msg, sig, exp = eges_amd.synth_sign_dev(77_000_000, n, 0)
+    pub_d = torch.empty((n, 65), dtype=torch.uint8, device=msg.device)
+    _, addr_d, st_d = eges_amd.ecrecover_batch_dev(msg, sig, pub=pub_d)
+    torch.cuda.synchronize()
+    mh, sh = msg.cpu().numpy(), sig.cpu().numpy()
+    pub, addr, st = eges_amd.ecrecover_batch(mh, sh)
+    same = bool(np.array_equal(pub, pub_d.cpu().numpy()) and np.array_equal(addr, addr_d.cpu().numpy())
+                and np.array_equal(st, st_d.cpu().numpy()))
+    correct = bool((st == 0).all() and np.array_equal(addr, exp.cpu().numpy()))
+    # golden fixture through the split path too (every reject class)
+    gm, gs, gp, gst = tiled_golden(200_000)
+    p3, _, s3 = eges_amd.ecrecover_batch(gm, gs)
+    golden = bool(np.array_equal(s3, gst) and np.array_equal(p3, gp))
+    return {"devices": ndev, "same_as_single": same, "correct": correct, "golden": golden}
+
+
+if __name__ == "__main__":
+    mode = sys.argv[1]
+    out = {"small_grid": small_grid, "logical_devices": logical_devices}[mode]()
+    print(json.dumps(out), flush=True)

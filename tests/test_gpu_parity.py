@@ -64,14 +64,48 @@ def test_synth_roundtrip(engine, oracle):
         assert oracle.pub_to_addr(pub) == e[i].tobytes()
 
 
-def test_multi_chunk_overlapped_launches(engine):
+def test_multi_chunk_overlapped_launches(engine, oracle):
     """A device batch larger than one pass (2^21 signatures) runs as launches alternating between
-    two streams with separate workspaces (capi.hip run_recover_dev_overlap): every address of a
-    ragged 2^21 + 4099 batch must still equal the synthetic signer's expectation."""
+    two streams with separate workspaces (capi.hip run_recover_dev_overlap). On a caller stream
+    that still has queued work, with the pub output: every byte of a ragged 2^21 + 4099 batch
+    must equal the same items recovered as single-pass (non-overlapped) calls, and a following
+    host-buffer and verify call on the device must still be right (the d.last join)."""
     import torch
     n = (1 << 21) + 4099
     msg, sig, exp = engine.synth_sign_dev(1 << 30, n, 0)
-    _, addr, st = engine.ecrecover_batch_dev(msg, sig)
     torch.cuda.synchronize()
+    dev = msg.device
+    s = torch.cuda.Stream(dev)
+    pub = torch.empty((n, 65), dtype=torch.uint8, device=dev)
+    addr = torch.empty((n, 20), dtype=torch.uint8, device=dev)
+    st = torch.empty((n,), dtype=torch.uint8, device=dev)
+    with torch.cuda.stream(s):
+        junk = torch.randn(4096, 4096, device=dev)
+        for _ in range(8):  # prior work on the caller's stream that the engine must wait for
+            junk = junk @ junk
+            junk = junk / junk.norm()
+        pub.fill_(0xAB)
+    engine.ecrecover_batch_dev(msg, sig, pub=pub, addr=addr, status=st, stream=s.cuda_stream)
+    s.synchronize()
     assert bool((st == 0).all().item())
     assert torch.equal(addr, exp)
+    # the same items as single-pass calls (each <= one pass: no overlap)
+    h = n // 2
+    pub2 = torch.empty_like(pub)
+    addr2 = torch.empty_like(addr)
+    st2 = torch.empty_like(st)
+    for lo, hi in ((0, h), (h, n)):
+        engine.ecrecover_batch_dev(msg[lo:hi], sig[lo:hi], pub=pub2[lo:hi], addr=addr2[lo:hi], status=st2[lo:hi])
+    torch.cuda.synchronize()
+    assert torch.equal(pub, pub2) and torch.equal(addr, addr2) and torch.equal(st, st2)
+    # host-buffer and verify calls right after, on the same device
+    idx = [0, h - 1, h, n - 1]
+    mh, sh = msg[idx].cpu().numpy(), sig[idx].cpu().numpy()
+    p3, a3, s3 = engine.ecrecover_batch(mh, sh)
+    assert (s3 == 0).all() and np.array_equal(p3, pub[idx].cpu().numpy())
+    lens = np.full(len(idx), 65, np.uint8)
+    ok = engine.verify_batch(p3, lens, mh, sh[:, :64])
+    assert ok.tolist() == [1, 1, 1, 1]
+    for j in (0, 3):
+        ost, opub = oracle.recover_pubkey(mh[j].tobytes(), sh[j].tobytes())
+        assert ost == 0 and opub == p3[j].tobytes()

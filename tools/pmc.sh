@@ -1,4 +1,6 @@
-# PMC passes for the recover kernel (one counter group per rocprofv3 run). Run via gpurun.
+# PMC passes for the dominant kernels (one counter group per rocprofv3 run; each pass within the
+# per-block limits: <= 8 SQ, FETCH_SIZE / WRITE_SIZE alone). Run via gpurun; writes
+# gpurun_out/pmc_traffic.json in the schema bench.py reads (tools/pmc_summary.py).
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -9,4 +11,5 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD 
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- $B > gpurun_out/pmc_fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- $B > gpurun_out/pmc_write.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc_tcc -o run --output-format csv -- $B > gpurun_out/pmc_tcc.log 2>&1
+python tools/pmc_summary.py gpurun_out 1048576 gpurun_out/pmc_traffic.json > /dev/null
 echo done
