@@ -9,7 +9,7 @@ Pure-Python restatement of what the reference does from raw transaction bytes to
       Stream.Bytes (single byte < 0x80 rule) ......... :668-688
       Stream.uint / Bool ............................. :707-756
       decodeBigInt (leading zero bytes) .............. :254-269
-      decodeByteArray ([20]byte Recipient) ........... :390-425
+      decodeByteArray ([N]byte, [20]byte Recipient) .. :390-413
       makeOptionalPtrDecoder (rlp:"nil") ............. :464-490
       struct decoder: too few / too many elements .... :418-435
   - the signer's Hash (FrontierSigner.Hash transaction_signing.go:207-216, EIP155Signer.Hash
@@ -128,20 +128,35 @@ class _Stream:
             raise DecodeError("invalid boolean")
         return v == 1
 
+    def byte_array(self, n):
+        """decodeByteArray into [n]byte (rlp/decode.go:390-413)."""
+        k, size, bv = self.kind()
+        if k == "byte":
+            if n == 0:
+                raise DecodeError("input string too long")
+            if n > 1:
+                raise DecodeError("input string too short")
+            return bytes([bv])
+        if k == "list":
+            raise DecodeError("ErrExpectedString")
+        if n < size:
+            raise DecodeError("input string too long")
+        if n > size:
+            raise DecodeError("input string too short")
+        c = self.content(size)
+        if size == 1 and c[0] < 128:
+            raise DecodeError("ErrCanonSize")
+        return c
+
     def address_or_nil(self):
+        """*common.Address with rlp:"nil" (makeOptionalPtrDecoder, rlp/decode.go:464-490): an
+        empty string or list decodes as nil, anything else as [20]byte."""
         save = self.pos
         k, size, bv = self.kind()
         if size == 0 and k != "byte":
             return None
         self.pos = save  # decodeByteArray re-reads the same (cached) kind
-        k, size, bv = self.kind()
-        if k == "byte":
-            raise DecodeError("input string too short")
-        if k == "list":
-            raise DecodeError("ErrExpectedString")
-        if size != 20:
-            raise DecodeError("wrong address length")
-        return self.content(20)
+        return self.byte_array(20)
 
     def list_start(self):
         k, size, _ = self.kind()
@@ -155,21 +170,41 @@ class _Stream:
         self.ends.pop()
 
 
-def decode_txdata(raw):
-    """rlp.DecodeBytes(raw, &tx) for the Geec txdata struct -> dict, or raises DecodeError."""
-    s = _Stream(raw)
+def decode_struct(s, readers):
+    """Struct decoder (rlp/decode.go:418-435): a list whose elements are read in field order;
+    EOL before the last field is "too few elements", leftover elements "too many"."""
     s.list_start()
     try:
-        d = dict(nonce=s.uint(64), price=s.bigint(), gas=s.uint(64), to=s.address_or_nil(), value=s.bigint(),
-                 data=s.bytes_(), is_geec=s.boolean(), v=s.bigint(), r=s.bigint(), s=s.bigint())
+        vals = [r() for r in readers]
     except DecodeError as e:
         if str(e) == "EOL":
             raise DecodeError("too few elements")
         raise
     s.list_end()
+    return vals
+
+
+def decode_bytes(raw, reader):
+    """rlp.DecodeBytes (rlp/decode.go:119-129): one value read by reader(stream), no trailing data."""
+    s = _Stream(raw)
+    v = reader(s)
     if s.pos != len(s.b):
         raise DecodeError("ErrMoreThanOneValue")
-    return d
+    return v
+
+
+TXDATA_FIELDS = ("nonce", "price", "gas", "to", "value", "data", "is_geec", "v", "r", "s")
+
+
+def txdata_readers(s):
+    """Field readers of the Geec txdata struct, in order (core/types/transaction.go:59-76)."""
+    return [lambda: s.uint(64), s.bigint, lambda: s.uint(64), s.address_or_nil, s.bigint, s.bytes_, s.boolean,
+            s.bigint, s.bigint, s.bigint]
+
+
+def decode_txdata(raw):
+    """rlp.DecodeBytes(raw, &tx) for the Geec txdata struct -> dict, or raises DecodeError."""
+    return decode_bytes(raw, lambda s: dict(zip(TXDATA_FIELDS, decode_struct(s, txdata_readers(s)))))
 
 
 # ------------------------------------------------------------------ encoder (rlp/encode.go)
