@@ -89,6 +89,17 @@ static int overlap_parts(size_t n) {
   return n > CHUNK ? 2 : 0;
 }
 
+// Batches (or pipeline chunks) of at most this many signatures run on the latency kernel
+// (k_recover_lat.hip: one signature per 16-lane row); larger ones on the lane-serial throughput
+// kernel. EGES_LAT_MAX overrides it (0 = never); read per call so tests can A/B both kernels.
+#ifndef EGES_LAT_MAX_DEFAULT
+#define EGES_LAT_MAX_DEFAULT 8192
+#endif
+static size_t lat_max() {
+  const char* e = std::getenv("EGES_LAT_MAX");
+  return e && *e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)EGES_LAT_MAX_DEFAULT;
+}
+
 std::mutex g_mu;
 std::vector<DevPtr> g_devs;
 bool g_inited = false;
@@ -207,6 +218,13 @@ struct Serial {
   ~Serial() { (void)hipEventRecord(d.last, st); }
 };
 
+// One recover pass over prepared records: the latency kernel for small passes, else the
+// resident-grid lane-serial kernel (its workspace bound checked by the launcher).
+hipError_t launch_recover_pass(Dev& d, const RecoverParams& p, hipStream_t st) {
+  if (p.n <= lat_max()) return launch_recover_lat(p, st);
+  return launch_recover(p, d.mb_recover, d.ws_blocks, st);
+}
+
 // ------------------------------------------------------------------ device-side pipelines
 // All pointers device pointers; d.mu held by the caller.
 #ifdef EGES_PHASE_STAMPS
@@ -276,7 +294,7 @@ int run_recover_dev(Dev& d, const uint8_t* msg, const uint8_t* sig, size_t n, ui
     HIPCHK(hipMemsetAsync(g_stamps, 0, g_stamp_waves * 8 * sizeof(uint64_t), st));
     HIPCHK(launch_recover_stamped(p, d.mb_recover, d.ws_blocks, st, g_stamps));
 #else
-    HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, st));
+    HIPCHK(launch_recover_pass(d, p, st));
 #endif
   }
   return EGES_SUCCESS;
@@ -296,7 +314,7 @@ int run_sender_dev(Dev& d, const uint8_t* sighash, const uint8_t* r, const uint8
     HIPCHK(launch_prep_sender(sighash + off * 32, r + off * 32, s + off * 32, v + off * 32, vflags ? vflags + off : nullptr,
                               m, (uint32_t)n_pad, signer, chain_id, rec, st));
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr + off * 20, nullptr, d.gtab, d.ws};
-    HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, st));
+    HIPCHK(launch_recover_pass(d, p, st));
   }
   return EGES_SUCCESS;
 }
@@ -325,7 +343,7 @@ int run_sender_raw_dev(Dev& d, const uint8_t* raw, const uint64_t* offsets, size
     HIPCHK(launch_tx_rows(raw, offsets, off, m, signer, chain_id, hs, rr, sr, vr, vf, st));
     HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, m, (uint32_t)n_pad, signer, chain_id, rec, st));
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr + off * 20, nullptr, d.gtab, d.ws};
-    HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, st));
+    HIPCHK(launch_recover_pass(d, p, st));
   }
   return EGES_SUCCESS;
 }
@@ -345,7 +363,7 @@ int run_precompile_dev(Dev& d, const uint8_t* input, const uint32_t* inlen, size
     const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
     HIPCHK(launch_prep_precompile(input + off * 128, inlen ? inlen + off : nullptr, m, (uint32_t)n_pad, rec, st));
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, out32 + off * 32 + 12, nullptr, d.gtab, d.ws, 32};
-    HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, st));
+    HIPCHK(launch_recover_pass(d, p, st));
   }
   return EGES_SUCCESS;
 }
@@ -469,7 +487,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       HIPCHK(launch_prep_ecrecover(dm, ds, (uint32_t)m, (uint32_t)m_pad, rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, j.addr ? o_addr : nullptr, j.pub ? o_pub : nullptr,
                       d.gtab, d.ws};
-      HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, st));
+      HIPCHK(launch_recover_pass(d, p, st));
     } else if (j.kind == HostJob::SENDER) {
       uint8_t* dh = B;
       uint8_t* dr = dh + m * 32;
@@ -486,7 +504,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       HIPCHK(launch_prep_sender(dh, dr, dsv, dv, j.e ? df : nullptr, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id,
                                 rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
-      HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, st));
+      HIPCHK(launch_recover_pass(d, p, st));
     } else if (j.kind == HostJob::PRECOMPILE) {
       uint8_t* din = B;
       uint32_t* dlen = reinterpret_cast<uint32_t*>(din + m * 128);
@@ -497,7 +515,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       HIPCHK(hipMemsetAsync(o_addr, 0, m * 32, st));
       HIPCHK(launch_prep_precompile(din, j.inlen ? dlen : nullptr, (uint32_t)m, (uint32_t)m_pad, rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr + 12, nullptr, d.gtab, d.ws, 32};
-      HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, st));
+      HIPCHK(launch_recover_pass(d, p, st));
     } else if (j.kind == HostJob::SENDER_RAW) {
       uint8_t* draw = B;
       uint64_t* doff = reinterpret_cast<uint64_t*>(draw + align_up(rg.raw_len, 8));
@@ -513,7 +531,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, vf, st));
       HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
-      HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, st));
+      HIPCHK(launch_recover_pass(d, p, st));
     } else {
       uint8_t* dp = B;
       uint8_t* dl = dp + m * 65;

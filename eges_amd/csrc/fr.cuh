@@ -1,0 +1,242 @@
+#pragma once
+// Row-form field arithmetic mod p for the latency path (gfx950): one field element spread over
+// a 16-lane DPP row, limb-parallel.
+//
+// The throughput kernels (fe.cuh) give every lane its own signature and a whole 9-limb element;
+// one signature then costs one lane's serial instruction chain (~333k instructions, ~0.78 ms on
+// a lightly loaded SIMD). For small batches (a 1000-transaction Geec block, single calls) the
+// latency kernel (k_recover_lat.hip) gives every signature a whole wavefront instead: each
+// field element lives in one VGPR of a 16-lane row (lane L = limb L of the radix-2^29 value,
+// lanes 9..15 zero), and the four rows of the wave compute up to four independent field
+// products of the same signature at once (quad steps, frg.cuh).
+//
+// Product a*b in a row: lane L accumulates column L = sum_i a_i b_(L-i) with a_i broadcast by
+// DPP row_newbcast and b shifted by DPP row_shr (zero fill), one v_mad_u64_u32 per term, so
+// every lane does 9 MADs instead of 81. Column 16 = a_8 b_8 is the row-uniform "tail". The
+// reduction is three parallel carry rounds (DPP row_shr:1) around one fold of columns 9..17
+// into 0..8 with 2^261 == 2^37 + 31264 (mod p) (DPP row_shl:8 / :9), and a last fold of the
+// carry out of limb 8. (A lane-level Python model of this reduction, checked on weak and
+// lazy-magnitude inputs, was used to derive the bounds in the comments.) Same values as libsecp256k1's field (field_10x26_impl.h:440,769); the
+// representation is this engine's own.
+//
+// Magnitude (as fe.cuh): every limb <= m * 2^29 (limb 0 may carry up to 2^18 more). fr_mul /
+// fr_sqr need m(a) * m(b) <= 6.5 and return m = 1; fr_sub<M>(a, b) needs m(b) < 2M and
+// returns m(a) + 2M, at most 7. Lanes 9..15 are kept zero by every operation.
+#include "fe.cuh"
+
+namespace eges {
+
+// ------------------------------------------------------------------ lanes and DPP
+DEV uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+DEV uint32_t row_lane() { return lane_id() & 15u; }
+DEV uint32_t row_id() { return lane_id() >> 4; }
+
+// lane L of each row <- lane I of the same row
+template <int I>
+DEV uint32_t bcast(uint32_t x) {
+  static_assert(I >= 0 && I < 16, "row_newbcast");
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150 + I, 0xF, 0xF, true);
+}
+// lane L <- lane L - I of the same row, 0 for L < I
+template <int I>
+DEV uint32_t shr(uint32_t x) {
+  static_assert(I >= 1 && I < 16, "row_shr");
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x110 + I, 0xF, 0xF, true);
+}
+// lane L <- lane L + I of the same row, 0 for L + I > 15
+template <int I>
+DEV uint32_t shl(uint32_t x) {
+  static_assert(I >= 1 && I < 16, "row_shl");
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x100 + I, 0xF, 0xF, true);
+}
+// every row <- row R (LDS crossbar permute; no LDS memory used)
+template <int R>
+DEV uint32_t rep_row(uint32_t x) {
+  const int addr = (int)((row_lane() + 16u * R) << 2);
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)x);
+}
+
+// ------------------------------------------------------------------ the element
+struct fr {
+  uint32_t v;  // limb row_lane() (0 for lanes 9..15)
+};
+
+// Row-lane constants, written as sums of independent selects so that they compile to
+// v_cndmask (a nested ?: chain on the lane index becomes a branchy switch). 64p limbs per lane
+// (fe.cuh fe_sub): 2^30 - 62528, 2^30 - 514, 2^30 - 2 (lanes 2..8), 0 (lanes 9..15).
+DEV uint32_t lane_pick(uint32_t L, uint32_t l0, uint32_t v0, uint32_t l1, uint32_t v1) {
+  return (L == l0 ? v0 : 0u) + (L == l1 ? v1 : 0u);
+}
+template <int M>
+DEV uint32_t kconst() {
+  const uint32_t L = row_lane();
+  const uint32_t kk = 0x3FFFFFFEu * M;
+  return (L <= 8 ? kk : 0u) + lane_pick(L, 0, 0x3FFF0BC0u * M - kk, 1, 0x3FFFFDFEu * M - kk);
+}
+DEV uint32_t cfold() {  // 2^261 == 31264 + 2^8 * 2^29 (mod p): factor per destination lane
+  return lane_pick(row_lane(), 0, FOLD0, 1, 256u);
+}
+DEV uint32_t low9(uint32_t x) { return row_lane() <= 8 ? x : 0u; }
+
+DEV fr fr_zero() { return fr{0u}; }
+DEV fr fr_one() { return fr{row_lane() == 0 ? 1u : 0u}; }
+DEV fr fr_small(uint32_t x) { return fr{row_lane() == 0 ? x : 0u}; }  // x < 2^29
+
+DEV fr fr_add(fr a, fr b) { return fr{a.v + b.v}; }
+template <int M>
+DEV fr fr_sub(fr a, fr b) {
+  static_assert(M >= 1 && M <= 3, "fr_sub: M in 1..3");
+  return fr{a.v + kconst<M>() - b.v};
+}
+template <int M>
+DEV fr fr_neg(fr a) { return fr_sub<M>(fr_zero(), a); }
+DEV fr fr_mul_small(fr a, uint32_t k) { return fr{a.v * k}; }
+DEV fr fr_select(bool c, fr a, fr b) { return fr{c ? a.v : b.v}; }
+
+// One parallel carry round: limbs < 2^32 -> magnitude 1 (limb 0 <= 2^29 + 2^18).
+DEV fr fr_normalize_weak(fr a) {
+  const uint32_t c = a.v >> 29;
+  const uint32_t e8 = bcast<8>(c);
+  const uint32_t z = (a.v & M29) + cfold() * e8;
+  return fr{low9(z + shr<1>(c))};
+}
+
+// ------------------------------------------------------------------ product
+namespace frdetail {
+template <int I>
+DEV void mac(uint64_t& acc, uint32_t a, uint32_t b) {
+  const uint32_t ai = bcast<I>(a);
+  const uint32_t bi = shr<I>(b);
+  acc = mad64(ai, bi, acc);
+}
+}  // namespace frdetail
+
+// columns 0..15 of a * b (lane L = column L) on top of `col`; tail = column 16 = a_8 b_8.
+// Three independent MAD chains (the asm barriers keep the compiler from re-associating them
+// into one 9-deep dependent chain: at one wave per SIMD the kernel is latency-bound).
+DEV void fr_cols(uint64_t& col, uint64_t& tail, fr a, fr b) {
+  uint64_t c1 = 0, c2 = 0;
+  asm volatile("" : "+v"(c1), "+v"(c2));
+  col = mad64(bcast<0>(a.v), b.v, col);
+  frdetail::mac<1>(c1, a.v, b.v);
+  frdetail::mac<2>(c2, a.v, b.v);
+  frdetail::mac<3>(col, a.v, b.v);
+  frdetail::mac<4>(c1, a.v, b.v);
+  frdetail::mac<5>(c2, a.v, b.v);
+  frdetail::mac<6>(col, a.v, b.v);
+  frdetail::mac<7>(c1, a.v, b.v);
+  const uint32_t a8 = bcast<8>(a.v);
+  c2 = mad64(a8, shr<8>(b.v), c2);
+  asm volatile("" : "+v"(c1), "+v"(c2));
+  col += c1 + c2;
+  tail = (uint64_t)a8 * bcast<8>(b.v);
+}
+
+// columns (lane L = column L, < 2^63.9) + tail (column 16) -> reduced row element, magnitude 1
+DEV fr fr_reduce(uint64_t col, uint64_t tail) {
+  const uint32_t L = row_lane();
+  // carry round 1 (64-bit carries, 35 bits)
+  const uint32_t lo = (uint32_t)col & M29;
+  const uint64_t c = col >> 29;
+  const uint32_t clo = (uint32_t)c, chi = (uint32_t)(c >> 32);
+  const uint64_t N = (uint64_t)lo + (((uint64_t)shr<1>(chi) << 32) | shr<1>(clo));
+  tail += ((uint64_t)bcast<15>(chi) << 32) | bcast<15>(clo);
+  // carry round 2 (carries < 2^6)
+  const uint32_t d = (uint32_t)(N >> 29);
+  const uint32_t m = ((uint32_t)N & M29) + shr<1>(d);
+  tail += bcast<15>(d);
+  const uint32_t t16 = (uint32_t)tail & M29, t17 = (uint32_t)(tail >> 29);  // t17 < 2^32
+  // fold columns 9..16 into 0..8: column k adds 31264 x into k-9 and 2^8 x into k-8.
+  // Column 17 (2^493 == 31264 2^232 + 2^16 2^29 + 8003584 (mod p)) folds straight into
+  // lanes 8, 1 and 0.
+  uint32_t X = shl<9>(m);  // columns 9..15 -> lanes 0..6 (lanes 8.. get 0)
+  X = L == 7 ? t16 : X;
+  uint32_t Y = shl<8>(m);  // columns 9..15 -> lanes 1..7 (lane 0 would get column 8: excluded)
+  Y = L == 0 ? 0u : Y;
+  Y = L == 8 ? t16 : Y;
+  const uint32_t c17 = lane_pick(L, 0, FOLD0 * 256u, 1, 65536u) + (L == 8 ? FOLD0 : 0u);
+  const uint64_t R = mad64(c17, t17, mad64(X, FOLD0, mad64(Y, 256u, (uint64_t)m)));  // < 2^54.6
+  // carry round 3, with limb 8's carry (a multiple of 2^261) folded into lanes 0 and 1
+  const uint32_t e = (uint32_t)(R >> 29);  // < 2^25.6 (lane 0), 2^18.8 (lane 1), 2^17.7 (lane 8)
+  const uint32_t e8 = bcast<8>(e);
+  const uint64_t z = mad64(e8, cfold(), (uint64_t)((uint32_t)R & M29));  // < 2^32.6
+  const uint32_t zc = (uint32_t)(z >> 29);
+  return fr{low9(((uint32_t)z & M29) + shr<1>(e + zc))};
+}
+
+DEV fr fr_mul(fr a, fr b) {
+  uint64_t col = 0, tail;
+  fr_cols(col, tail, a, b);
+  return fr_reduce(col, tail);
+}
+DEV fr fr_sqr(fr a) { return fr_mul(a, a); }
+
+// a * b - 2^SH c with the subtraction preset into the columns (magnitude(c) < 2M)
+template <int M, int SH = 0>
+DEV fr fr_mul_sub(fr a, fr b, fr c) {
+  static_assert(M >= 1 && M <= 3 && SH >= 0 && SH <= 3, "fr_mul_sub");
+  uint64_t col = (uint64_t)(kconst<M>() - c.v) << SH, tail;
+  fr_cols(col, tail, a, b);
+  return fr_reduce(col, tail);
+}
+template <int M, int SH = 0>
+DEV fr fr_sqr_sub(fr a, fr c) { return fr_mul_sub<M, SH>(a, a, c); }
+
+// ------------------------------------------------------------------ conversions
+// row form -> lane-serial form (every lane of the row gets all 9 limbs)
+DEV fe fr_to_fe(fr a) {
+  fe r;
+  r.v[0] = bcast<0>(a.v);
+  r.v[1] = bcast<1>(a.v);
+  r.v[2] = bcast<2>(a.v);
+  r.v[3] = bcast<3>(a.v);
+  r.v[4] = bcast<4>(a.v);
+  r.v[5] = bcast<5>(a.v);
+  r.v[6] = bcast<6>(a.v);
+  r.v[7] = bcast<7>(a.v);
+  r.v[8] = bcast<8>(a.v);
+  return r;
+}
+// lane-serial form (row-uniform) -> row form
+DEV fr fe_to_fr(const fe& x) {
+  const uint32_t L = row_lane();
+  uint32_t v = 0;
+#pragma unroll
+  for (int i = 0; i < FE_LIMBS; ++i) v = L == (uint32_t)i ? x.v[i] : v;
+  return fr{v};
+}
+DEV fr fr_normalize(fr a) { return fe_to_fr(fe_normalize(fr_to_fe(a))); }
+DEV bool fr_is_zero(fr a) { return fe_is_zero(fr_to_fe(a)); }
+DEV bool fr_equal(fr a, fr b) { return fr_is_zero(fr_sub<1>(a, b)); }
+
+// ------------------------------------------------------------------ quad steps
+// Per-row operand choice: row r of the result takes x_r.
+DEV uint32_t rowsel(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+  const uint32_t r = row_id();
+  return r == 0 ? x0 : r == 1 ? x1 : r == 2 ? x2 : x3;
+}
+DEV fr rowsel(fr a0, fr a1, fr a2, fr a3) { return fr{rowsel(a0.v, a1.v, a2.v, a3.v)}; }
+template <int R>
+DEV fr rep(fr a) { return fr{rep_row<R>(a.v)}; }
+
+// Four independent products in one pass (row r: a_r * b_r), results replicated to every row.
+DEV void fr_mul4(fr& r0, fr& r1, fr& r2, fr& r3, fr a0, fr b0, fr a1, fr b1, fr a2, fr b2, fr a3, fr b3) {
+  const fr p = fr_mul(rowsel(a0, a1, a2, a3), rowsel(b0, b1, b2, b3));
+  r0 = rep<0>(p);
+  r1 = rep<1>(p);
+  r2 = rep<2>(p);
+  r3 = rep<3>(p);
+}
+DEV void fr_mul3(fr& r0, fr& r1, fr& r2, fr a0, fr b0, fr a1, fr b1, fr a2, fr b2) {
+  const fr p = fr_mul(rowsel(a0, a1, a2, a2), rowsel(b0, b1, b2, b2));
+  r0 = rep<0>(p);
+  r1 = rep<1>(p);
+  r2 = rep<2>(p);
+}
+DEV void fr_mul2(fr& r0, fr& r1, fr a0, fr b0, fr a1, fr b1) {
+  const fr p = fr_mul(rowsel(a0, a1, a0, a1), rowsel(b0, b1, b0, b1));
+  r0 = rep<0>(p);
+  r1 = rep<1>(p);
+}
+
+}  // namespace eges

@@ -1,0 +1,308 @@
+// Latency kernel for small recover batches: one signature per 16-lane row (4 per wave).
+//
+// Same path and same outputs as recover_kernel (k_recover.hip; recovery/main_impl.h:38-191,
+// ecmult_impl.h:286-404, eckey_impl.h:36-52, crypto.go:194-197), for batches too small to fill
+// the GPU with one signature per lane: there, a signature costs one lane's serial chain
+// (~0.78 ms for a 1000-transaction block on 16 of 1024 SIMDs). Here every field product is
+// limb-parallel over the 16 lanes of the signature's row (fr.cuh), so a block of 1000
+// signatures spreads over 250 waves and each signature's chain is shorter.
+//
+//   parse, x = r (+n), R = lift_x(x) ...... row form (fr_sqrt), failures carry G and r = 1
+//   r^-1, u1 = -z/r, u2 = s/r, GLV split . lane-serial code, every lane of the row alike
+//   table {1..16}R on one global Z ....... co-Z dblu / zaddu + backward rescale (as core.cuh)
+//   Strauss over 26 windows ............. unchecked adds, exact redo of the wave if a row's
+//                                          accumulator was poisoned (Z == 0 and not infinity)
+//   Z^-1 (safegcd, lane-serial), affine, serialize, Keccak address; lane 0 of the row stores.
+#include "core.cuh"
+#include "frg.cuh"
+
+namespace eges {
+
+constexpr int LAT_WG = 256;
+constexpr int LROWS = LAT_WG / 16;  // signatures per block
+
+struct LatLds {
+  uint32_t tab[LROWS][PTAB][2][16];  // {1..16} * R (x, y), row form, per signature
+  uint32_t zr[LROWS][PTAB][16];      // Z ratios while the table is built
+  int8_t rdig[LROWS][2][RWIN];
+  gdig_t gdig[LROWS][2][GWIN];
+};
+
+// signed fixed-window recoding (core.cuh recode) into this row's digit array
+template <int W, int NW, class D>
+DEV void recode_row(const glv_half& h, D* out) {
+  uint32_t m[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) m[i] = h.mag[i];
+  int carry = 0;
+#pragma unroll 1
+  for (int w = 0; w < NW; ++w) {
+    int v = (int)(m[0] & ((1u << W) - 1)) + carry;
+    carry = v > (1 << (W - 1)) ? 1 : 0;
+    v -= carry << W;
+    out[w] = (D)(h.neg ? -v : v);  // every lane of the row writes the same value
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m[i] = (m[i] >> W) | (m[i + 1] << (32 - W));
+    m[4] >>= W;
+  }
+}
+
+DEV ger lds_pt(const uint32_t (*e)[16]) {
+  const uint32_t L = row_lane();
+  ger p;
+  p.x.v = e[0][L];
+  p.y.v = e[1][L];
+  return p;
+}
+DEV void lds_put_pt(uint32_t (*e)[16], const ger& p) {
+  const uint32_t L = row_lane();
+  e[0][L] = p.x.v;
+  e[1][L] = p.y.v;
+}
+// fixed-base table record (core.cuh layout: 9 limbs of x, 9 of y, 2 pad) -> row form
+DEV ger gtab_pt(const uint32_t* rec) {
+  const uint32_t L = row_lane();
+  const uint32_t k = L <= 8 ? L : 8u;
+  const uint32_t x = rec[k], y = rec[FE_LIMBS + k];
+  ger p;
+  p.x.v = L <= 8 ? x : 0u;
+  p.y.v = L <= 8 ? y : 0u;
+  return p;
+}
+
+DEV ger ger_neg_if(const ger& p, bool neg) {
+  ger r;
+  r.x = p.x;
+  r.y = fr_select(neg, fr_neg<1>(p.y), p.y);
+  return r;
+}
+
+// acc += p (core.cuh add_step / add_step_fast, row form; inf is row-uniform)
+template <bool CHECKED>
+DEV void add_r(gejr& acc, bool& inf, const ger& p, bool use) {
+  gejr s;
+  bool to_inf = false;
+  if (CHECKED) {
+    bool hz, rz;
+    s = gejr_add_ge_t<ADD_PLAIN, true>(acc, p, nullptr, hz, rz);
+    const bool exc = use && !inf && hz;
+    if (__any(exc)) s = gejr_select(exc && rz, gejr_double(acc), s);
+    to_inf = exc && !rz;
+  } else {
+    bool h, r;
+    s = gejr_add_ge_t<ADD_PLAIN, false>(acc, p, nullptr, h, r);
+  }
+  gejr pj;
+  pj.x = p.x;
+  pj.y = p.y;
+  pj.z = fr_one();
+  s = gejr_select(inf, pj, s);
+  acc = gejr_select(use, s, acc);
+  inf = use ? (inf ? false : to_inf) : inf;
+}
+// acc (on the table's isomorphic curve, global Z = zeta) += p (true curve)
+template <bool CHECKED>
+DEV void add_r_zinv(gejr& acc, bool& inf, const ger& p, bool use, const fr& zeta) {
+  gejr s;
+  bool to_inf = false;
+  if (CHECKED) {
+    bool hz, rz;
+    s = gejr_add_ge_t<ADD_ZINV, true>(acc, p, &zeta, hz, rz);
+    const bool exc = use && !inf && hz;
+    if (__any(exc)) s = gejr_select(exc && rz, gejr_double(acc), s);
+    to_inf = exc && !rz;
+  } else {
+    bool h, r;
+    s = gejr_add_ge_t<ADD_ZINV, false>(acc, p, &zeta, h, r);
+  }
+  if (__any(use && inf)) {  // acc = p mapped onto the isomorphic curve: (x zeta^2, y zeta^3, 1)
+    const fr z2 = fr_sqr(zeta);
+    const fr z3 = fr_mul(z2, zeta);
+    gejr pj;
+    pj.x = fr_mul(p.x, z2);
+    pj.y = fr_mul(p.y, z3);
+    pj.z = fr_one();
+    s = gejr_select(inf, pj, s);
+  }
+  acc = gejr_select(use, s, acc);
+  inf = use ? (inf ? false : to_inf) : inf;
+}
+
+template <bool CHECKED>
+DEV void strauss_row(gejr& acc, bool& inf, LatLds& S, int row, const uint32_t* gtab, const fr& zeta,
+                     const fr& beta) {
+  inf = true;
+  acc.x = fr_zero();
+  acc.y = fr_zero();
+  acc.z = fr_zero();
+#pragma unroll 1
+  for (int w = RWIN - 1; w >= 0; --w) {
+    if (w != RWIN - 1) {
+#pragma unroll 1
+      for (int k = 0; k < RBITS; ++k) acc = gejr_double(acc);
+    }
+    const int nadd = (w % GSTEP) == 0 ? 4 : 2;
+#pragma unroll 1
+    for (int j = 0; j < nadd; ++j) {
+      const int d = j < 2 ? (int)S.rdig[row][j][w] : (int)S.gdig[row][j - 2][w / GSTEP];
+      const int a = d < 0 ? -d : d;
+      const int e = a > 0 ? a - 1 : 0;
+      if (j < 2) {
+        ger p = lds_pt(S.tab[row][e]);
+        if (j == 1) p.x = fr_mul(p.x, beta);
+        add_r<CHECKED>(acc, inf, ger_neg_if(p, d < 0), d != 0);
+      } else {
+        const ger p = gtab_pt(gtab + ((size_t)(j - 2) * GTAB + e) * PT_WORDS);
+        add_r_zinv<CHECKED>(acc, inf, ger_neg_if(p, d < 0), d != 0, zeta);
+      }
+    }
+  }
+}
+
+// Q = u_r * P + u_g * G for this row's signature (core.cuh ecmult_core, row form)
+DEV void ecmult_row(gejr& acc, bool& inf, const ger& P, const sc& u_r, const sc& u_g, const uint32_t* gtab,
+                    LatLds& S, int row, const fr& beta) {
+  {
+    glv_half h1, h2;
+    glv_split(h1, h2, u_r);
+    recode_row<RBITS, RWIN, int8_t>(h1, S.rdig[row][0]);
+    recode_row<RBITS, RWIN, int8_t>(h2, S.rdig[row][1]);
+    glv_half g0, g1;
+    g0.neg = false;
+    g1.neg = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      g0.mag[i] = u_g.v[i];
+      g1.mag[i] = u_g.v[4 + i];
+    }
+    g0.mag[4] = 0;
+    g1.mag[4] = 0;
+    recode_row<GBITS, GWIN, gdig_t>(g0, S.gdig[row][0]);
+    recode_row<GBITS, GWIN, gdig_t>(g1, S.gdig[row][1]);
+  }
+  // table {1..PTAB} * P on one global Z (co-Z additions, backward rescale; core.cuh)
+  fr zeta;
+  {
+    lds_put_pt(S.tab[row][0], P);
+    gejr D;
+    ger B;
+    gejr_dblu(D, B, P);
+    S.zr[row][0][row_lane()] = D.z.v;  // Z_2 / Z_1 = 2y
+    ger T;
+    T.x = D.x;
+    T.y = D.y;
+    lds_put_pt(S.tab[row][1], T);
+#pragma unroll 1
+    for (int i = 2; i < PTAB; ++i) {
+      const fr zr = gejr_zaddu(T, B);  // T = (i+1) P
+      lds_put_pt(S.tab[row][i], T);
+      S.zr[row][i - 1][row_lane()] = zr.v;
+    }
+    fr rho = fr_one();
+#pragma unroll 1
+    for (int i = PTAB - 2; i >= 0; --i) {
+      const fr zr{S.zr[row][i][row_lane()]};  // Z_{i+2} / Z_{i+1}
+      rho = i == PTAB - 2 ? zr : fr_mul(rho, zr);
+      const ger J = lds_pt(S.tab[row][i]);
+      const fr r2 = fr_sqr(rho);
+      const fr r3 = fr_mul(r2, rho);
+      ger a;
+      a.x = fr_mul(J.x, r2);
+      a.y = fr_mul(J.y, r3);
+      lds_put_pt(S.tab[row][i], a);
+    }
+    zeta = rho;
+  }
+  strauss_row<false>(acc, inf, S, row, gtab, zeta, beta);
+  if (__any(!inf && fr_is_zero(acc.z))) strauss_row<true>(acc, inf, S, row, gtab, zeta, beta);
+  acc.z = fr_mul(acc.z, zeta);
+}
+
+__global__ void __launch_bounds__(LAT_WG) recover_lat_kernel(RecoverParams prm) {
+  __shared__ LatLds S;
+  const int row = (int)(threadIdx.x >> 4);
+  const uint32_t idx0 = blockIdx.x * LROWS + (uint32_t)row;
+  const bool in = idx0 < prm.n;
+  const uint32_t idx = in ? idx0 : prm.n - 1;
+  const uint32_t np = prm.n_pad;
+  // --- parse (every lane of the row reads the same record)
+  uint32_t rl[8], sl[8], zl[8];
+  rec_get(prm, 8, idx, rl);
+  rec_get(prm, 16, idx, sl);
+  rec_get(prm, 0, idx, zl);
+  const uint32_t meta = prm.rec[(size_t)24 * np + idx];
+  const uint32_t recid = meta & 3u;
+  bool ok = ((meta >> 8) & 0xffu) == ST_OK;
+  bool ovr, ovs, ovz;
+  sc R = sc_from_limbs(rl, ovr);
+  const sc Sv = sc_from_limbs(sl, ovs);
+  const sc Z = sc_from_limbs(zl, ovz);  // msg mod n (main_impl.h:183)
+  ok = ok && !ovr && !ovs && !sc_is_zero(R) && !sc_is_zero(Sv);
+  uint32_t xr[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) xr[i] = R.v[i];
+  if (recid & 2u) {  // x = r + n, only when r < p - n (main_impl.h:101-109)
+    ok = ok && !u256_ge(R.v, P_MINUS_N);
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      c += (uint64_t)xr[i] + SC_N[i];
+      xr[i] = (uint32_t)c;
+      c >>= 32;
+    }
+  }
+  ger Rp;
+  ok = ger_set_xo(Rp, fe_to_fr(fe_from_u256(xr)), (recid & 1u) != 0) && ok;
+  // failed signatures carry the generator and r = 1, so every later step stays well-defined
+  const ge G = gen_point();
+  Rp.x = fr_select(ok, Rp.x, fe_to_fr(G.x));
+  Rp.y = fr_select(ok, Rp.y, fe_to_fr(G.y));
+  R = sc_select(ok, R, sc_one());
+  // --- u1 = -z / r, u2 = s / r (main_impl.h:114-117)
+  const sc rinv = sc_inv(R);
+  const sc u1 = sc_neg(sc_mul(rinv, Z));
+  const sc u2 = sc_select(ok, sc_mul(rinv, Sv), sc_one());
+  // --- Q = u2 R + u1 G
+  const fr beta = fe_to_fr(fe_const(FE_BETA));
+  gejr Q;
+  bool qinf;
+  ecmult_row(Q, qinf, Rp, u2, u1, prm.gtab, S, row, beta);
+  ok = ok && !qinf;  // main_impl.h:120
+  // --- affine, serialize, address
+  const fr zq = fr_select(ok, Q.z, fr_one());
+  const fr zi = fe_to_fr(fe_inv(fr_to_fe(zq)));
+  const fr zi2 = fr_sqr(zi);
+  const fr zi3 = fr_mul(zi2, zi);
+  uint32_t X[8], Y[8];
+  fe_to_u256(X, fe_normalize(fr_to_fe(fr_mul(Q.x, zi2))));
+  fe_to_u256(Y, fe_normalize(fr_to_fe(fr_mul(Q.y, zi3))));
+  uint32_t a[5];
+  pub_address(a, X, Y);
+  if (in && row_lane() == 0) {
+    const uint32_t pre_st = (meta >> 8) & 0xffu;
+    prm.status[idx] = (uint8_t)(pre_st != ST_OK ? pre_st : (ok ? ST_OK : ST_RECOVER_FAILED));
+    if (prm.addr) {
+      uint32_t* dst = reinterpret_cast<uint32_t*>(prm.addr + (size_t)idx * prm.addr_stride);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) dst[i] = ok ? a[i] : 0u;
+    }
+    if (prm.pub) {
+      uint8_t* dst = prm.pub + (size_t)idx * 65;
+      if (ok) {
+        dst[0] = 4;
+        write_be32(dst + 1, X);
+        write_be32(dst + 33, Y);
+      } else {
+        for (int i = 0; i < 65; ++i) dst[i] = 0;
+      }
+    }
+  }
+}
+
+hipError_t launch_recover_lat(const RecoverParams& p, hipStream_t st) {
+  if (p.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(recover_lat_kernel, dim3((p.n + LROWS - 1) / LROWS), dim3(LAT_WG), 0, st, p);
+  return hipGetLastError();
+}
+
+}  // namespace eges

@@ -86,6 +86,9 @@ hipError_t launch_recover_stamped(const RecoverParams& p, int max_blocks, int ws
 // max_blocks: the resident grid; ws_blocks: blocks the workspace p.ws was allocated for. A
 // launch whose grid would exceed ws_blocks is refused (hipErrorInvalidValue), never run.
 hipError_t launch_recover(const RecoverParams& p, int max_blocks, int ws_blocks, hipStream_t st);
+// Small batches: one signature per 16-lane row, limb-parallel field arithmetic (k_recover_lat.hip).
+// Same inputs (prep records) and outputs as launch_recover; no workspace.
+hipError_t launch_recover_lat(const RecoverParams& p, hipStream_t st);
 hipError_t launch_verify(const VerifyParams& p, int max_blocks, int ws_blocks, hipStream_t st);
 // Blocks the lane-serial kernels may need for a pass of n signatures at a resident grid of
 // max_blocks (grid_for_lane_serial: more than resident when n > max_blocks * WG * MAX_SLOTS).

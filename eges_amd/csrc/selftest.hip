@@ -286,3 +286,123 @@ extern "C" double eges_opbench(int op, int reps) {
   const double lanes = (double)blocks * 256;
   return (double)ms * 2.4e6 * prop.multiProcessorCount * 4 / (lanes * reps);
 }
+
+// ---------------------------------------------------------------- row-form field (fr.cuh)
+// One item per 16-lane row; canonical 256-bit words in and out, as eges_selftest.
+#include "fr.cuh"
+namespace eges {
+enum : int {
+  FR_MUL = 0,      // a * b
+  FR_SQR = 1,      // a^2
+  FR_MULSUB = 2,   // a * b - 4c
+  FR_SUB = 3,      // a - b
+  FR_LAZY = 4,     // (2a) * (a + 2b) - 2b (a - b): magnitudes 2 x 3, fr_sub<1>
+  FR_NORMW = 5,    // normalize_weak(7a) (limbs up to 7 * 2^29)
+  FR_CHAIN = 6,    // 64 squarings of a, then * b
+  FR_QUAD = 7,     // fr_mul4: row-replicated a, b, c; out = a*b + b*c + c*a + a*a (4 products in one pass)
+};
+__global__ void fr_selftest_kernel(int op, uint32_t n, const uint32_t* A, const uint32_t* B, const uint32_t* C,
+                                   uint32_t* out) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t item = gid >> 4;
+  if (op == FR_QUAD) item = gid >> 6;  // one item per wave: operands replicated in all rows
+  const bool in = item < n;
+  const uint32_t i = in ? item : 0;
+  const fr a = fe_to_fr(ld(A, i)), b = fe_to_fr(ld(B, i)), c = fe_to_fr(ld(C, i));
+  fr r;
+  switch (op) {
+    case FR_MUL: r = fr_mul(a, b); break;
+    case FR_SQR: r = fr_sqr(a); break;
+    case FR_MULSUB: r = fr_mul_sub<1, 2>(a, b, c); break;
+    case FR_SUB: r = fr_sub<1>(a, b); break;
+    case FR_LAZY: {
+      const fr a2 = fr_add(a, a);
+      const fr t = fr_add(a, fr_add(b, b));
+      const fr u = fr_mul(a2, t);
+      const fr w = fr_mul(fr_add(b, b), fr_sub<1>(a, b));
+      r = fr_sub<1>(u, w);
+      break;
+    }
+    case FR_NORMW: r = fr_normalize_weak(fr_mul_small(a, 7)); break;
+    case FR_CHAIN: {
+      fr t = a;
+#pragma unroll 1
+      for (int k = 0; k < 64; ++k) t = fr_sqr(t);
+      r = fr_mul(t, b);
+      break;
+    }
+    case FR_QUAD: {
+      fr p0, p1, p2, p3;
+      fr_mul4(p0, p1, p2, p3, a, b, b, c, c, a, a, a);
+      r = fr_add(fr_add(p0, p1), fr_add(p2, p3));
+      break;
+    }
+    default: r = a;
+  }
+  const fe o = fe_normalize(fr_to_fe(r));
+  uint32_t x[8];
+  fe_to_u256(x, o);
+  if (in && (threadIdx.x & (op == FR_QUAD ? 63 : 15)) == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out[(size_t)i * 8 + k] = x[k];
+  }
+}
+
+// Latency microbenchmark: one wave per CU, each runs a chain of `reps` dependent squarings in
+// lane-serial form (mode 0: fe_sqr, every lane its own chain) or row form (mode 1: fr_sqr).
+__global__ void __launch_bounds__(64) fr_latency_kernel(int mode, int reps, uint32_t* sink) {
+  uint32_t w[8];
+  for (int k = 0; k < 8; ++k) w[k] = (blockIdx.x * 64 + threadIdx.x + 1) * 2654435761u + k * 40503u;
+  fe a = fe_from_u256(w);
+  uint32_t acc = 0;
+  if (mode == 0) {
+#pragma unroll 1
+    for (int r = 0; r < reps; ++r) a = fe_sqr(a);
+    for (int k = 0; k < FE_LIMBS; ++k) acc += a.v[k];
+  } else {
+    fr x = fe_to_fr(a);
+#pragma unroll 1
+    for (int r = 0; r < reps; ++r) x = fr_sqr(x);
+    acc = x.v;
+  }
+  sink[blockIdx.x * 64 + threadIdx.x] = acc;
+}
+}  // namespace eges
+
+extern "C" int eges_fr_selftest(int op, uint32_t n, const uint32_t* a, const uint32_t* b, const uint32_t* c,
+                                uint32_t* out) {
+  const size_t B = (size_t)n * 32;
+  uint32_t *da, *db, *dc, *dout;
+  if (hipMalloc(&da, B) || hipMalloc(&db, B) || hipMalloc(&dc, B) || hipMalloc(&dout, B)) return -1;
+  (void)hipMemcpy(da, a, B, hipMemcpyHostToDevice);
+  (void)hipMemcpy(db, b, B, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dc, c, B, hipMemcpyHostToDevice);
+  const uint32_t lanes = (op == eges::FR_QUAD ? 64u : 16u) * n;
+  hipLaunchKernelGGL(eges::fr_selftest_kernel, dim3((lanes + 255) / 256), dim3(256), 0, 0, op, n, da, db, dc, dout);
+  hipError_t e = hipDeviceSynchronize();
+  (void)hipMemcpy(out, dout, B, hipMemcpyDeviceToHost);
+  (void)hipFree(da); (void)hipFree(db); (void)hipFree(dc); (void)hipFree(dout);
+  return e == hipSuccess ? 0 : -2;
+}
+
+// ns per dependent squaring at one wave per CU (mode 0 lane-serial fe, 1 row-form fr)
+extern "C" double eges_fr_latency(int mode, int reps) {
+  hipDeviceProp_t prop;
+  (void)hipGetDeviceProperties(&prop, 0);
+  const int blocks = prop.multiProcessorCount;
+  uint32_t* sink;
+  if (hipMalloc(&sink, (size_t)blocks * 64 * 4) != hipSuccess) return -1;
+  hipLaunchKernelGGL(eges::fr_latency_kernel, dim3(blocks), dim3(64), 0, 0, mode, 8, sink);
+  (void)hipDeviceSynchronize();
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, 0);
+  hipLaunchKernelGGL(eges::fr_latency_kernel, dim3(blocks), dim3(64), 0, 0, mode, reps, sink);
+  (void)hipEventRecord(e1, 0);
+  (void)hipEventSynchronize(e1);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipFree(sink);
+  return (double)ms * 1e6 / reps;
+}

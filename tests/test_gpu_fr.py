@@ -1,0 +1,74 @@
+"""GPU unit tests of the row-form (limb-parallel) field layer of the latency kernel
+(eges_amd/csrc/fr.cuh) against Python big integers, through libeges_selftest.so: every
+operation on weak inputs (>= p, all-ones limbs), lazy magnitudes, long squaring chains, the
+quad step (four products in the four rows of a wave), plus the latency of a dependent
+squaring in row form vs the lane-serial form (printed, for the record)."""
+import ctypes
+import os
+import random
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from test_gpu_field import P, dec, enc, samples
+
+pytestmark = pytest.mark.gpu
+FR = dict(MUL=0, SQR=1, MULSUB=2, SUB=3, LAZY=4, NORMW=5, CHAIN=6, QUAD=7)
+
+
+@pytest.fixture(scope="module")
+def st():
+    import torch  # noqa: F401  (share the HIP runtime, see eges_amd/_lib.py)
+    lib = ctypes.CDLL(os.path.join(ROOT, "eges_amd", "libeges_selftest.so"))
+    lib.eges_fr_selftest.argtypes = [ctypes.c_int, ctypes.c_uint32] + [ctypes.c_void_p] * 4
+    lib.eges_fr_latency.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.eges_fr_latency.restype = ctypes.c_double
+    return lib
+
+
+def run(st, op, a, b, c):
+    n = len(a)
+    arrs = [enc(v) for v in (a, b, c)]
+    out = np.zeros((n, 8), np.uint32)
+    p = lambda x: ctypes.c_void_p(x.ctypes.data)
+    assert st.eges_fr_selftest(FR[op], n, *[p(x) for x in arrs], p(out)) == 0
+    return dec(out)
+
+
+def expect(op, a, b, c):
+    if op == "MUL":
+        return a * b % P
+    if op == "SQR":
+        return a * a % P
+    if op == "MULSUB":
+        return (a * b - 4 * c) % P
+    if op == "SUB":
+        return (a - b) % P
+    if op == "LAZY":
+        return (2 * a * (a + 2 * b) - 2 * b * (a - b)) % P
+    if op == "NORMW":
+        return 7 * a % P
+    if op == "CHAIN":
+        return pow(a, 2**64, P) * b % P
+    if op == "QUAD":
+        return (a * b + b * c + c * a + a * a) % P
+
+
+@pytest.mark.parametrize("op", list(FR))
+def test_fr_ops(st, op):
+    rnd = random.Random(1234 + FR[op])
+    n = 1500
+    a, b, c = samples(rnd, n), samples(rnd, n)[::-1], samples(rnd, n)
+    rnd.shuffle(c)
+    got = run(st, op, a, b, c)
+    bad = [i for i in range(n) if got[i] != expect(op, a[i], b[i], c[i])]
+    assert not bad, [(i, hex(a[i]), hex(b[i]), hex(got[i])) for i in bad[:5]]
+
+
+def test_fr_latency_record(st):
+    lane = st.eges_fr_latency(0, 4000)
+    row = st.eges_fr_latency(1, 4000)
+    print(f"\ndependent squaring at one wave per CU: lane-serial {lane:.1f} ns, row form {row:.1f} ns "
+          f"({lane / row:.2f}x)")
+    assert row > 0 and lane > 0

@@ -1,0 +1,95 @@
+"""The latency kernel (k_recover_lat.hip: one signature per 16-lane row) against the throughput
+kernel and the golden fixtures. Batches up to EGES_LAT_MAX signatures take the latency kernel;
+EGES_LAT_MAX=0 forces the lane-serial kernel (capi.hip lat_max is read per call), so every
+case runs both ways and must agree byte for byte, and with the reference-generated fixtures."""
+import os
+import time
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+class lat_max:
+    def __init__(self, v):
+        self.v = v
+
+    def __enter__(self):
+        self.old = os.environ.get("EGES_LAT_MAX")
+        os.environ["EGES_LAT_MAX"] = str(self.v)
+
+    def __exit__(self, *a):
+        if self.old is None:
+            os.environ.pop("EGES_LAT_MAX", None)
+        else:
+            os.environ["EGES_LAT_MAX"] = self.old
+
+
+def test_lat_kernel_golden_recover(engine):
+    g = load_golden("recover.npz")
+    with lat_max(1 << 20):
+        pub, addr, st = engine.ecrecover_batch(g["msg"], g["sig"])
+    names = list(g["kind_names"])
+    bad = np.nonzero(st != g["status"])[0]
+    assert bad.size == 0, [(int(i), names[g["kind"][i]], int(st[i]), int(g["status"][i])) for i in bad[:20]]
+    assert np.array_equal(pub, g["pub"])
+    with lat_max(0):
+        pub2, addr2, st2 = engine.ecrecover_batch(g["msg"], g["sig"])
+    assert np.array_equal(addr, addr2) and np.array_equal(st, st2)
+
+
+def test_lat_kernel_golden_sender(engine):
+    g = load_golden("sender.npz")
+    keys = sorted(set(zip(g["signer"].tolist(), g["chain_id"].tolist())))
+    for signer, cid in keys:
+        sel = np.nonzero((g["signer"] == signer) & (g["chain_id"] == cid))[0]
+        with lat_max(1 << 20):
+            addr, st = engine.sender_batch(g["sighash"][sel], g["r"][sel], g["s"][sel], g["v"][sel], g["vflags"][sel],
+                                           signer, cid)
+        assert np.array_equal(st, g["status"][sel]) and np.array_equal(addr, g["addr"][sel])
+
+
+@pytest.mark.parametrize("n", [1, 2, 15, 16, 17, 1000, 4097])
+def test_lat_kernel_sizes_and_adversarial(engine, n):
+    """Ragged sizes around the 16-signature block, C3's 1000, and the adversarial mix's classes."""
+    import torch
+    from eges_amd import workloads
+    msg, sig, exp = engine.synth_sign_dev(31_000 + n, n, 0)
+    torch.cuda.synchronize()
+    sig_h = sig.cpu().numpy()
+    kind = workloads.adversarial_mix(sig_h, frac=0.3 if n > 16 else 0.0, seed=n)
+    mh = msg.cpu().numpy()
+    with lat_max(1 << 20):
+        p1, a1, s1 = engine.ecrecover_batch(mh, sig_h)
+    with lat_max(0):
+        p2, a2, s2 = engine.ecrecover_batch(mh, sig_h)
+    assert np.array_equal(s1, s2) and np.array_equal(p1, p2) and np.array_equal(a1, a2)
+    assert np.array_equal(s1, workloads.expected_status(kind, "ecrecover"))
+    ok = s1 == 0
+    assert np.array_equal(a1[ok], exp.cpu().numpy()[ok])
+
+
+def test_lat_kernel_block_latency_record(engine):
+    """C3's shape through eges_sender_batch on both kernels (printed for the record)."""
+    import torch
+    from eges_amd import txs
+    from eges_amd._lib import SIGNER_EIP155
+    sighash = txs.geec_block(7000, 1000, payload=100)
+    sig_d, exp_d = engine.synth_sign_msg_dev(torch.from_numpy(sighash).to("cuda:0"), 7000)
+    torch.cuda.synchronize()
+    r, s, v = txs.sender_rows(sig_d.cpu().numpy(), txs.GEEC_CHAIN_ID)
+    out = {}
+    for name, lm in (("latency", 1 << 20), ("lane-serial", 0)):
+        with lat_max(lm):
+            ts = []
+            for i in range(12):
+                t0 = time.perf_counter()
+                addr, st = engine.sender_batch(sighash, r, s, v, None, SIGNER_EIP155, txs.GEEC_CHAIN_ID)
+                ts.append(time.perf_counter() - t0)
+            assert (st == 0).all() and np.array_equal(addr, exp_d.cpu().numpy())
+            out[name] = float(np.median(ts[2:])) * 1e3
+    print(f"\n1000-tx block via eges_sender_batch: latency kernel {out['latency']:.3f} ms, "
+          f"lane-serial kernel {out['lane-serial']:.3f} ms")
