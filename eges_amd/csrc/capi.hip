@@ -26,6 +26,11 @@ using namespace eges;
 constexpr size_t CHUNK = PASS_MAX;  // signatures per device pass (bounds scratch memory)
 // host-buffer shards of at least 2 * PIPE_MIN items are split into >= 2 pipelined chunks
 constexpr size_t PIPE_MIN = size_t(1) << 18;
+// Single-chunk host-buffer calls whose device region fits this many bytes are staged through
+// one pinned host buffer: the caller's inputs are packed on the host, moved by ONE H2D copy,
+// and the outputs come back by one D2H copy (a 1000-transaction block otherwise pays five
+// pageable H2D and two pageable D2H copies, ~0.1 ms).
+constexpr size_t PIN_BYTES = size_t(8) << 20;
 #ifndef EGES_PIPE_PARTS
 #define EGES_PIPE_PARTS 4
 #endif
@@ -66,6 +71,7 @@ struct Dev {
   int ws_blocks = 0;  // blocks ws (and ws2) hold: every launch's grid is checked against it
   uint8_t* buf = nullptr;  // per-call device scratch, grown on demand
   size_t buf_cap = 0;
+  uint8_t* pin = nullptr;  // pinned host staging of single-chunk host-buffer calls (PIN_BYTES)
   // overlapped recover launches (EGES_OVERLAP): a second stream, workspace and its events
   hipStream_t aux = nullptr;
   uint32_t* ws2 = nullptr;
@@ -179,6 +185,7 @@ Dev::~Dev() {
   if (gtab) (void)hipFree(gtab);
   if (ws) (void)hipFree(ws);
   if (buf) (void)hipFree(buf);
+  if (pin) (void)hipHostFree(pin);
   if (last) (void)hipEventDestroy(last);
   for (int r = 0; r < 2; ++r) {
     if (ev_in[r]) (void)hipEventDestroy(ev_in[r]);
@@ -220,7 +227,30 @@ struct Serial {
 
 // One recover pass over prepared records: the latency kernel for small passes, else the
 // resident-grid lane-serial kernel (its workspace bound checked by the launcher).
+#ifdef EGES_PHASE_STAMPS
+static uint64_t* g_stamps = nullptr;
+static size_t g_stamp_waves = 0, g_stamp_cap = 0;
+static hipError_t stamp_buf(size_t waves, hipStream_t st) {
+  if (waves > g_stamp_cap) {
+    if (g_stamps) (void)hipFree(g_stamps);
+    g_stamps = nullptr;
+    g_stamp_cap = 0;
+    hipError_t e = hipMalloc(&g_stamps, waves * 8 * sizeof(uint64_t));
+    if (e != hipSuccess) return e;
+    g_stamp_cap = waves;
+  }
+  g_stamp_waves = waves;
+  return hipMemsetAsync(g_stamps, 0, waves * 8 * sizeof(uint64_t), st);
+}
+#endif
+
 hipError_t launch_recover_pass(Dev& d, const RecoverParams& p, hipStream_t st) {
+#ifdef EGES_PHASE_STAMPS
+  if (p.n <= lat_max()) {
+    hipError_t e = stamp_buf(lat_waves(p.n), st);
+    return e != hipSuccess ? e : launch_recover_lat_stamped(p, st, g_stamps);
+  }
+#endif
   if (p.n <= lat_max()) return launch_recover_lat(p, st);
   return launch_recover(p, d.mb_recover, d.ws_blocks, st);
 }
@@ -229,8 +259,6 @@ hipError_t launch_recover_pass(Dev& d, const RecoverParams& p, hipStream_t st) {
 // All pointers device pointers; d.mu held by the caller.
 #ifdef EGES_PHASE_STAMPS
 // Diagnostic build (libeges_diag.so): per-wave phase cycle sums of the last recover launch.
-static uint64_t* g_stamps = nullptr;
-static size_t g_stamp_waves = 0;
 extern "C" size_t eges_diag_read_stamps(uint64_t* out, size_t max_waves) {
   const size_t w = g_stamp_waves < max_waves ? g_stamp_waves : max_waves;
   if (g_stamps && out && w) {
@@ -289,13 +317,13 @@ int run_recover_dev(Dev& d, const uint8_t* msg, const uint8_t* sig, size_t n, ui
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr ? addr + off * 20 : nullptr, pub ? pub + off * 65 : nullptr,
                     d.gtab, d.ws};
 #ifdef EGES_PHASE_STAMPS
-    if (!g_stamps) HIPCHK(hipMalloc(&g_stamps, (size_t)d.mb_recover * 4 /* waves per block */ * 8 * sizeof(uint64_t)));
-    g_stamp_waves = (size_t)d.mb_recover * 4 /* waves per block */;
-    HIPCHK(hipMemsetAsync(g_stamps, 0, g_stamp_waves * 8 * sizeof(uint64_t), st));
-    HIPCHK(launch_recover_stamped(p, d.mb_recover, d.ws_blocks, st, g_stamps));
-#else
-    HIPCHK(launch_recover_pass(d, p, st));
+    if (p.n > lat_max()) {
+      HIPCHK(stamp_buf((size_t)d.ws_blocks * 4 /* waves per block */, st));
+      HIPCHK(launch_recover_stamped(p, d.mb_recover, d.ws_blocks, st, g_stamps));
+      continue;
+    }
 #endif
+    HIPCHK(launch_recover_pass(d, p, st));
   }
   return EGES_SUCCESS;
 }
@@ -440,28 +468,76 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
   if (rc) return rc;
   // a single chunk has nothing to overlap: one stream, no cross-stream waits (C3 latency)
   hipStream_t st = d.stream, sx = nreg > 1 ? d.copy : d.stream;
+  const bool pinned = nreg == 1 && worst <= PIN_BYTES;
+  if (pinned && !d.pin && hipHostMalloc(&d.pin, PIN_BYTES, hipHostMallocDefault) != hipSuccess) {
+    d.pin = nullptr;
+    return set_err(EGES_E_NOMEM, "hipHostMalloc(%zu) failed", PIN_BYTES);
+  }
   HIPCHK(hipStreamWaitEvent(st, d.last, 0));
   HIPCHK(hipStreamWaitEvent(sx, d.last, 0));
+  // Input staging: each input array goes to its offset in the device region B, either by its
+  // own (pageable) copy on the copy stream, or packed into the pinned buffer at the same offset
+  // and moved as one copy by flush_in().
+  size_t in_ext = 0;
+  auto h2d = [&](uint8_t* B, uint8_t* dst, const void* src, size_t bytes) -> int {
+    if (!bytes) return EGES_SUCCESS;
+    if (pinned) {
+      const size_t o = (size_t)(dst - B);
+      std::memcpy(d.pin + o, src, bytes);
+      in_ext = std::max(in_ext, o + bytes);
+      return EGES_SUCCESS;
+    }
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, sx));
+    return EGES_SUCCESS;
+  };
+  auto flush_in = [&](uint8_t* B) -> int {
+    if (pinned && in_ext) HIPCHK(hipMemcpyAsync(B, d.pin, in_ext, hipMemcpyHostToDevice, sx));
+    return EGES_SUCCESS;
+  };
+#define H2D(B, dst, src, bytes)                   \
+  do {                                             \
+    int rc_ = h2d((B), (dst), (src), (bytes));     \
+    if (rc_) return rc_;                           \
+  } while (0)
+#define FLUSH_IN(B)                 \
+  do {                              \
+    int rc_ = flush_in(B);          \
+    if (rc_) return rc_;            \
+  } while (0)
   struct Pending {
     size_t base, m;
     int r;
     uint8_t* B;
     Region g;
   };
+  const size_t astride = j.kind == HostJob::PRECOMPILE ? 32 : 20;
+  auto sighash_off = [&](const Pending& q) { return align_up(q.g.raw_len, 8) + 8 * (q.m + 1); };
   auto outputs = [&](const Pending& q) -> int {  // D2H of one chunk, on the copy stream
     uint8_t* o_pub = q.B + q.g.o_out;
     uint8_t* o_addr = o_pub + q.m * 65;
     uint8_t* o_st = o_addr + q.m * 32;
     HIPCHK(hipStreamWaitEvent(sx, d.ev_k[q.r], 0));
+    if (pinned) {  // one copy of the output area (+ the signing hashes), unpacked after the sync
+      HIPCHK(hipMemcpyAsync(d.pin + q.g.o_out, o_pub, q.m * (65 + 32 + 1), hipMemcpyDeviceToHost, sx));
+      if (j.kind == HostJob::SENDER_RAW && j.sighash)
+        HIPCHK(hipMemcpyAsync(d.pin + sighash_off(q), q.B + sighash_off(q), q.m * 32, hipMemcpyDeviceToHost, sx));
+      return EGES_SUCCESS;
+    }
     if (j.pub) HIPCHK(hipMemcpyAsync(j.pub + q.base * 65, o_pub, q.m * 65, hipMemcpyDeviceToHost, sx));
-    const size_t astride = j.kind == HostJob::PRECOMPILE ? 32 : 20;
     if (j.addr) HIPCHK(hipMemcpyAsync(j.addr + q.base * astride, o_addr, q.m * astride, hipMemcpyDeviceToHost, sx));
     if (j.status) HIPCHK(hipMemcpyAsync(j.status + q.base, o_st, q.m, hipMemcpyDeviceToHost, sx));
-    if (j.kind == HostJob::SENDER_RAW && j.sighash) {
-      const uint8_t* hs = q.B + align_up(q.g.raw_len, 8) + 8 * (q.m + 1);
-      HIPCHK(hipMemcpyAsync(j.sighash + q.base * 32, hs, q.m * 32, hipMemcpyDeviceToHost, sx));
-    }
+    if (j.kind == HostJob::SENDER_RAW && j.sighash)
+      HIPCHK(hipMemcpyAsync(j.sighash + q.base * 32, q.B + sighash_off(q), q.m * 32, hipMemcpyDeviceToHost, sx));
     return EGES_SUCCESS;
+  };
+  auto unpack = [&](const Pending& q) {  // pinned mode, after the sync
+    const uint8_t* o_pub = d.pin + q.g.o_out;
+    const uint8_t* o_addr = o_pub + q.m * 65;
+    const uint8_t* o_st = o_addr + q.m * 32;
+    if (j.pub) std::memcpy(j.pub + q.base * 65, o_pub, q.m * 65);
+    if (j.addr) std::memcpy(j.addr + q.base * astride, o_addr, q.m * astride);
+    if (j.status) std::memcpy(j.status + q.base, o_st, q.m);
+    if (j.kind == HostJob::SENDER_RAW && j.sighash) std::memcpy(j.sighash + q.base * 32, d.pin + sighash_off(q), q.m * 32);
   };
   Pending prev{};
   bool have_prev = false;
@@ -480,8 +556,9 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
     if (j.kind == HostJob::RECOVER) {
       uint8_t* dm = B;
       uint8_t* ds = dm + m * 32;
-      HIPCHK(hipMemcpyAsync(dm, j.a + base * 32, m * 32, hipMemcpyHostToDevice, sx));
-      HIPCHK(hipMemcpyAsync(ds, j.b + base * 65, m * 65, hipMemcpyHostToDevice, sx));
+      H2D(B, dm, j.a + base * 32, m * 32);
+      H2D(B, ds, j.b + base * 65, m * 65);
+      FLUSH_IN(B);
       HIPCHK(hipEventRecord(d.ev_in[r], sx));
       HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
       HIPCHK(launch_prep_ecrecover(dm, ds, (uint32_t)m, (uint32_t)m_pad, rec, st));
@@ -494,11 +571,12 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       uint8_t* dsv = dr + m * 32;
       uint8_t* dv = dsv + m * 32;
       uint8_t* df = dv + m * 32;
-      HIPCHK(hipMemcpyAsync(dh, j.a + base * 32, m * 32, hipMemcpyHostToDevice, sx));
-      HIPCHK(hipMemcpyAsync(dr, j.b + base * 32, m * 32, hipMemcpyHostToDevice, sx));
-      HIPCHK(hipMemcpyAsync(dsv, j.c + base * 32, m * 32, hipMemcpyHostToDevice, sx));
-      HIPCHK(hipMemcpyAsync(dv, j.d + base * 32, m * 32, hipMemcpyHostToDevice, sx));
-      if (j.e) HIPCHK(hipMemcpyAsync(df, j.e + base, m, hipMemcpyHostToDevice, sx));
+      H2D(B, dh, j.a + base * 32, m * 32);
+      H2D(B, dr, j.b + base * 32, m * 32);
+      H2D(B, dsv, j.c + base * 32, m * 32);
+      H2D(B, dv, j.d + base * 32, m * 32);
+      if (j.e) H2D(B, df, j.e + base, m);
+      FLUSH_IN(B);
       HIPCHK(hipEventRecord(d.ev_in[r], sx));
       HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
       HIPCHK(launch_prep_sender(dh, dr, dsv, dv, j.e ? df : nullptr, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id,
@@ -508,8 +586,9 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
     } else if (j.kind == HostJob::PRECOMPILE) {
       uint8_t* din = B;
       uint32_t* dlen = reinterpret_cast<uint32_t*>(din + m * 128);
-      HIPCHK(hipMemcpyAsync(din, j.a + base * 128, m * 128, hipMemcpyHostToDevice, sx));
-      if (j.inlen) HIPCHK(hipMemcpyAsync(dlen, j.inlen + base, m * 4, hipMemcpyHostToDevice, sx));
+      H2D(B, din, j.a + base * 128, m * 128);
+      if (j.inlen) H2D(B, reinterpret_cast<uint8_t*>(dlen), j.inlen + base, m * 4);
+      FLUSH_IN(B);
       HIPCHK(hipEventRecord(d.ev_in[r], sx));
       HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
       HIPCHK(hipMemsetAsync(o_addr, 0, m * 32, st));
@@ -524,8 +603,9 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       uint8_t* sr = rr + m * 32;
       uint8_t* vr = sr + m * 32;
       uint8_t* vf = vr + m * 32;
-      if (rg.raw_len) HIPCHK(hipMemcpyAsync(draw, j.a + rg.raw_lo, rg.raw_len, hipMemcpyHostToDevice, sx));
-      HIPCHK(hipMemcpyAsync(doff, j.offsets + base, 8 * (m + 1), hipMemcpyHostToDevice, sx));
+      if (rg.raw_len) H2D(B, draw, j.a + rg.raw_lo, rg.raw_len);
+      H2D(B, reinterpret_cast<uint8_t*>(doff), j.offsets + base, 8 * (m + 1));
+      FLUSH_IN(B);
       HIPCHK(hipEventRecord(d.ev_in[r], sx));
       HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
       HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, vf, st));
@@ -537,10 +617,11 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       uint8_t* dl = dp + m * 65;
       uint8_t* dm = dl + m;
       uint8_t* ds = dm + m * 32;
-      HIPCHK(hipMemcpyAsync(dp, j.a + base * 65, m * 65, hipMemcpyHostToDevice, sx));
-      HIPCHK(hipMemcpyAsync(dl, j.b + base, m, hipMemcpyHostToDevice, sx));
-      HIPCHK(hipMemcpyAsync(dm, j.c + base * 32, m * 32, hipMemcpyHostToDevice, sx));
-      HIPCHK(hipMemcpyAsync(ds, j.d + base * 64, m * 64, hipMemcpyHostToDevice, sx));
+      H2D(B, dp, j.a + base * 65, m * 65);
+      H2D(B, dl, j.b + base, m);
+      H2D(B, dm, j.c + base * 32, m * 32);
+      H2D(B, ds, j.d + base * 64, m * 64);
+      FLUSH_IN(B);
       HIPCHK(hipEventRecord(d.ev_in[r], sx));
       HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
       VerifyParams p{dp, dl, dm, ds, (uint32_t)m, o_st, d.gtab, d.ws};
@@ -562,7 +643,10 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
   }
   HIPCHK(hipEventRecord(d.last, sx));
   HIPCHK(hipStreamSynchronize(sx));
+  if (pinned && have_prev) unpack(prev);
   return EGES_SUCCESS;
+#undef H2D
+#undef FLUSH_IN
 }
 
 // Contiguous index shards across the engine's devices.

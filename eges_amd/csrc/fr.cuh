@@ -210,33 +210,50 @@ DEV bool fr_is_zero(fr a) { return fe_is_zero(fr_to_fe(a)); }
 DEV bool fr_equal(fr a, fr b) { return fr_is_zero(fr_sub<1>(a, b)); }
 
 // ------------------------------------------------------------------ quad steps
-// Per-row operand choice: row r of the result takes x_r.
+// The latency kernel gives each signature a whole wave; a value used by the formulas is held
+// "replicated" (all four rows alike). A quad step computes up to four independent products of
+// one formula level at once, row r taking operands a_r, b_r (v_cndmask on the row), and hands
+// the four results back replicated with gfx950's v_permlane16_swap / v_permlane32_swap
+// (three VALU instructions for all four rows, no LDS round trip).
 DEV uint32_t rowsel(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
   const uint32_t r = row_id();
-  return r == 0 ? x0 : r == 1 ? x1 : r == 2 ? x2 : x3;
+  uint32_t v = x0;
+  v = r == 1 ? x1 : v;
+  v = r == 2 ? x2 : v;
+  v = r == 3 ? x3 : v;
+  return v;
 }
 DEV fr rowsel(fr a0, fr a1, fr a2, fr a3) { return fr{rowsel(a0.v, a1.v, a2.v, a3.v)}; }
-template <int R>
-DEV fr rep(fr a) { return fr{rep_row<R>(a.v)}; }
 
-// Four independent products in one pass (row r: a_r * b_r), results replicated to every row.
+// p = (p0, p1, p2, p3) by row -> each row's value replicated over the wave
+DEV void rep4(uint32_t p, uint32_t& r0, uint32_t& r1, uint32_t& r2, uint32_t& r3) {
+  const auto a = __builtin_amdgcn_permlane16_swap(p, p, false, false);      // (p0 p0 p2 p2), (p1 p1 p3 p3)
+  const auto b = __builtin_amdgcn_permlane32_swap(a[0], a[0], false, false);  // (p0 x4), (p2 x4)
+  const auto c = __builtin_amdgcn_permlane32_swap(a[1], a[1], false, false);  // (p1 x4), (p3 x4)
+  r0 = b[0];
+  r2 = b[1];
+  r1 = c[0];
+  r3 = c[1];
+}
+DEV void rep4(fr p, fr& r0, fr& r1, fr& r2, fr& r3) { rep4(p.v, r0.v, r1.v, r2.v, r3.v); }
+DEV void rep2(fr p, fr& r0, fr& r1) {  // rows (0, 1) -> replicated
+  const auto a = __builtin_amdgcn_permlane16_swap(p.v, p.v, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(a[0], a[0], false, false);
+  const auto c = __builtin_amdgcn_permlane32_swap(a[1], a[1], false, false);
+  r0.v = b[0];
+  r1.v = c[0];
+}
+
+// Independent products in one pass (row r: a_r * b_r), results replicated.
 DEV void fr_mul4(fr& r0, fr& r1, fr& r2, fr& r3, fr a0, fr b0, fr a1, fr b1, fr a2, fr b2, fr a3, fr b3) {
-  const fr p = fr_mul(rowsel(a0, a1, a2, a3), rowsel(b0, b1, b2, b3));
-  r0 = rep<0>(p);
-  r1 = rep<1>(p);
-  r2 = rep<2>(p);
-  r3 = rep<3>(p);
+  rep4(fr_mul(rowsel(a0, a1, a2, a3), rowsel(b0, b1, b2, b3)), r0, r1, r2, r3);
 }
 DEV void fr_mul3(fr& r0, fr& r1, fr& r2, fr a0, fr b0, fr a1, fr b1, fr a2, fr b2) {
-  const fr p = fr_mul(rowsel(a0, a1, a2, a2), rowsel(b0, b1, b2, b2));
-  r0 = rep<0>(p);
-  r1 = rep<1>(p);
-  r2 = rep<2>(p);
+  fr r3;
+  rep4(fr_mul(rowsel(a0, a1, a2, a2), rowsel(b0, b1, b2, b2)), r0, r1, r2, r3);
 }
 DEV void fr_mul2(fr& r0, fr& r1, fr a0, fr b0, fr a1, fr b1) {
-  const fr p = fr_mul(rowsel(a0, a1, a0, a1), rowsel(b0, b1, b0, b1));
-  r0 = rep<0>(p);
-  r1 = rep<1>(p);
+  rep2(fr_mul(rowsel(a0, a1, a0, a1), rowsel(b0, b1, b0, b1)), r0, r1);
 }
 
 }  // namespace eges

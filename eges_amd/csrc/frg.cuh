@@ -1,13 +1,16 @@
 #pragma once
-// secp256k1 group law in row form (fr.cuh) for the latency kernel (k_recover_lat.hip).
+// secp256k1 group law for the latency kernel (k_recover_lat.hip): one signature per wave,
+// field elements in row form (fr.cuh) held replicated over the four rows, and every formula
+// level's independent products computed together as one quad step (row r: product r).
 //
-// The same formulas, exceptional-case flags and magnitude bookkeeping as ge.cuh (dbl-2009-l
+// The formulas, exceptional-case flags and magnitude bookkeeping follow ge.cuh (dbl-2009-l
 // doubling, madd-2007-bl mixed addition with the ADD_ZINV variant of group_impl.h:463-517,
-// Meloni co-Z dblu / zaddu for the table, ge_set_xo_var group_impl.h:216-237), written over
-// row-form field elements: every row of a wave holds one signature's point, every field
-// product is limb-parallel over the row's lanes. Independent products of a formula are
-// adjacent so the compiler can interleave their instruction streams (a latency-bound single
-// wave per SIMD needs that ILP).
+// Meloni co-Z dblu / zaddu for the table, ge_set_xo_var group_impl.h:216-237). Levels:
+//   doubling        2M + 5S in 3 quad steps  {X^2, Y^2, YZ} {B^2, (X+B)^2, E^2} {E (2D - X3)}
+//   mixed addition  8M + 3S in 5 quad steps  {Z1^2, y2 Z1} {U2 - X1, S2 - Y1} {H^2, Z1 H, R^2}
+//                                            {H I, X1 I} {R2 (V - X3), Y1 J}   (+1 for ZINV)
+//   co-Z addition   4M + 2S in 4 quad steps
+// where a lane-serial kernel pays one product after another.
 #include "fr.cuh"
 
 namespace eges {
@@ -19,73 +22,81 @@ struct ger {
   fr x, y;
 };
 
-DEV gejr gejr_double(const gejr& a) {
-  const fr A = fr_sqr(a.x);
-  const fr B = fr_sqr(a.y);
-  const fr yz = fr_mul(a.y, a.z);
-  const fr C = fr_sqr(B);
-  const fr D = fr_sqr_sub<2>(fr_add(a.x, B), fr_add(A, C));  // (X+B)^2 - A - C = 2 X Y^2
-  const fr E = fr_normalize_weak(fr_add(fr_add(A, A), A));   // 3 X^2
+// In: X m1, Y <= 2, Z <= 2. Out: X, Y m1, Z m2. Z == 0 stays 0.
+DEV gejr gejq_double(const gejr& a) {
+  fr A, B, YZ;
+  fr_mul3(A, B, YZ, a.x, a.x, a.y, a.y, a.y, a.z);
+  const fr E = fr_normalize_weak(fr_add(fr_add(A, A), A));  // 3 X^2
+  const fr XB = fr_add(a.x, B);
+  fr C, T, F;
+  fr_mul3(C, T, F, B, B, XB, XB, E, E);
+  const fr D = fr_normalize_weak(fr_sub<2>(T, fr_add(A, C)));       // (X+B)^2 - A - C = 2 X Y^2
   gejr r;
-  r.x = fr_sqr_sub<1, 2>(E, D);                               // E^2 - 4D
-  const fr D2 = fr_add(D, D);
-  r.y = fr_mul_sub<1, 3>(E, fr_sub<1>(D2, r.x), C);           // E (4XY^2 - X3) - 8C
-  r.z = fr_add(yz, yz);
+  r.x = fr_normalize_weak(fr_sub<3>(F, fr_mul_small(D, 4)));        // E^2 - 4D
+  r.y = fr_mul_sub<1, 3>(E, fr_sub<1>(fr_add(D, D), r.x), C);      // E (4XY^2 - X3) - 8C
+  r.z = fr_add(YZ, YZ);                                             // 2 Y Z
   return r;
 }
 
-// Mixed addition (ge.cuh gej_add_ge_t): PLAIN, or ZINV (b on the true curve, a on the table's
-// isomorphic curve with global Z = *bzinv). CHECK computes h_zero (a == +-b) / r_zero.
+// Mixed addition (ge.cuh gej_add_ge_t). a: X m1, Y <= 2, Z <= 2, not infinity; b: x m1, y <= 2.
+// PLAIN: b in a's coordinates; ZINV: b on the true curve, a on the table's isomorphic curve
+// with global Z = *bzinv. CHECK computes h_zero (a == +-b) and r_zero.
 template <AddMode M, bool CHECK = true>
-DEV gejr gejr_add_ge_t(const gejr& a, const ger& b, const fr* bzinv, bool& h_zero, bool& r_zero) {
+DEV gejr gejq_add_ge_t(const gejr& a, const ger& b, const fr* bzinv, bool& h_zero, bool& r_zero) {
   const fr az = M == ADD_ZINV ? fr_mul(a.z, *bzinv) : a.z;
-  const fr Z1Z1 = fr_sqr(az);
-  const fr byz = fr_mul(b.y, az);
-  const fr H = fr_mul_sub<1>(b.x, Z1Z1, a.x);
-  const fr R = fr_mul_sub<2>(byz, Z1Z1, a.y);
+  fr Z1Z1, byz;
+  fr_mul2(Z1Z1, byz, az, az, b.y, az);
+  // H = b.x Z1Z1 - X1 (row 0) and R = b.y Z1^3 - Y1 (row 1), subtrahends preset per row
+  fr H, R;
+  rep2(fr_mul_sub<2>(rowsel(b.x, byz, b.x, byz), Z1Z1, rowsel(a.x, a.y, a.x, a.y)), H, R);
   if (CHECK) {
     h_zero = fr_is_zero(H);
     r_zero = fr_is_zero(R);
   }
-  const fr HH = fr_sqr(H);
-  const fr zh = fr_mul(a.z, H);
+  fr HH, zh, RR;
+  fr_mul3(HH, zh, RR, H, H, a.z, H, R, R);
   const fr HH2 = fr_add(HH, HH);
-  const fr I = fr_add(HH2, HH2);
-  const fr J = fr_mul(H, I);
-  const fr V = fr_mul(a.x, I);
-  const fr R2 = fr_add(R, R);
+  const fr I = fr_add(HH2, HH2);                                      // 4 HH, m4
+  fr J, V;
+  fr_mul2(J, V, H, I, a.x, I);
+  const fr R2sq = fr_normalize_weak(fr_mul_small(RR, 4));            // (2R)^2
   gejr r;
-  r.x = fr_sqr_sub<2>(R2, fr_add(J, fr_add(V, V)));
-  const fr YJ = fr_mul(a.y, J);
-  r.y = fr_mul_sub<1, 1>(R2, fr_sub<1>(V, r.x), YJ);
-  r.z = fr_add(zh, zh);
+  r.x = fr_normalize_weak(fr_sub<2>(R2sq, fr_add(J, fr_add(V, V))));  // R2^2 - J - 2V
+  const fr R2 = fr_add(R, R);
+  fr W, YJ;
+  fr_mul2(W, YJ, R2, fr_sub<1>(V, r.x), a.y, J);
+  r.y = fr_normalize_weak(fr_sub<2>(W, fr_add(YJ, YJ)));             // R2 (V - X3) - 2 Y1 J
+  r.z = fr_add(zh, zh);                                               // 2 Z1 H
   return r;
 }
 
-DEV void gejr_dblu(gejr& d, ger& p1, const ger& p) {
-  const fr A = fr_sqr(p.x);
-  const fr B = fr_sqr(p.y);
-  const fr C = fr_sqr(B);
-  const fr D = fr_sqr_sub<2>(fr_add(p.x, B), fr_add(A, C));
+// Start of the co-Z table: d = 2p in Jacobian with Z = 2y, and p1 = p on that same Z.
+DEV void gejq_dblu(gejr& d, ger& p1, const ger& p) {
+  fr A, B;
+  fr_mul2(A, B, p.x, p.x, p.y, p.y);
   const fr E = fr_normalize_weak(fr_add(fr_add(A, A), A));
-  d.x = fr_sqr_sub<1, 2>(E, D);
-  const fr D2 = fr_add(D, D);
-  d.y = fr_mul_sub<1, 3>(E, fr_sub<1>(D2, d.x), C);
+  const fr XB = fr_add(p.x, B);
+  fr C, T, F;
+  fr_mul3(C, T, F, B, B, XB, XB, E, E);
+  const fr D = fr_normalize_weak(fr_sub<2>(T, fr_add(A, C)));  // 2 x y^2
+  d.x = fr_normalize_weak(fr_sub<3>(F, fr_mul_small(D, 4)));
+  d.y = fr_mul_sub<1, 3>(E, fr_sub<1>(fr_add(D, D), d.x), C);
   d.z = fr_add(p.y, p.y);
-  p1.x = fr_normalize_weak(D2);
-  p1.y = fr_normalize_weak(fr_mul_small(fr_normalize_weak(fr_mul_small(C, 4)), 2));
+  p1.x = fr_normalize_weak(fr_add(D, D));                        // x (2y)^2 = 4 x y^2
+  p1.y = fr_normalize_weak(fr_mul_small(fr_normalize_weak(fr_mul_small(C, 4)), 2));  // 8 y^4
 }
 
-DEV fr gejr_zaddu(ger& t, ger& b) {
+// Co-Z addition with update (ge.cuh gej_zaddu): t <- t + b, b <- b, both on Z' = Z (X_t - X_b);
+// returns Z'/Z. t == +-b is the caller's to exclude. X, Y magnitude 1 in and out.
+DEV fr gejq_zaddu(ger& t, ger& b) {
   const fr dx = fr_normalize_weak(fr_sub<1>(t.x, b.x));
   const fr dy = fr_normalize_weak(fr_sub<1>(t.y, b.y));
-  const fr A = fr_sqr(dx);
-  const fr dy2 = fr_sqr(dy);
-  const fr B = fr_mul(b.x, A);
-  const fr C = fr_mul(t.x, A);
+  fr A, dy2;
+  fr_mul2(A, dy2, dx, dx, dy, dy);
+  fr B, C;
+  fr_mul2(B, C, b.x, A, t.x, A);
   const fr E = fr_mul(b.y, fr_sub<1>(C, B));
-  t.x = fr_sub<2>(dy2, fr_add(B, C));
-  t.x = fr_normalize_weak(t.x);
+  t.x = fr_normalize_weak(fr_sub<2>(dy2, fr_add(B, C)));
   t.y = fr_mul_sub<1>(dy, fr_sub<1>(B, t.x), E);
   b.x = B;
   b.y = E;
@@ -127,8 +138,7 @@ DEV bool fr_sqrt(fr& r, fr a) {
   return fr_equal(fr_sqr(t), a);
 }
 
-// y from x (canonical or magnitude 1) with the requested parity; false for a non-residue.
-// Returned coordinates are canonical.
+// y from x (magnitude 1) with the requested parity; false for a non-residue. Canonical out.
 DEV bool ger_set_xo(ger& r, fr x, bool odd) {
   const fr c = fr_add(fr_mul(fr_sqr(x), x), fr_small(7));
   fr y;

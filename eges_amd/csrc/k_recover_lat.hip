@@ -1,31 +1,33 @@
-// Latency kernel for small recover batches: one signature per 16-lane row (4 per wave).
+// Latency kernel for small recover batches: one signature per wave.
 //
 // Same path and same outputs as recover_kernel (k_recover.hip; recovery/main_impl.h:38-191,
 // ecmult_impl.h:286-404, eckey_impl.h:36-52, crypto.go:194-197), for batches too small to fill
 // the GPU with one signature per lane: there, a signature costs one lane's serial chain
-// (~0.78 ms for a 1000-transaction block on 16 of 1024 SIMDs). Here every field product is
-// limb-parallel over the 16 lanes of the signature's row (fr.cuh), so a block of 1000
-// signatures spreads over 250 waves and each signature's chain is shorter.
+// (~0.78 ms for a 1000-transaction block on 16 of 1024 SIMDs). Here a signature has a whole
+// wave: every field product is limb-parallel over a 16-lane row (fr.cuh), and the four rows
+// compute the independent products of each formula level together (quad steps, frg.cuh), so
+// a 1000-signature block spreads over 1000 waves and each signature's chain is ~4x shorter.
 //
 //   parse, x = r (+n), R = lift_x(x) ...... row form (fr_sqrt), failures carry G and r = 1
-//   r^-1, u1 = -z/r, u2 = s/r, GLV split . lane-serial code, every lane of the row alike
+//   r^-1, u1 = -z/r, u2 = s/r, GLV split . lane-serial code, every lane alike
 //   table {1..16}R on one global Z ....... co-Z dblu / zaddu + backward rescale (as core.cuh)
-//   Strauss over 26 windows ............. unchecked adds, exact redo of the wave if a row's
+//   Strauss over 26 windows ............. unchecked adds, exact redo if the
 //                                          accumulator was poisoned (Z == 0 and not infinity)
-//   Z^-1 (safegcd, lane-serial), affine, serialize, Keccak address; lane 0 of the row stores.
+//   Z^-1 (safegcd, lane-serial), affine, serialize, Keccak address; lane 0 stores.
+#include <type_traits>
+
 #include "core.cuh"
 #include "frg.cuh"
 
 namespace eges {
 
-constexpr int LAT_WG = 256;
-constexpr int LROWS = LAT_WG / 16;  // signatures per block
+constexpr int LAT_WG = 64;  // one wave = one signature
 
 struct LatLds {
-  uint32_t tab[LROWS][PTAB][2][16];  // {1..16} * R (x, y), row form, per signature
-  uint32_t zr[LROWS][PTAB][16];      // Z ratios while the table is built
-  int8_t rdig[LROWS][2][RWIN];
-  gdig_t gdig[LROWS][2][GWIN];
+  uint32_t tab[PTAB][2][16];  // {1..16} * R (x, y), row form (all four rows read the same words)
+  uint32_t zr[PTAB][16];      // Z ratios while the table is built
+  int8_t rdig[2][RWIN];
+  gdig_t gdig[2][GWIN];
 };
 
 // signed fixed-window recoding (core.cuh recode) into this row's digit array
@@ -40,7 +42,7 @@ DEV void recode_row(const glv_half& h, D* out) {
     int v = (int)(m[0] & ((1u << W) - 1)) + carry;
     carry = v > (1 << (W - 1)) ? 1 : 0;
     v -= carry << W;
-    out[w] = (D)(h.neg ? -v : v);  // every lane of the row writes the same value
+    out[w] = (D)(h.neg ? -v : v);  // every lane writes the same value
 #pragma unroll
     for (int i = 0; i < 4; ++i) m[i] = (m[i] >> W) | (m[i + 1] << (32 - W));
     m[4] >>= W;
@@ -77,20 +79,20 @@ DEV ger ger_neg_if(const ger& p, bool neg) {
   return r;
 }
 
-// acc += p (core.cuh add_step / add_step_fast, row form; inf is row-uniform)
+// acc += p (core.cuh add_step / add_step_fast, quad form; inf is wave-uniform)
 template <bool CHECKED>
 DEV void add_r(gejr& acc, bool& inf, const ger& p, bool use) {
   gejr s;
   bool to_inf = false;
   if (CHECKED) {
     bool hz, rz;
-    s = gejr_add_ge_t<ADD_PLAIN, true>(acc, p, nullptr, hz, rz);
+    s = gejq_add_ge_t<ADD_PLAIN, true>(acc, p, nullptr, hz, rz);
     const bool exc = use && !inf && hz;
-    if (__any(exc)) s = gejr_select(exc && rz, gejr_double(acc), s);
+    if (__any(exc)) s = gejr_select(exc && rz, gejq_double(acc), s);
     to_inf = exc && !rz;
   } else {
     bool h, r;
-    s = gejr_add_ge_t<ADD_PLAIN, false>(acc, p, nullptr, h, r);
+    s = gejq_add_ge_t<ADD_PLAIN, false>(acc, p, nullptr, h, r);
   }
   gejr pj;
   pj.x = p.x;
@@ -107,13 +109,13 @@ DEV void add_r_zinv(gejr& acc, bool& inf, const ger& p, bool use, const fr& zeta
   bool to_inf = false;
   if (CHECKED) {
     bool hz, rz;
-    s = gejr_add_ge_t<ADD_ZINV, true>(acc, p, &zeta, hz, rz);
+    s = gejq_add_ge_t<ADD_ZINV, true>(acc, p, &zeta, hz, rz);
     const bool exc = use && !inf && hz;
-    if (__any(exc)) s = gejr_select(exc && rz, gejr_double(acc), s);
+    if (__any(exc)) s = gejr_select(exc && rz, gejq_double(acc), s);
     to_inf = exc && !rz;
   } else {
     bool h, r;
-    s = gejr_add_ge_t<ADD_ZINV, false>(acc, p, &zeta, h, r);
+    s = gejq_add_ge_t<ADD_ZINV, false>(acc, p, &zeta, h, r);
   }
   if (__any(use && inf)) {  // acc = p mapped onto the isomorphic curve: (x zeta^2, y zeta^3, 1)
     const fr z2 = fr_sqr(zeta);
@@ -129,8 +131,7 @@ DEV void add_r_zinv(gejr& acc, bool& inf, const ger& p, bool use, const fr& zeta
 }
 
 template <bool CHECKED>
-DEV void strauss_row(gejr& acc, bool& inf, LatLds& S, int row, const uint32_t* gtab, const fr& zeta,
-                     const fr& beta) {
+DEV void strauss_wave(gejr& acc, bool& inf, LatLds& S, const uint32_t* gtab, const fr& zeta, const fr& beta) {
   inf = true;
   acc.x = fr_zero();
   acc.y = fr_zero();
@@ -139,16 +140,16 @@ DEV void strauss_row(gejr& acc, bool& inf, LatLds& S, int row, const uint32_t* g
   for (int w = RWIN - 1; w >= 0; --w) {
     if (w != RWIN - 1) {
 #pragma unroll 1
-      for (int k = 0; k < RBITS; ++k) acc = gejr_double(acc);
+      for (int k = 0; k < RBITS; ++k) acc = gejq_double(acc);
     }
     const int nadd = (w % GSTEP) == 0 ? 4 : 2;
 #pragma unroll 1
     for (int j = 0; j < nadd; ++j) {
-      const int d = j < 2 ? (int)S.rdig[row][j][w] : (int)S.gdig[row][j - 2][w / GSTEP];
+      const int d = j < 2 ? (int)S.rdig[j][w] : (int)S.gdig[j - 2][w / GSTEP];
       const int a = d < 0 ? -d : d;
       const int e = a > 0 ? a - 1 : 0;
       if (j < 2) {
-        ger p = lds_pt(S.tab[row][e]);
+        ger p = lds_pt(S.tab[e]);
         if (j == 1) p.x = fr_mul(p.x, beta);
         add_r<CHECKED>(acc, inf, ger_neg_if(p, d < 0), d != 0);
       } else {
@@ -159,14 +160,15 @@ DEV void strauss_row(gejr& acc, bool& inf, LatLds& S, int row, const uint32_t* g
   }
 }
 
-// Q = u_r * P + u_g * G for this row's signature (core.cuh ecmult_core, row form)
-DEV void ecmult_row(gejr& acc, bool& inf, const ger& P, const sc& u_r, const sc& u_g, const uint32_t* gtab,
-                    LatLds& S, int row, const fr& beta) {
+// Q = u_r * P + u_g * G for this wave's signature (core.cuh ecmult_core, quad form)
+template <class ST>
+DEV void ecmult_wave(gejr& acc, bool& inf, const ger& P, const sc& u_r, const sc& u_g, const uint32_t* gtab,
+                     LatLds& S, const fr& beta, ST* st) {
   {
     glv_half h1, h2;
     glv_split(h1, h2, u_r);
-    recode_row<RBITS, RWIN, int8_t>(h1, S.rdig[row][0]);
-    recode_row<RBITS, RWIN, int8_t>(h2, S.rdig[row][1]);
+    recode_row<RBITS, RWIN, int8_t>(h1, S.rdig[0]);
+    recode_row<RBITS, RWIN, int8_t>(h2, S.rdig[1]);
     glv_half g0, g1;
     g0.neg = false;
     g1.neg = false;
@@ -177,55 +179,68 @@ DEV void ecmult_row(gejr& acc, bool& inf, const ger& P, const sc& u_r, const sc&
     }
     g0.mag[4] = 0;
     g1.mag[4] = 0;
-    recode_row<GBITS, GWIN, gdig_t>(g0, S.gdig[row][0]);
-    recode_row<GBITS, GWIN, gdig_t>(g1, S.gdig[row][1]);
+    recode_row<GBITS, GWIN, gdig_t>(g0, S.gdig[0]);
+    recode_row<GBITS, GWIN, gdig_t>(g1, S.gdig[1]);
   }
+  st->mark(2);
   // table {1..PTAB} * P on one global Z (co-Z additions, backward rescale; core.cuh)
   fr zeta;
   {
-    lds_put_pt(S.tab[row][0], P);
+    const uint32_t L = row_lane();
+    lds_put_pt(S.tab[0], P);
     gejr D;
     ger B;
-    gejr_dblu(D, B, P);
-    S.zr[row][0][row_lane()] = D.z.v;  // Z_2 / Z_1 = 2y
+    gejq_dblu(D, B, P);
+    S.zr[0][L] = D.z.v;  // Z_2 / Z_1 = 2y
     ger T;
     T.x = D.x;
     T.y = D.y;
-    lds_put_pt(S.tab[row][1], T);
+    lds_put_pt(S.tab[1], T);
 #pragma unroll 1
     for (int i = 2; i < PTAB; ++i) {
-      const fr zr = gejr_zaddu(T, B);  // T = (i+1) P
-      lds_put_pt(S.tab[row][i], T);
-      S.zr[row][i - 1][row_lane()] = zr.v;
+      const fr zr = gejq_zaddu(T, B);  // T = (i+1) P
+      lds_put_pt(S.tab[i], T);
+      S.zr[i - 1][L] = zr.v;
     }
-    fr rho = fr_one();
+    // entry i (< PTAB - 1) is rescaled by rho_i = prod_{k=i}^{PTAB-2} Z_{k+2}/Z_{k+1} = Z_PTAB / Z_{i+1}:
+    // x rho^2, y rho^3, software-pipelined two quad steps per entry
+    fr rho{S.zr[PTAB - 2][L]};
+    fr s2 = fr_sqr(rho);
 #pragma unroll 1
     for (int i = PTAB - 2; i >= 0; --i) {
-      const fr zr{S.zr[row][i][row_lane()]};  // Z_{i+2} / Z_{i+1}
-      rho = i == PTAB - 2 ? zr : fr_mul(rho, zr);
-      const ger J = lds_pt(S.tab[row][i]);
-      const fr r2 = fr_sqr(rho);
-      const fr r3 = fr_mul(r2, rho);
+      const ger J = lds_pt(S.tab[i]);
+      const fr zn{S.zr[i > 0 ? i - 1 : 0][L]};
+      fr ax, s3, rho_n;
+      fr_mul3(ax, s3, rho_n, J.x, s2, s2, rho, rho, zn);   // x rho^2, rho^3, next rho
+      fr ay, s2_n;
+      fr_mul2(ay, s2_n, J.y, s3, rho_n, rho_n);            // y rho^3, next rho^2
       ger a;
-      a.x = fr_mul(J.x, r2);
-      a.y = fr_mul(J.y, r3);
-      lds_put_pt(S.tab[row][i], a);
+      a.x = ax;
+      a.y = ay;
+      lds_put_pt(S.tab[i], a);
+      if (i == 0) break;
+      rho = rho_n;
+      s2 = s2_n;
     }
-    zeta = rho;
+    zeta = rho;  // rho_0 = Z_PTAB / Z_1 with Z_1 = 1
   }
-  strauss_row<false>(acc, inf, S, row, gtab, zeta, beta);
-  if (__any(!inf && fr_is_zero(acc.z))) strauss_row<true>(acc, inf, S, row, gtab, zeta, beta);
+  st->mark(3);
+  strauss_wave<false>(acc, inf, S, gtab, zeta, beta);
+  if (__any(!inf && fr_is_zero(acc.z))) strauss_wave<true>(acc, inf, S, gtab, zeta, beta);
   acc.z = fr_mul(acc.z, zeta);
+  st->mark(4);
 }
 
-__global__ void __launch_bounds__(LAT_WG) recover_lat_kernel(RecoverParams prm) {
+// Phase marks (diagnostic build only): 0 parse + lift, 1 r^-1 + u1/u2, 2 GLV + digits,
+// 3 table, 4 Strauss, 5 Z^-1 + affine, 6 Keccak + stores.
+template <class ST>
+DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   __shared__ LatLds S;
-  const int row = (int)(threadIdx.x >> 4);
-  const uint32_t idx0 = blockIdx.x * LROWS + (uint32_t)row;
-  const bool in = idx0 < prm.n;
-  const uint32_t idx = in ? idx0 : prm.n - 1;
+  ST st_;
+  ST* st = &st_;
+  const uint32_t idx = blockIdx.x;  // grid = n: every wave has a signature
   const uint32_t np = prm.n_pad;
-  // --- parse (every lane of the row reads the same record)
+  // --- parse (every lane reads the same record)
   uint32_t rl[8], sl[8], zl[8];
   rec_get(prm, 8, idx, rl);
   rec_get(prm, 16, idx, sl);
@@ -258,27 +273,33 @@ __global__ void __launch_bounds__(LAT_WG) recover_lat_kernel(RecoverParams prm) 
   Rp.x = fr_select(ok, Rp.x, fe_to_fr(G.x));
   Rp.y = fr_select(ok, Rp.y, fe_to_fr(G.y));
   R = sc_select(ok, R, sc_one());
+  st->mark(0);
   // --- u1 = -z / r, u2 = s / r (main_impl.h:114-117)
   const sc rinv = sc_inv(R);
   const sc u1 = sc_neg(sc_mul(rinv, Z));
   const sc u2 = sc_select(ok, sc_mul(rinv, Sv), sc_one());
+  st->mark(1);
   // --- Q = u2 R + u1 G
   const fr beta = fe_to_fr(fe_const(FE_BETA));
   gejr Q;
   bool qinf;
-  ecmult_row(Q, qinf, Rp, u2, u1, prm.gtab, S, row, beta);
+  ecmult_wave(Q, qinf, Rp, u2, u1, prm.gtab, S, beta, st);
   ok = ok && !qinf;  // main_impl.h:120
   // --- affine, serialize, address
   const fr zq = fr_select(ok, Q.z, fr_one());
   const fr zi = fe_to_fr(fe_inv(fr_to_fe(zq)));
-  const fr zi2 = fr_sqr(zi);
-  const fr zi3 = fr_mul(zi2, zi);
+  fr zi2, zi3;
+  zi2 = fr_sqr(zi);
+  fr X1, Y1;
+  fr_mul2(X1, zi3, Q.x, zi2, zi2, zi);
+  Y1 = fr_mul(Q.y, zi3);
   uint32_t X[8], Y[8];
-  fe_to_u256(X, fe_normalize(fr_to_fe(fr_mul(Q.x, zi2))));
-  fe_to_u256(Y, fe_normalize(fr_to_fe(fr_mul(Q.y, zi3))));
+  fe_to_u256(X, fe_normalize(fr_to_fe(X1)));
+  fe_to_u256(Y, fe_normalize(fr_to_fe(Y1)));
+  st->mark(5);
   uint32_t a[5];
   pub_address(a, X, Y);
-  if (in && row_lane() == 0) {
+  if (lane_id() == 0) {
     const uint32_t pre_st = (meta >> 8) & 0xffu;
     prm.status[idx] = (uint8_t)(pre_st != ST_OK ? pre_st : (ok ? ST_OK : ST_RECOVER_FAILED));
     if (prm.addr) {
@@ -297,12 +318,35 @@ __global__ void __launch_bounds__(LAT_WG) recover_lat_kernel(RecoverParams prm) 
       }
     }
   }
+  st->mark(6);
+  if constexpr (!std::is_same<ST, NoStamp>::value) {
+    if (lane_id() == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) stamps[(size_t)blockIdx.x * 8 + i] = st_.acc[i];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(LAT_WG) recover_lat_kernel(RecoverParams prm) {
+  recover_lat_body<NoStamp>(prm, nullptr);
 }
 
 hipError_t launch_recover_lat(const RecoverParams& p, hipStream_t st) {
   if (p.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(recover_lat_kernel, dim3((p.n + LROWS - 1) / LROWS), dim3(LAT_WG), 0, st, p);
+  hipLaunchKernelGGL(recover_lat_kernel, dim3(p.n), dim3(LAT_WG), 0, st, p);
   return hipGetLastError();
 }
+
+#ifdef EGES_PHASE_STAMPS
+__global__ void __launch_bounds__(LAT_WG) recover_lat_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
+  recover_lat_body<Stamper>(prm, stamps);
+}
+hipError_t launch_recover_lat_stamped(const RecoverParams& p, hipStream_t st, uint64_t* stamps) {
+  if (p.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(recover_lat_kernel_stamped, dim3(p.n), dim3(LAT_WG), 0, st, p, stamps);
+  return hipGetLastError();
+}
+size_t lat_waves(uint32_t n) { return n; }
+#endif
 
 }  // namespace eges

@@ -82,6 +82,8 @@ hipError_t launch_tx_rows(const uint8_t* raw, const uint64_t* offsets, uint64_t 
                           hipStream_t st);
 #ifdef EGES_PHASE_STAMPS
 hipError_t launch_recover_stamped(const RecoverParams& p, int max_blocks, int ws_blocks, hipStream_t st, uint64_t* stamps);
+hipError_t launch_recover_lat_stamped(const RecoverParams& p, hipStream_t st, uint64_t* stamps);
+size_t lat_waves(uint32_t n);
 #endif
 // max_blocks: the resident grid; ws_blocks: blocks the workspace p.ws was allocated for. A
 // launch whose grid would exceed ws_blocks is refused (hipErrorInvalidValue), never run.

@@ -299,13 +299,14 @@ enum : int {
   FR_LAZY = 4,     // (2a) * (a + 2b) - 2b (a - b): magnitudes 2 x 3, fr_sub<1>
   FR_NORMW = 5,    // normalize_weak(7a) (limbs up to 7 * 2^29)
   FR_CHAIN = 6,    // 64 squarings of a, then * b
-  FR_QUAD = 7,     // fr_mul4: row-replicated a, b, c; out = a*b + b*c + c*a + a*a (4 products in one pass)
+  FR_QUAD = 7,     // fr_mul4 (a*b, b*c, c*a, a*a in one pass): out = (ab + 2bc + 3ca) * a^2
+  FR_QUAD2 = 8,    // fr_mul2 (a*b, c*c): out = ab + 2c^2
 };
 __global__ void fr_selftest_kernel(int op, uint32_t n, const uint32_t* A, const uint32_t* B, const uint32_t* C,
                                    uint32_t* out) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t item = gid >> 4;
-  if (op == FR_QUAD) item = gid >> 6;  // one item per wave: operands replicated in all rows
+  if (op >= FR_QUAD) item = gid >> 6;  // one item per wave: operands replicated in all rows
   const bool in = item < n;
   const uint32_t i = in ? item : 0;
   const fr a = fe_to_fr(ld(A, i)), b = fe_to_fr(ld(B, i)), c = fe_to_fr(ld(C, i));
@@ -334,7 +335,14 @@ __global__ void fr_selftest_kernel(int op, uint32_t n, const uint32_t* A, const 
     case FR_QUAD: {
       fr p0, p1, p2, p3;
       fr_mul4(p0, p1, p2, p3, a, b, b, c, c, a, a, a);
-      r = fr_add(fr_add(p0, p1), fr_add(p2, p3));
+      r = fr_add(fr_add(p0, fr_mul_small(p1, 2)), fr_mul_small(p2, 3));
+      r = fr_mul(r, p3);
+      break;
+    }
+    case FR_QUAD2: {
+      fr q0, q1;
+      fr_mul2(q0, q1, a, b, c, c);
+      r = fr_add(q0, fr_mul_small(q1, 2));
       break;
     }
     default: r = a;
@@ -342,7 +350,7 @@ __global__ void fr_selftest_kernel(int op, uint32_t n, const uint32_t* A, const 
   const fe o = fe_normalize(fr_to_fe(r));
   uint32_t x[8];
   fe_to_u256(x, o);
-  if (in && (threadIdx.x & (op == FR_QUAD ? 63 : 15)) == 0) {
+  if (in && (threadIdx.x & (op >= FR_QUAD ? 63 : 15)) == 0) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) out[(size_t)i * 8 + k] = x[k];
   }
@@ -377,7 +385,7 @@ extern "C" int eges_fr_selftest(int op, uint32_t n, const uint32_t* a, const uin
   (void)hipMemcpy(da, a, B, hipMemcpyHostToDevice);
   (void)hipMemcpy(db, b, B, hipMemcpyHostToDevice);
   (void)hipMemcpy(dc, c, B, hipMemcpyHostToDevice);
-  const uint32_t lanes = (op == eges::FR_QUAD ? 64u : 16u) * n;
+  const uint32_t lanes = (op >= eges::FR_QUAD ? 64u : 16u) * n;
   hipLaunchKernelGGL(eges::fr_selftest_kernel, dim3((lanes + 255) / 256), dim3(256), 0, 0, op, n, da, db, dc, dout);
   hipError_t e = hipDeviceSynchronize();
   (void)hipMemcpy(out, dout, B, hipMemcpyDeviceToHost);

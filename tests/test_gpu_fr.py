@@ -14,7 +14,7 @@ from conftest import ROOT
 from test_gpu_field import P, dec, enc, samples
 
 pytestmark = pytest.mark.gpu
-FR = dict(MUL=0, SQR=1, MULSUB=2, SUB=3, LAZY=4, NORMW=5, CHAIN=6, QUAD=7)
+FR = dict(MUL=0, SQR=1, MULSUB=2, SUB=3, LAZY=4, NORMW=5, CHAIN=6, QUAD=7, QUAD2=8)
 
 
 @pytest.fixture(scope="module")
@@ -51,8 +51,10 @@ def expect(op, a, b, c):
         return 7 * a % P
     if op == "CHAIN":
         return pow(a, 2**64, P) * b % P
-    if op == "QUAD":
-        return (a * b + b * c + c * a + a * a) % P
+    if op == "QUAD":  # rows 0..3 of one pass: ab, bc, ca, a^2 (each row's result told apart)
+        return (a * b + 2 * b * c + 3 * c * a) * a * a % P
+    if op == "QUAD2":
+        return (a * b + 2 * c * c) % P
 
 
 @pytest.mark.parametrize("op", list(FR))
