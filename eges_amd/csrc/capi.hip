@@ -475,25 +475,21 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
   }
   HIPCHK(hipStreamWaitEvent(st, d.last, 0));
   HIPCHK(hipStreamWaitEvent(sx, d.last, 0));
-  // Input staging: each input array goes to its offset in the device region B, either by its
-  // own (pageable) copy on the copy stream, or packed into the pinned buffer at the same offset
-  // and moved as one copy by flush_in().
-  size_t in_ext = 0;
+  // Input staging: each input array goes to its offset in the region, either by its own
+  // (pageable) copy into device memory on the copy stream, or, for a pinned call, packed into
+  // the pinned buffer at the same offset, where the kernels read it directly (zero-copy: no
+  // H2D / D2H operations at all, the outputs are written straight into the pinned buffer too).
   auto h2d = [&](uint8_t* B, uint8_t* dst, const void* src, size_t bytes) -> int {
     if (!bytes) return EGES_SUCCESS;
     if (pinned) {
-      const size_t o = (size_t)(dst - B);
-      std::memcpy(d.pin + o, src, bytes);
-      in_ext = std::max(in_ext, o + bytes);
+      std::memcpy(dst, src, bytes);  // dst points into the pinned buffer (see I below)
       return EGES_SUCCESS;
     }
+    (void)B;
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, sx));
     return EGES_SUCCESS;
   };
-  auto flush_in = [&](uint8_t* B) -> int {
-    if (pinned && in_ext) HIPCHK(hipMemcpyAsync(B, d.pin, in_ext, hipMemcpyHostToDevice, sx));
-    return EGES_SUCCESS;
-  };
+  auto flush_in = [&](uint8_t*) -> int { return EGES_SUCCESS; };
 #define H2D(B, dst, src, bytes)                   \
   do {                                             \
     int rc_ = h2d((B), (dst), (src), (bytes));     \
@@ -517,8 +513,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
     uint8_t* o_addr = o_pub + q.m * 65;
     uint8_t* o_st = o_addr + q.m * 32;
     HIPCHK(hipStreamWaitEvent(sx, d.ev_k[q.r], 0));
-    if (pinned) {  // one copy of the output area (+ the signing hashes), unpacked after the sync
-      HIPCHK(hipMemcpyAsync(d.pin + q.g.o_out, o_pub, q.m * (65 + 32 + 1), hipMemcpyDeviceToHost, sx));
+    if (pinned) {  // outputs are already in the pinned buffer; the signing hashes are not
       if (j.kind == HostJob::SENDER_RAW && j.sighash)
         HIPCHK(hipMemcpyAsync(d.pin + sighash_off(q), q.B + sighash_off(q), q.m * 32, hipMemcpyDeviceToHost, sx));
       return EGES_SUCCESS;
@@ -548,13 +543,14 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
     const int r = ci % nreg;
     const Region rg = region_for(j, base, m);
     uint8_t* B = d.buf + (size_t)r * worst;
-    uint8_t* o_pub = B + rg.o_out;
+    uint8_t* I = pinned ? d.pin : B;  // where the kernels read the inputs
+    uint8_t* o_pub = (pinned ? d.pin : B) + rg.o_out;
     uint8_t* o_addr = o_pub + m * 65;
     uint8_t* o_st = o_addr + m * 32;
     uint32_t* rec = reinterpret_cast<uint32_t*>(B + rg.o_rec);
     // --- inputs (copy stream), then the kernels (compute stream)
     if (j.kind == HostJob::RECOVER) {
-      uint8_t* dm = B;
+      uint8_t* dm = I;
       uint8_t* ds = dm + m * 32;
       H2D(B, dm, j.a + base * 32, m * 32);
       H2D(B, ds, j.b + base * 65, m * 65);
@@ -566,7 +562,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
                       d.gtab, d.ws};
       HIPCHK(launch_recover_pass(d, p, st));
     } else if (j.kind == HostJob::SENDER) {
-      uint8_t* dh = B;
+      uint8_t* dh = I;
       uint8_t* dr = dh + m * 32;
       uint8_t* dsv = dr + m * 32;
       uint8_t* dv = dsv + m * 32;
@@ -584,21 +580,22 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
       HIPCHK(launch_recover_pass(d, p, st));
     } else if (j.kind == HostJob::PRECOMPILE) {
-      uint8_t* din = B;
+      uint8_t* din = I;
       uint32_t* dlen = reinterpret_cast<uint32_t*>(din + m * 128);
       H2D(B, din, j.a + base * 128, m * 128);
       if (j.inlen) H2D(B, reinterpret_cast<uint8_t*>(dlen), j.inlen + base, m * 4);
       FLUSH_IN(B);
       HIPCHK(hipEventRecord(d.ev_in[r], sx));
       HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
-      HIPCHK(hipMemsetAsync(o_addr, 0, m * 32, st));
+      if (pinned) std::memset(o_addr, 0, m * 32);
+      else HIPCHK(hipMemsetAsync(o_addr, 0, m * 32, st));
       HIPCHK(launch_prep_precompile(din, j.inlen ? dlen : nullptr, (uint32_t)m, (uint32_t)m_pad, rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr + 12, nullptr, d.gtab, d.ws, 32};
       HIPCHK(launch_recover_pass(d, p, st));
     } else if (j.kind == HostJob::SENDER_RAW) {
-      uint8_t* draw = B;
+      uint8_t* draw = I;
       uint64_t* doff = reinterpret_cast<uint64_t*>(draw + align_up(rg.raw_len, 8));
-      uint8_t* hs = reinterpret_cast<uint8_t*>(doff + (m + 1));
+      uint8_t* hs = B + align_up(rg.raw_len, 8) + 8 * (m + 1);  // decoded rows: device memory
       uint8_t* rr = hs + m * 32;
       uint8_t* sr = rr + m * 32;
       uint8_t* vr = sr + m * 32;
@@ -613,7 +610,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
       HIPCHK(launch_recover_pass(d, p, st));
     } else {
-      uint8_t* dp = B;
+      uint8_t* dp = I;
       uint8_t* dl = dp + m * 65;
       uint8_t* dm = dl + m;
       uint8_t* ds = dm + m * 32;

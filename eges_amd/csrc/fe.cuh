@@ -404,5 +404,12 @@ DEV fe fe_inv(const fe& a) {
   modinv256<ModP>(y, x);
   return fe_from_u256(y);
 }
+// Variable-time form, for wave-uniform data only (the latency kernel).
+DEV fe fe_inv_var(const fe& a) {
+  uint32_t x[8], y[8];
+  fe_to_u256(x, fe_normalize(a));
+  modinv256_var<ModP>(y, x);
+  return fe_from_u256(y);
+}
 
 }  // namespace eges

@@ -9,7 +9,7 @@
 // a 1000-signature block spreads over 1000 waves and each signature's chain is ~4x shorter.
 //
 //   parse, x = r (+n), R = lift_x(x) ...... row form (fr_sqrt), failures carry G and r = 1
-//   r^-1, u1 = -z/r, u2 = s/r, GLV split . lane-serial code, every lane alike
+//   r^-1, u1 = -z/r, u2 = s/r, GLV split . wave 1, lane-serial code, concurrent with the lift
 //   table {1..16}R on one global Z ....... co-Z dblu / zaddu + backward rescale (as core.cuh)
 //   Strauss over 26 windows ............. unchecked adds, exact redo if the
 //                                          accumulator was poisoned (Z == 0 and not infinity)
@@ -21,7 +21,9 @@
 
 namespace eges {
 
-constexpr int LAT_WG = 64;  // one wave = one signature
+// One signature per workgroup of two waves: wave 0 lifts R (square root) and builds the table
+// while wave 1 computes r^-1 (safegcd), u1, u2 and the window digits; they meet at one barrier.
+constexpr int LAT_WG = 128;
 
 struct LatLds {
   uint32_t tab[PTAB][2][16];  // {1..16} * R (x, y), row form (all four rows read the same words)
@@ -161,28 +163,30 @@ DEV void strauss_wave(gejr& acc, bool& inf, LatLds& S, const uint32_t* gtab, con
 }
 
 // Q = u_r * P + u_g * G for this wave's signature (core.cuh ecmult_core, quad form)
-template <class ST>
-DEV void ecmult_wave(gejr& acc, bool& inf, const ger& P, const sc& u_r, const sc& u_g, const uint32_t* gtab,
-                     LatLds& S, const fr& beta, ST* st) {
-  {
-    glv_half h1, h2;
-    glv_split(h1, h2, u_r);
-    recode_row<RBITS, RWIN, int8_t>(h1, S.rdig[0]);
-    recode_row<RBITS, RWIN, int8_t>(h2, S.rdig[1]);
-    glv_half g0, g1;
-    g0.neg = false;
-    g1.neg = false;
+// GLV split of u_r and signed windows of both scalars (core.cuh ecmult_core's digits)
+DEV void recode_digits(const sc& u_r, const sc& u_g, LatLds& S) {
+  glv_half h1, h2;
+  glv_split(h1, h2, u_r);
+  recode_row<RBITS, RWIN, int8_t>(h1, S.rdig[0]);
+  recode_row<RBITS, RWIN, int8_t>(h2, S.rdig[1]);
+  glv_half g0, g1;
+  g0.neg = false;
+  g1.neg = false;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      g0.mag[i] = u_g.v[i];
-      g1.mag[i] = u_g.v[4 + i];
-    }
-    g0.mag[4] = 0;
-    g1.mag[4] = 0;
-    recode_row<GBITS, GWIN, gdig_t>(g0, S.gdig[0]);
-    recode_row<GBITS, GWIN, gdig_t>(g1, S.gdig[1]);
+  for (int i = 0; i < 4; ++i) {
+    g0.mag[i] = u_g.v[i];
+    g1.mag[i] = u_g.v[4 + i];
   }
-  st->mark(2);
+  g0.mag[4] = 0;
+  g1.mag[4] = 0;
+  recode_row<GBITS, GWIN, gdig_t>(g0, S.gdig[0]);
+  recode_row<GBITS, GWIN, gdig_t>(g1, S.gdig[1]);
+}
+
+// Q = u_r * P + u_g * G for this workgroup's signature (core.cuh ecmult_core, quad form); the
+// digits come from wave 1 (recode_digits), the barrier below is where wave 0 picks them up.
+template <class ST>
+DEV void ecmult_wave(gejr& acc, bool& inf, const ger& P, const uint32_t* gtab, LatLds& S, const fr& beta, ST* st) {
   // table {1..PTAB} * P on one global Z (co-Z additions, backward rescale; core.cuh)
   fr zeta;
   {
@@ -225,14 +229,16 @@ DEV void ecmult_wave(gejr& acc, bool& inf, const ger& P, const sc& u_r, const sc
     zeta = rho;  // rho_0 = Z_PTAB / Z_1 with Z_1 = 1
   }
   st->mark(3);
+  __syncthreads();  // wave 1's digits
+  st->mark(1);
   strauss_wave<false>(acc, inf, S, gtab, zeta, beta);
   if (__any(!inf && fr_is_zero(acc.z))) strauss_wave<true>(acc, inf, S, gtab, zeta, beta);
   acc.z = fr_mul(acc.z, zeta);
   st->mark(4);
 }
 
-// Phase marks (diagnostic build only): 0 parse + lift, 1 r^-1 + u1/u2, 2 GLV + digits,
-// 3 table, 4 Strauss, 5 Z^-1 + affine, 6 Keccak + stores.
+// Phase marks of wave 0 (diagnostic build only): 0 parse + lift, 3 table, 1 wait for wave 1's
+// r^-1 / u1 / u2 / digits, 4 Strauss, 5 Z^-1 + affine, 6 Keccak + stores.
 template <class ST>
 DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   __shared__ LatLds S;
@@ -266,28 +272,34 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
       c >>= 32;
     }
   }
+  const bool wave1 = threadIdx.x >= 64;
+  if (wave1) {
+    // --- u1 = -z / r, u2 = s / r (main_impl.h:114-117), digits into LDS. A signature whose R
+    // fails to lift is recovered from G instead (wave 0); its scalars stay well-defined either way.
+    R = sc_select(ok, R, sc_one());
+    const sc rinv = sc_inv_var(R);  // wave-uniform data: variable-time safegcd
+    const sc u1 = sc_neg(sc_mul(rinv, Z));
+    const sc u2 = sc_select(ok, sc_mul(rinv, Sv), sc_one());
+    recode_digits(u2, u1, S);
+    __syncthreads();  // digits ready
+    return;
+  }
   ger Rp;
   ok = ger_set_xo(Rp, fe_to_fr(fe_from_u256(xr)), (recid & 1u) != 0) && ok;
-  // failed signatures carry the generator and r = 1, so every later step stays well-defined
+  // failed signatures carry the generator, so every later step stays well-defined
   const ge G = gen_point();
   Rp.x = fr_select(ok, Rp.x, fe_to_fr(G.x));
   Rp.y = fr_select(ok, Rp.y, fe_to_fr(G.y));
-  R = sc_select(ok, R, sc_one());
   st->mark(0);
-  // --- u1 = -z / r, u2 = s / r (main_impl.h:114-117)
-  const sc rinv = sc_inv(R);
-  const sc u1 = sc_neg(sc_mul(rinv, Z));
-  const sc u2 = sc_select(ok, sc_mul(rinv, Sv), sc_one());
-  st->mark(1);
   // --- Q = u2 R + u1 G
   const fr beta = fe_to_fr(fe_const(FE_BETA));
   gejr Q;
   bool qinf;
-  ecmult_wave(Q, qinf, Rp, u2, u1, prm.gtab, S, beta, st);
+  ecmult_wave(Q, qinf, Rp, prm.gtab, S, beta, st);
   ok = ok && !qinf;  // main_impl.h:120
   // --- affine, serialize, address
   const fr zq = fr_select(ok, Q.z, fr_one());
-  const fr zi = fe_to_fr(fe_inv(fr_to_fe(zq)));
+  const fr zi = fe_to_fr(fe_inv_var(fr_to_fe(zq)));
   fr zi2, zi3;
   zi2 = fr_sqr(zi);
   fr X1, Y1;
