@@ -6,11 +6,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -58,6 +60,19 @@ int env_int(const char* name, int dflt) {
     if (e_ != hipSuccess) return set_err(EGES_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
+// A small-call lane: its own stream, device scratch and pinned staging, so that concurrent
+// single-chunk host calls that run on the latency kernel (which needs no shared workspace) do
+// not queue behind each other on the device mutex.
+constexpr int NLANES = 4;
+struct Lane {
+  std::mutex mu;
+  hipStream_t stream = nullptr;
+  uint8_t* buf = nullptr;
+  size_t buf_cap = 0;
+  uint8_t* pin = nullptr;
+  hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_k[2] = {nullptr, nullptr};
+};
+
 struct Dev {
   int id = -1;
   int cus = 0;
@@ -77,6 +92,7 @@ struct Dev {
   uint32_t* ws2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::mutex mu;
+  Lane lanes[NLANES];
   ~Dev();
 };
 using DevPtr = std::shared_ptr<Dev>;
@@ -123,20 +139,21 @@ struct DevGuard {  // restores the caller's current device
   }
 };
 
-int dev_ensure_buf(Dev& d, size_t bytes) {
-  if (bytes <= d.buf_cap) return EGES_SUCCESS;
-  if (d.buf) {
-    HIPCHK(hipStreamSynchronize(d.stream));
-    HIPCHK(hipEventSynchronize(d.last));
-    HIPCHK(hipFree(d.buf));
-    d.buf = nullptr;
-    d.buf_cap = 0;
+int ensure_buf(uint8_t*& buf, size_t& cap_io, hipStream_t st, hipEvent_t last, size_t bytes, size_t min_cap) {
+  if (bytes <= cap_io) return EGES_SUCCESS;
+  if (buf) {
+    HIPCHK(hipStreamSynchronize(st));
+    if (last) HIPCHK(hipEventSynchronize(last));
+    HIPCHK(hipFree(buf));
+    buf = nullptr;
+    cap_io = 0;
   }
-  size_t cap = std::max(bytes, size_t(64) << 20);
-  if (hipMalloc(&d.buf, cap) != hipSuccess) return set_err(EGES_E_NOMEM, "hipMalloc(%zu) failed", cap);
-  d.buf_cap = cap;
+  size_t cap = std::max(bytes, min_cap);
+  if (hipMalloc(&buf, cap) != hipSuccess) return set_err(EGES_E_NOMEM, "hipMalloc(%zu) failed", cap);
+  cap_io = cap;
   return EGES_SUCCESS;
 }
+int dev_ensure_buf(Dev& d, size_t bytes) { return ensure_buf(d.buf, d.buf_cap, d.stream, d.last, bytes, size_t(64) << 20); }
 
 int init_device(int id, DevPtr* out) {
   hipDeviceProp_t prop;
@@ -147,6 +164,15 @@ int init_device(int id, DevPtr* out) {
   DevPtr d = std::make_shared<Dev>();
   d->id = id;
   d->cus = prop.multiProcessorCount;
+  // the small-call lanes' streams first: HIP hands out its hardware queues (GPU_MAX_HW_QUEUES,
+  // 4 by default) round-robin in stream-creation order, and lanes sharing a queue serialise
+  for (Lane& l : d->lanes) {
+    HIPCHK(hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking));
+    for (int r = 0; r < 2; ++r) {
+      HIPCHK(hipEventCreateWithFlags(&l.ev_in[r], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&l.ev_k[r], hipEventDisableTiming));
+    }
+  }
   HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&d->last, hipEventDisableTiming));
   HIPCHK(hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking));
@@ -197,6 +223,16 @@ Dev::~Dev() {
     (void)hipEventDestroy(ev_fork);
     (void)hipEventDestroy(ev_join);
     (void)hipFree(ws2);
+  }
+  for (Lane& l : lanes) {
+    if (l.stream) (void)hipStreamSynchronize(l.stream);
+    if (l.buf) (void)hipFree(l.buf);
+    if (l.pin) (void)hipHostFree(l.pin);
+    for (int r = 0; r < 2; ++r) {
+      if (l.ev_in[r]) (void)hipEventDestroy(l.ev_in[r]);
+      if (l.ev_k[r]) (void)hipEventDestroy(l.ev_k[r]);
+    }
+    if (l.stream) (void)hipStreamDestroy(l.stream);
   }
   if (stream) (void)hipStreamDestroy(stream);
 }
@@ -456,7 +492,6 @@ Region region_for(const HostJob& j, size_t base, size_t m) {
 // i-1's outputs (host order H2D(i+1), K(i+1), D2H(i): the pageable D2H blocks this thread
 // until K(i) is done, by which time K(i+1) is queued behind it). Synchronous overall.
 int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
-  std::lock_guard<std::mutex> lk(d.mu);
   DevGuard g(d.id);
   // a shard big enough to pipeline runs as >= 2 chunks (each still a full resident grid)
   size_t c = std::min(CHUNK, cnt);
@@ -464,17 +499,46 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
   size_t worst = 0;  // region size: SENDER_RAW depends on the bytes of each chunk
   for (size_t base = off; base < off + cnt; base += c) worst = std::max(worst, region_for(j, base, std::min(c, off + cnt - base)).total);
   const int nreg = cnt > c ? 2 : 1;
-  int rc = dev_ensure_buf(d, worst * nreg);
+  const bool pinned = nreg == 1 && worst <= PIN_BYTES;
+  // Small calls on the latency kernel (no shared workspace) run on one of the device's lanes,
+  // concurrently with each other; everything else on the device's main resources, in order.
+  const bool small = pinned && cnt <= lat_max() && j.kind != HostJob::VERIFY;
+  Lane* lane = nullptr;
+  std::unique_lock<std::mutex> lk;
+  if (small) {
+    for (Lane& l : d.lanes) {
+      std::unique_lock<std::mutex> t(l.mu, std::try_to_lock);
+      if (t.owns_lock()) {
+        lane = &l;
+        lk = std::move(t);
+        break;
+      }
+    }
+    if (!lane) {
+      static std::atomic<unsigned> rr{0};
+      lane = &d.lanes[rr++ % NLANES];
+      lk = std::unique_lock<std::mutex>(lane->mu);
+    }
+  } else {
+    lk = std::unique_lock<std::mutex>(d.mu);
+  }
+  uint8_t*& dbuf = small ? lane->buf : d.buf;
+  uint8_t*& pin = small ? lane->pin : d.pin;
+  hipEvent_t* ev_in = small ? lane->ev_in : d.ev_in;
+  hipEvent_t* ev_k = small ? lane->ev_k : d.ev_k;
+  int rc = small ? ensure_buf(lane->buf, lane->buf_cap, lane->stream, nullptr, worst, size_t(4) << 20)
+                 : dev_ensure_buf(d, worst * nreg);
   if (rc) return rc;
   // a single chunk has nothing to overlap: one stream, no cross-stream waits (C3 latency)
-  hipStream_t st = d.stream, sx = nreg > 1 ? d.copy : d.stream;
-  const bool pinned = nreg == 1 && worst <= PIN_BYTES;
-  if (pinned && !d.pin && hipHostMalloc(&d.pin, PIN_BYTES, hipHostMallocDefault) != hipSuccess) {
-    d.pin = nullptr;
+  hipStream_t st = small ? lane->stream : d.stream, sx = nreg > 1 ? d.copy : st;
+  if (pinned && !pin && hipHostMalloc(&pin, PIN_BYTES, hipHostMallocDefault) != hipSuccess) {
+    pin = nullptr;
     return set_err(EGES_E_NOMEM, "hipHostMalloc(%zu) failed", PIN_BYTES);
   }
-  HIPCHK(hipStreamWaitEvent(st, d.last, 0));
-  HIPCHK(hipStreamWaitEvent(sx, d.last, 0));
+  if (!small) {
+    HIPCHK(hipStreamWaitEvent(st, d.last, 0));
+    HIPCHK(hipStreamWaitEvent(sx, d.last, 0));
+  }
   // Input staging: each input array goes to its offset in the region, either by its own
   // (pageable) copy into device memory on the copy stream, or, for a pinned call, packed into
   // the pinned buffer at the same offset, where the kernels read it directly (zero-copy: no
@@ -512,10 +576,10 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
     uint8_t* o_pub = q.B + q.g.o_out;
     uint8_t* o_addr = o_pub + q.m * 65;
     uint8_t* o_st = o_addr + q.m * 32;
-    HIPCHK(hipStreamWaitEvent(sx, d.ev_k[q.r], 0));
+    HIPCHK(hipStreamWaitEvent(sx, ev_k[q.r], 0));
     if (pinned) {  // outputs are already in the pinned buffer; the signing hashes are not
       if (j.kind == HostJob::SENDER_RAW && j.sighash)
-        HIPCHK(hipMemcpyAsync(d.pin + sighash_off(q), q.B + sighash_off(q), q.m * 32, hipMemcpyDeviceToHost, sx));
+        HIPCHK(hipMemcpyAsync(pin + sighash_off(q), q.B + sighash_off(q), q.m * 32, hipMemcpyDeviceToHost, sx));
       return EGES_SUCCESS;
     }
     if (j.pub) HIPCHK(hipMemcpyAsync(j.pub + q.base * 65, o_pub, q.m * 65, hipMemcpyDeviceToHost, sx));
@@ -526,13 +590,13 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
     return EGES_SUCCESS;
   };
   auto unpack = [&](const Pending& q) {  // pinned mode, after the sync
-    const uint8_t* o_pub = d.pin + q.g.o_out;
+    const uint8_t* o_pub = pin + q.g.o_out;
     const uint8_t* o_addr = o_pub + q.m * 65;
     const uint8_t* o_st = o_addr + q.m * 32;
     if (j.pub) std::memcpy(j.pub + q.base * 65, o_pub, q.m * 65);
     if (j.addr) std::memcpy(j.addr + q.base * astride, o_addr, q.m * astride);
     if (j.status) std::memcpy(j.status + q.base, o_st, q.m);
-    if (j.kind == HostJob::SENDER_RAW && j.sighash) std::memcpy(j.sighash + q.base * 32, d.pin + sighash_off(q), q.m * 32);
+    if (j.kind == HostJob::SENDER_RAW && j.sighash) std::memcpy(j.sighash + q.base * 32, pin + sighash_off(q), q.m * 32);
   };
   Pending prev{};
   bool have_prev = false;
@@ -542,9 +606,9 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
     const size_t m_pad = align_up(m, 64);
     const int r = ci % nreg;
     const Region rg = region_for(j, base, m);
-    uint8_t* B = d.buf + (size_t)r * worst;
-    uint8_t* I = pinned ? d.pin : B;  // where the kernels read the inputs
-    uint8_t* o_pub = (pinned ? d.pin : B) + rg.o_out;
+    uint8_t* B = dbuf + (size_t)r * worst;
+    uint8_t* I = pinned ? pin : B;  // where the kernels read the inputs
+    uint8_t* o_pub = (pinned ? pin : B) + rg.o_out;
     uint8_t* o_addr = o_pub + m * 65;
     uint8_t* o_st = o_addr + m * 32;
     uint32_t* rec = reinterpret_cast<uint32_t*>(B + rg.o_rec);
@@ -555,8 +619,8 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       H2D(B, dm, j.a + base * 32, m * 32);
       H2D(B, ds, j.b + base * 65, m * 65);
       FLUSH_IN(B);
-      HIPCHK(hipEventRecord(d.ev_in[r], sx));
-      HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
+      HIPCHK(hipEventRecord(ev_in[r], sx));
+      HIPCHK(hipStreamWaitEvent(st, ev_in[r], 0));
       HIPCHK(launch_prep_ecrecover(dm, ds, (uint32_t)m, (uint32_t)m_pad, rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, j.addr ? o_addr : nullptr, j.pub ? o_pub : nullptr,
                       d.gtab, d.ws};
@@ -573,8 +637,8 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       H2D(B, dv, j.d + base * 32, m * 32);
       if (j.e) H2D(B, df, j.e + base, m);
       FLUSH_IN(B);
-      HIPCHK(hipEventRecord(d.ev_in[r], sx));
-      HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
+      HIPCHK(hipEventRecord(ev_in[r], sx));
+      HIPCHK(hipStreamWaitEvent(st, ev_in[r], 0));
       HIPCHK(launch_prep_sender(dh, dr, dsv, dv, j.e ? df : nullptr, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id,
                                 rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
@@ -585,8 +649,8 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       H2D(B, din, j.a + base * 128, m * 128);
       if (j.inlen) H2D(B, reinterpret_cast<uint8_t*>(dlen), j.inlen + base, m * 4);
       FLUSH_IN(B);
-      HIPCHK(hipEventRecord(d.ev_in[r], sx));
-      HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
+      HIPCHK(hipEventRecord(ev_in[r], sx));
+      HIPCHK(hipStreamWaitEvent(st, ev_in[r], 0));
       if (pinned) std::memset(o_addr, 0, m * 32);
       else HIPCHK(hipMemsetAsync(o_addr, 0, m * 32, st));
       HIPCHK(launch_prep_precompile(din, j.inlen ? dlen : nullptr, (uint32_t)m, (uint32_t)m_pad, rec, st));
@@ -603,8 +667,8 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       if (rg.raw_len) H2D(B, draw, j.a + rg.raw_lo, rg.raw_len);
       H2D(B, reinterpret_cast<uint8_t*>(doff), j.offsets + base, 8 * (m + 1));
       FLUSH_IN(B);
-      HIPCHK(hipEventRecord(d.ev_in[r], sx));
-      HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
+      HIPCHK(hipEventRecord(ev_in[r], sx));
+      HIPCHK(hipStreamWaitEvent(st, ev_in[r], 0));
       HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, vf, st));
       HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
@@ -619,13 +683,13 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       H2D(B, dm, j.c + base * 32, m * 32);
       H2D(B, ds, j.d + base * 64, m * 64);
       FLUSH_IN(B);
-      HIPCHK(hipEventRecord(d.ev_in[r], sx));
-      HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
+      HIPCHK(hipEventRecord(ev_in[r], sx));
+      HIPCHK(hipStreamWaitEvent(st, ev_in[r], 0));
       VerifyParams p{dp, dl, dm, ds, (uint32_t)m, o_st, d.gtab, d.ws};
       verify_scratch_bind(p, B + rg.o_rec, m_pad);
       HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
     }
-    HIPCHK(hipEventRecord(d.ev_k[r], st));
+    HIPCHK(hipEventRecord(ev_k[r], st));
     // --- the previous chunk's outputs, while this chunk computes
     if (have_prev) {
       rc = outputs(prev);
@@ -638,7 +702,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
     rc = outputs(prev);
     if (rc) return rc;
   }
-  HIPCHK(hipEventRecord(d.last, sx));
+  if (!small) HIPCHK(hipEventRecord(d.last, sx));
   HIPCHK(hipStreamSynchronize(sx));
   if (pinned && have_prev) unpack(prev);
   return EGES_SUCCESS;
@@ -713,6 +777,92 @@ void keccakf_host(uint64_t st[25]) {
     st[0] ^= RC[round];
   }
 }
+
+// ------------------------------------------------------------------ single-item coalescing
+// The reference's single-item calls (secp256k1_ext_ecdsa_recover / _verify, ext.h:30-75) run on
+// one shared read-only context from any goroutine (secp256.go:45-52). Here concurrent single-item
+// callers are coalesced ("group commit"): a caller enqueues its request; if no batch is in
+// flight it becomes the leader, takes every queued request (its own included) and runs them as
+// one batch (the latency kernel for small batches); the others wait on a condition variable and
+// are served by that batch or the next one. Nothing is serialised per request.
+struct RecoverReq {
+  const uint8_t* msg;
+  const uint8_t* sig;
+  uint8_t* pub;
+  int result = 0;
+  bool done = false;
+};
+struct VerifyReq {
+  const uint8_t* sig;
+  const uint8_t* msg;
+  const uint8_t* pub;
+  uint8_t publen;
+  int result = 0;
+  bool done = false;
+};
+
+void run_group(std::vector<RecoverReq*>& g) {
+  const size_t n = g.size();
+  std::vector<uint8_t> msg(n * 32), sig(n * 65), pub(n * 65), st(n);
+  for (size_t i = 0; i < n; ++i) {
+    std::memcpy(&msg[i * 32], g[i]->msg, 32);
+    std::memcpy(&sig[i * 65], g[i]->sig, 65);
+  }
+  const int rc = eges_ecrecover_batch(msg.data(), sig.data(), n, pub.data(), nullptr, st.data());
+  for (size_t i = 0; i < n; ++i) {
+    const bool ok = rc == EGES_SUCCESS && st[i] == EGES_OK;
+    if (ok) std::memcpy(g[i]->pub, &pub[i * 65], 65);
+    g[i]->result = ok ? 1 : 0;
+  }
+}
+void run_group(std::vector<VerifyReq*>& g) {
+  const size_t n = g.size();
+  std::vector<uint8_t> pub(n * 65, 0), publen(n), msg(n * 32), sig(n * 64), ok(n);
+  for (size_t i = 0; i < n; ++i) {
+    std::memcpy(&pub[i * 65], g[i]->pub, g[i]->publen);
+    publen[i] = g[i]->publen;
+    std::memcpy(&msg[i * 32], g[i]->msg, 32);
+    std::memcpy(&sig[i * 64], g[i]->sig, 64);
+  }
+  const int rc = eges_verify_batch(pub.data(), publen.data(), msg.data(), sig.data(), n, ok.data());
+  for (size_t i = 0; i < n; ++i) g[i]->result = (rc == EGES_SUCCESS && ok[i]) ? 1 : 0;
+}
+
+// Up to NLANES groups are in flight at once (one per small-call lane of the device), so a
+// caller that arrives while a group runs does not wait for it to finish before its own starts.
+template <class Req>
+struct Coalescer {
+  static constexpr size_t MAX_GROUP = 4096;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<Req*> queue;
+  int inflight = 0;
+
+  void submit(Req* r) {
+    std::unique_lock<std::mutex> lk(mu);
+    queue.push_back(r);
+    while (!r->done) {
+      const bool mine_queued = std::find(queue.begin(), queue.end(), r) != queue.end();
+      if (mine_queued && inflight < NLANES) {
+        ++inflight;
+        std::vector<Req*> g;
+        const size_t take = std::min(queue.size(), MAX_GROUP);
+        g.assign(queue.begin(), queue.begin() + take);
+        queue.erase(queue.begin(), queue.begin() + take);
+        lk.unlock();
+        run_group(g);
+        lk.lock();
+        for (Req* q : g) q->done = true;
+        --inflight;
+        cv.notify_all();
+      } else {
+        cv.wait(lk);
+      }
+    }
+  }
+};
+Coalescer<RecoverReq> g_recover_co;
+Coalescer<VerifyReq> g_verify_co;
 
 }  // namespace
 
@@ -854,24 +1004,18 @@ int eges_verify_batch(const uint8_t* pub, const uint8_t* publen, const uint8_t* 
 
 int eges_ecdsa_recover(unsigned char* pubkey_out65, const unsigned char* sigdata65, const unsigned char* msgdata32) {
   if (!pubkey_out65 || !sigdata65 || !msgdata32) return 0;
-  uint8_t st = EGES_RECOVER_FAILED;
-  uint8_t pub[65];
-  if (eges_ecrecover_batch(msgdata32, sigdata65, 1, pub, nullptr, &st) != EGES_SUCCESS) return 0;
-  if (st != EGES_OK) return 0;
-  std::memcpy(pubkey_out65, pub, 65);
-  return 1;
+  RecoverReq r{msgdata32, sigdata65, pubkey_out65};
+  g_recover_co.submit(&r);
+  return r.result;
 }
 
 int eges_ecdsa_verify(const unsigned char* sigdata64, const unsigned char* msgdata32, const unsigned char* pubkeydata,
                       size_t pubkeylen) {
   if (!sigdata64 || !msgdata32 || !pubkeydata) return 0;
   if (pubkeylen != 33 && pubkeylen != 65) return 0;  // eckey_pubkey_parse accepts only these sizes
-  uint8_t pub[65] = {0};
-  std::memcpy(pub, pubkeydata, pubkeylen);
-  const uint8_t len = (uint8_t)pubkeylen;
-  uint8_t ok = 0;
-  if (eges_verify_batch(pub, &len, msgdata32, sigdata64, 1, &ok) != EGES_SUCCESS) return 0;
-  return ok ? 1 : 0;
+  VerifyReq r{sigdata64, msgdata32, pubkeydata, (uint8_t)pubkeylen};
+  g_verify_co.submit(&r);
+  return r.result;
 }
 
 int eges_ecrecover_batch_dev(int device, const uint8_t* msg, const uint8_t* sig, size_t n, uint8_t* pub_out,

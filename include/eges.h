@@ -15,7 +15,8 @@
  *     meaning the HIP null stream) and are asynchronous on that stream.
  *   - n == 0 is valid and a no-op. A NULL pointer where n > 0 needs it returns
  *     EGES_E_NULLPTR (never crashes).
- *   - Thread-safe: concurrent callers are serialised per device.
+ *   - Thread-safe. Concurrent single-item callers are coalesced into shared batches (group
+ *     commit); batch calls from several threads run one after another on a device.
  *   - There is no CPU fallback: without a usable gfx950 device every compute entry fails
  *     with EGES_E_NODEVICE.
  */

@@ -57,3 +57,53 @@ def test_concurrent_batch_and_single_item_callers(engine):
         th.join(timeout=100)
     assert not any(th.is_alive() for th in threads), "a caller thread did not return"
     assert not errors, errors[:10]
+
+
+def test_coalesced_single_item_callers(engine):
+    """8 threads x 2000 single eges_ecdsa_recover calls (the reference's per-goroutine
+    secp256k1_ext_ecdsa_recover, ext.h:30-47): coalesced into shared batches (capi.hip
+    Coalescer), every result bit-exact against the golden fixture. Rates printed for the record."""
+    import time
+    from eges_amd._lib import lib
+    g = load_golden("recover.npz")
+    msg, sig, exp_pub, exp_st = g["msg"], g["sig"], g["pub"], g["status"]
+    idx = [i for i in range(msg.shape[0]) if sig[i, 64] < 4]  # checkSignature filters recid >= 4 in Go
+    per_thread, nthreads = 2000, 8
+    errors = []
+    lat = []
+
+    def worker(t):
+        out = (ctypes.c_ubyte * 65)()
+        try:
+            for k in range(per_thread):
+                i = idx[(t * 7919 + k * 31) % len(idx)]
+                t0 = time.perf_counter()
+                rc = lib.eges_ecdsa_recover(out, sig[i].tobytes(), msg[i].tobytes())
+                if t == 0:
+                    lat.append(time.perf_counter() - t0)
+                want = 1 if exp_st[i] == 0 else 0
+                if rc != want or (rc == 1 and bytes(out) != exp_pub[i].tobytes()):
+                    errors.append((t, k, i, rc))
+        except Exception as e:
+            errors.append(("exc", t, repr(e)))
+
+    # single caller first (p50 latency of one call), then 8 concurrent callers
+    one = (ctypes.c_ubyte * 65)()
+    ts = []
+    for k in range(200):
+        i = idx[k % len(idx)]
+        t0 = time.perf_counter()
+        lib.eges_ecdsa_recover(one, sig[i].tobytes(), msg[i].tobytes())
+        ts.append(time.perf_counter() - t0)
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(nthreads)]
+    t0 = time.perf_counter()
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=200)
+    dt = time.perf_counter() - t0
+    assert not any(th.is_alive() for th in threads), "a caller thread did not return"
+    assert not errors, errors[:10]
+    print(f"\nsingle eges_ecdsa_recover p50 {np.median(ts[20:]) * 1e3:.3f} ms (one caller); "
+          f"{nthreads} callers x {per_thread}: {nthreads * per_thread / dt:.0f} recoveries/s, "
+          f"p50 {np.median(lat) * 1e3:.3f} ms per call")
