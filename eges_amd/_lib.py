@@ -31,6 +31,10 @@ SIGNER_FRONTIER = 0
 SIGNER_HOMESTEAD = 1
 SIGNER_EIP155 = 2
 
+LIST_FAKE = 1
+LIST_GEEC = 2
+LIST_TXS = 4
+
 VF_V_WIDE = 1
 VF_R_WIDE = 2
 VF_S_WIDE = 4
@@ -53,6 +57,7 @@ SIGNATURES = {
     "eges_sender_batch": (_I, [_P, _P, _P, _P, _P, _SZ, _I, _U64, _P, _P]),
     "eges_sender_raw_batch": (_I, [_P, _P, _SZ, _I, _U64, _P, _P, _P]),
     "eges_ecrecover_precompile_batch": (_I, [_P, _P, _SZ, _P, _P]),
+    "eges_block_senders_raw": (_I, [_P, _SZ, _U32, _I, _U64, _SZ, _P, _P, _P, _P]),
     "eges_verify_batch": (_I, [_P, _P, _P, _P, _SZ, _P]),
     "eges_ecrecover_batch_dev": (_I, [_I, _P, _P, _SZ, _P, _P, _P, _P]),
     "eges_sender_batch_dev": (_I, [_I, _P, _P, _P, _P, _P, _SZ, _I, _U64, _P, _P, _P]),

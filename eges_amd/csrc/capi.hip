@@ -742,6 +742,76 @@ int run_host(const HostJob& j, size_t n) {
   return EGES_SUCCESS;
 }
 
+// ------------------------------------------------------------------ Geec block (extblock) split
+// RLP item header at b[p] inside [p, end) (rlp/decode.go readKind :937-990 and the Kind bound
+// checks :874-907): kind 0 = byte, 1 = string, 2 = list; hl = header length, sz = payload size.
+bool rlp_head(const uint8_t* b, size_t p, size_t end, int& kind, size_t& hl, size_t& sz) {
+  if (p >= end) return false;  // EOL / EOF
+  const uint8_t x = b[p];
+  if (x < 0x80) {
+    kind = 0;
+    hl = 1;
+    sz = 0;
+    return true;
+  }
+  size_t ll = 0;
+  if (x < 0xB8) {
+    kind = 1;
+    sz = x - 0x80u;
+  } else if (x < 0xC0) {
+    kind = 1;
+    ll = x - 0xB7u;
+  } else if (x < 0xF8) {
+    kind = 2;
+    sz = x - 0xC0u;
+  } else {
+    kind = 2;
+    ll = x - 0xF7u;
+  }
+  hl = 1 + ll;
+  if (ll) {  // readUint: big-endian length, no leading zero byte, and >= 56 (ErrCanonSize)
+    if (p + 1 + ll > end || b[p + 1] == 0) return false;
+    sz = 0;
+    for (size_t k = 0; k < ll; ++k) sz = (sz << 8) | b[p + 1 + k];
+    if (sz < 56) return false;
+  }
+  return sz <= end - p - hl;  // ErrElemTooLarge / ErrValueTooLarge
+}
+
+// The extblock list (core/types/block.go:188-195: Header, FakeTxs, GeecTxs, Txs, Uncles,
+// Confirm rlp:"nil") of a whole block as rlp.DecodeBytes sees its structure: exactly six
+// elements, the first five lists, the last empty or a list, no trailing bytes. Fills, for
+// the three transaction lists, the item offsets (absolute in b; n_k + 1 each). Header, uncle
+// and confirm-message field contents are not decoded (not on the signature path).
+bool split_extblock(const uint8_t* b, size_t len, std::vector<uint64_t> offs[3]) {
+  int kind;
+  size_t hl, sz;
+  if (!rlp_head(b, 0, len, kind, hl, sz) || kind != 2 || hl + sz != len) return false;
+  size_t p = hl;
+  const size_t end = len;
+  for (int e = 0; e < 6; ++e) {
+    if (!rlp_head(b, p, end, kind, hl, sz)) return false;
+    if (e < 5 && kind != 2) return false;                      // Header, tx lists, Uncles: lists
+    if (e == 5 && !(kind == 2 || (kind == 1 && sz == 0))) return false;  // *ConfirmBlockMsg, rlp:"nil"
+    if (e >= 1 && e <= 3) {                                     // FakeTxs, GeecTxs, Txs
+      std::vector<uint64_t>& o = offs[e - 1];
+      o.clear();
+      size_t q = p + hl;
+      const size_t le = p + hl + sz;
+      o.push_back(q);
+      while (q < le) {
+        int k2;
+        size_t h2, s2;
+        if (!rlp_head(b, q, le, k2, h2, s2)) return false;
+        q += h2 + s2;
+        o.push_back(q);
+      }
+    }
+    p += hl + sz;
+  }
+  return p == end;  // "input list has too many elements"
+}
+
 // ------------------------------------------------------------------ host Keccak-256
 const uint64_t RC[24] = {0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808AULL, 0x8000000080008000ULL,
                          0x000000000000808BULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
@@ -973,6 +1043,39 @@ int eges_sender_raw_batch(const uint8_t* raw, const uint64_t* offsets, size_t n,
   j.status = status;
   j.sighash = sighash_out;
   return run_host(j, n);
+}
+
+int eges_block_senders_raw(const uint8_t* block, size_t len, uint32_t lists, int signer, uint64_t chain_id,
+                           size_t cap, uint8_t* addr_out, uint8_t* status, uint32_t* counts, int* block_status) {
+  if (!block || !counts || !block_status) return set_err(EGES_E_NULLPTR, "NULL argument");
+  if (signer < 0 || signer > 2) return set_err(EGES_E_INVALID_ARG, "bad signer %d", signer);
+  std::vector<uint64_t> offs[3];
+  counts[0] = counts[1] = counts[2] = 0;
+  if (!split_extblock(block, len, offs)) {
+    *block_status = EGES_DECODE_FAILED;
+    return EGES_SUCCESS;
+  }
+  size_t total = 0;
+  for (int k = 0; k < 3; ++k) {
+    counts[k] = (uint32_t)(offs[k].size() - 1);
+    if (lists & (1u << k)) total += counts[k];
+  }
+  if (total > cap) return set_err(EGES_E_INVALID_ARG, "block has %zu selected transactions, cap %zu", total, cap);
+  if (total && (!addr_out || !status)) return set_err(EGES_E_NULLPTR, "NULL output");
+  *block_status = EGES_OK;
+  size_t base = 0;
+  for (int k = 0; k < 3; ++k) {
+    if (!(lists & (1u << k)) || counts[k] == 0) continue;
+    const std::vector<uint64_t>& o = offs[k];
+    const int rc = eges_sender_raw_batch(block + o[0], o.data(), counts[k], signer, chain_id, addr_out + base * 20,
+                                         status + base, nullptr);
+    if (rc) return rc;
+    base += counts[k];
+  }
+  // rlp.DecodeBytes of the block fails on any undecodable transaction of the selected lists
+  for (size_t i = 0; i < total; ++i)
+    if (status[i] == EGES_DECODE_FAILED) *block_status = EGES_DECODE_FAILED;
+  return EGES_SUCCESS;
 }
 
 int eges_ecrecover_precompile_batch(const uint8_t* input, const uint32_t* inlen, size_t n, uint8_t* out32,

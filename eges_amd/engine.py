@@ -88,6 +88,24 @@ def sender_raw_batch(raws, signer, chain_id, want_sighash=False):
     return addr, status, sighash
 
 
+def block_senders_raw(block, lists=_lib.LIST_TXS, signer=_lib.SIGNER_EIP155, chain_id=None, cap=None):
+    """Senders of a whole Geec block (extblock RLP, core/types/block.go:188-195) through
+    eges_block_senders_raw -> (addr (m,20), status (m,), counts (3,), block_status) for the
+    selected lists (bits: 1 FakeTxs, 2 GeecTxs, 4 Txs), concatenated in list order."""
+    from .txs import GEEC_CHAIN_ID
+    chain_id = GEEC_CHAIN_ID if chain_id is None else chain_id
+    blk = np.frombuffer(bytes(block), np.uint8) if len(block) else np.zeros(1, np.uint8)
+    cap = cap if cap is not None else max(1, len(block) // 2)
+    addr = np.zeros((cap, 20), np.uint8)
+    status = np.zeros(cap, np.uint8)
+    counts = np.zeros(3, np.uint32)
+    bst = ctypes.c_int(-1)
+    check(lib.eges_block_senders_raw(_p(blk), len(block), int(lists), int(signer), int(chain_id), cap, _p(addr),
+                                     _p(status), _p(counts), ctypes.byref(bst)))
+    m = sum(int(counts[k]) for k in range(3) if lists & (1 << k))  # 0 when the structure fails
+    return addr[:m].copy(), status[:m].copy(), counts, bst.value
+
+
 def ecrecover_precompile_batch(inputs):
     """The EVM ECRECOVER precompile (core/vm/contracts.go:77-101) over a list of call inputs
     (bytes of any length) -> (out (n,32), status (n,)); item i returns out[i] when status[i] == 0

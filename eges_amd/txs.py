@@ -217,3 +217,27 @@ def sender_inputs(txs, chain_id):
             rows[1 + k][i] = np.frombuffer(b, np.uint8)
             vflags[i] |= flag if wide else 0
     return rows[0], rows[1], rows[2], rows[3], vflags
+
+
+# ------------------------------------------------------------------ Geec blocks (extblock)
+def geec_header(number=1, coinbase=b"\x11" * 20):
+    """A Geec header's RLP (core/types/block.go:70-90: the 15 go-ethereum fields plus Regs and
+    TrustRand). Its contents are not on the signature path; any well-formed list serves."""
+    return rlp_list([rlp_bytes(b"\x00" * 32), rlp_bytes(b"\x1d" * 32), rlp_bytes(coinbase), rlp_bytes(b"\x00" * 32),
+                     rlp_bytes(b"\x00" * 32), rlp_bytes(b"\x00" * 32), rlp_bytes(b"\x00" * 256), rlp_uint(1),
+                     rlp_uint(number), rlp_uint(8_000_000), rlp_uint(0), rlp_uint(1_560_000_000), rlp_bytes(b""),
+                     rlp_bytes(b"\x00" * 32), rlp_bytes(b"\x00" * 8), rlp_list([]), rlp_uint(7)])
+
+
+def fake_tx(coinbase=b"\x11" * 20, data_len=100, is_geec=False, data=None):
+    """types.NewTransaction(0, coinbase, 0, 0, 0, data) with V = R = S = 0: the placeholders the
+    Geec leader pads blocks with (consensus/geec/geec.go:333-339) and, with IsGeecTxn set, the
+    unsigned UDP payload transactions (consensus/geec/geec_api.go:33-35)."""
+    return encode_geec_tx(0, 0, 0, coinbase, 0, bytes(data_len) if data is None else data, is_geec, 0, 0, 0)
+
+
+def geec_extblock(fake, geec, txs, header=None, uncles=(), confirm=None):
+    """extblock RLP (core/types/block.go:188-195): [Header, FakeTxs, GeecTxs, Txs, Uncles,
+    Confirm]; confirm None encodes the nil pointer (0xC0, rlp/encode.go nil struct pointer)."""
+    return rlp_list([header or geec_header(), rlp_list(list(fake)), rlp_list(list(geec)), rlp_list(list(txs)),
+                     rlp_list(list(uncles)), confirm if confirm is not None else rlp_list([])])

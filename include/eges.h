@@ -125,6 +125,23 @@ int eges_sender_batch(const uint8_t *sighash, const uint8_t *r, const uint8_t *s
 int eges_sender_raw_batch(const uint8_t *raw, const uint64_t *offsets, size_t n, int signer, uint64_t chain_id,
                           uint8_t *addr_out, uint8_t *status, uint8_t *sighash_out);
 
+/* Senders of a whole Geec block: block is the RLP of one block as the
+ * wire and the chain carry it, the extblock list of core/types/block.go:188-195
+ * [Header, FakeTxs, GeecTxs, Txs, Uncles, Confirm]. The list structure is split as
+ * rlp.DecodeBytes(block, &b) (Block.DecodeRLP, block.go:273-282) walks it; every transaction of
+ * the lists selected by `lists` (bit 0 FakeTxs, bit 1 GeecTxs, bit 2 Txs) then goes through
+ * eges_sender_raw_batch's path (GPU decode, signing hash, recovery). counts[3] receives the
+ * item count of each list; addr_out / status (cap entries) receive the selected lists' results
+ * concatenated in list order. *block_status = EGES_OK, or EGES_DECODE_FAILED when the block
+ * structure (or a selected transaction) would make rlp.DecodeBytes fail; header, uncle and
+ * confirm-message field contents are not decoded. Returns EGES_E_INVALID_ARG when more than
+ * cap transactions are selected. */
+#define EGES_LIST_FAKE 0x1u
+#define EGES_LIST_GEEC 0x2u
+#define EGES_LIST_TXS 0x4u
+int eges_block_senders_raw(const uint8_t *block, size_t len, uint32_t lists, int signer, uint64_t chain_id,
+                           size_t cap, uint8_t *addr_out, uint8_t *status, uint32_t *counts, int *block_status);
+
 /* The EVM ECRECOVER precompile (core/vm/contracts.go:77-101, address 0x01) over a batch: input
  * n*128 (hash, v, r, s as 32-byte words); inlen n (nullable = all 128): bytes at or past
  * inlen[i] read as zero, which is the RightPadBytes of :82 (a longer input passes its first 128

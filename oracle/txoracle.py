@@ -19,6 +19,8 @@ Pure-Python restatement of what the reference does from raw transaction bytes to
   - the sender itself through the C oracle's Sender (oracle.c, pinned by oracle/_ref);
   - the EVM ECRECOVER precompile's Run (core/vm/contracts.go:77-101), pinned by the reference's
     own sample (contracts_test.go:390-395).
+  - the extblock list structure of a whole Geec block (core/types/block.go:188-195,273-282)
+    around it (split_extblock / block_senders).
 Pinned by: the reference's Vitalik EIP-155 vectors (transaction_signing_test.go:79-116) and the
 Homestead recipient vectors (transaction_test.go:82-127), re-encoded in the 10-field Geec form;
 the 9-field originals must fail to decode under the Geec struct.
@@ -267,6 +269,57 @@ def sender_raw(oracle, raw, signer, chain_id):
     flags = (1 if vw else 0) | (2 if rw else 0) | (4 if sw else 0)
     st, addr = oracle.sender(signer, chain_id, h, rb, sb, vb, flags)
     return st, (addr if st == 0 else bytes(20)), h
+
+
+def split_extblock(raw):
+    """Structure of rlp.DecodeBytes(raw, &block) (Block.DecodeRLP core/types/block.go:273-282 into
+    extblock :188-195): [Header, FakeTxs, GeecTxs, Txs, Uncles, Confirm rlp:"nil"] -> the raw
+    encodings of the three transaction lists' items, or DecodeError. Header / uncle / confirm
+    field contents are not decoded (not on the signature path)."""
+    s = _Stream(raw)
+    s.list_start()
+    lists = []
+    for e in range(6):
+        try:
+            k, size, _ = s.kind()
+        except DecodeError as err:
+            raise DecodeError("too few elements" if str(err) == "EOL" else str(err))
+        if e < 5 and k != "list":
+            raise DecodeError("ErrExpectedList")
+        if e == 5 and not (k == "list" or (k == "string" and size == 0)):
+            raise DecodeError("confirm: expected list or nil")
+        body = s.content(size) if k != "byte" else b""
+        if 1 <= e <= 3:
+            items = []
+            t = _Stream(body)
+            while t.pos < len(t.b):
+                start = t.pos
+                k2, size2, _ = t.kind()
+                if k2 != "byte":
+                    t.content(size2)
+                items.append(t.b[start:t.pos])
+            lists.append(items)
+    s.list_end()
+    if s.pos != len(s.b):
+        raise DecodeError("ErrMoreThanOneValue")
+    return lists
+
+
+def block_senders(oracle, raw, lists_mask, signer, chain_id):
+    """eges_block_senders_raw restated: (statuses, addrs, counts, block_status)."""
+    try:
+        lists = split_extblock(raw)
+    except DecodeError:
+        return [], [], [0, 0, 0], DECODE_FAILED
+    sts, addrs = [], []
+    for k in range(3):
+        if lists_mask & (1 << k):
+            for item in lists[k]:
+                st, addr, _ = sender_raw(oracle, item, signer, chain_id)
+                sts.append(st)
+                addrs.append(addr)
+    bst = DECODE_FAILED if DECODE_FAILED in sts else 0
+    return sts, addrs, [len(x) for x in lists], bst
 
 
 def precompile_ecrecover(oracle, inp):
