@@ -13,6 +13,26 @@ def _p(a):
     return ctypes.c_void_p(a.ctypes.data)
 
 
+# EGES_ORACLE_RECORD=<file>: append every call made through these wrappers (inputs and outputs)
+# to <file>, so that `make -C oracle sanitize` can replay the Python tests' exact calls in the
+# ASan/UBSan build (oracle/sanitize_main.c --replay). Record: u8 op, u8 nfields, then per field
+# u32 length + bytes; ints are 8-byte little-endian.
+_RECORD = os.environ.get("EGES_ORACLE_RECORD")
+OPS = dict(keccak256=1, sponge=2, recover_pubkey=3, recover_batch=4, verify=5, sender=6, pub_to_addr=7,
+           eref_ecrecover=8, eref_batch_mt=9)
+
+
+def _rec(op, *fields):
+    if not _RECORD:
+        return
+    out = bytearray([OPS[op], len(fields)])
+    for f in fields:
+        b = int(f).to_bytes(8, "little", signed=True) if isinstance(f, (int, np.integer)) else bytes(f)
+        out += len(b).to_bytes(4, "little") + b
+    with open(_RECORD, "ab") as fh:
+        fh.write(out)
+
+
 def have_ref():
     return os.path.exists(REF_SO)
 
@@ -40,12 +60,14 @@ class Oracle:
         a = np.frombuffer(bytes(data) or b"\0", np.uint8)
         out = np.zeros(32, np.uint8)
         self.L.oracle_keccak256(_p(a), len(data), _p(out))
+        _rec("keccak256", bytes(data), out)
         return out.tobytes()
 
     def sponge(self, data: bytes, outlen: int, rate: int, ds: int) -> bytes:
         a = np.frombuffer(bytes(data) or b"\0", np.uint8)
         out = np.zeros(outlen, np.uint8)
         self.L.oracle_sponge(_p(a), len(data), _p(out), outlen, rate, ds)
+        _rec("sponge", bytes(data), outlen, rate, ds, out)
         return out.tobytes()
 
     def recover_pubkey(self, msg: bytes, sig: bytes):
@@ -54,6 +76,7 @@ class Oracle:
         s = np.frombuffer(bytes(sig), np.uint8)
         pub = np.zeros(65, np.uint8)
         st = self.L.oracle_recover_pubkey(_p(pub), _p(s), _p(m))
+        _rec("recover_pubkey", m, s, st, pub)
         return st, pub.tobytes()
 
     def recover_batch(self, msg, sig):
@@ -64,24 +87,29 @@ class Oracle:
         addr = np.zeros((n, 20), np.uint8)
         st = np.zeros(n, np.uint8)
         self.L.oracle_recover_batch(n, _p(msg), _p(sig), _p(pub), _p(addr), _p(st))
+        _rec("recover_batch", n, msg, sig, pub, addr, st)
         return pub, addr, st
 
     def verify(self, pub: bytes, msg: bytes, sig: bytes) -> int:
         p = np.frombuffer(bytes(pub) or b"\0", np.uint8)
         m = np.frombuffer(bytes(msg) or b"\0", np.uint8)
         s = np.frombuffer(bytes(sig) or b"\0", np.uint8)
-        return self.L.oracle_verify_signature(_p(p), len(pub), _p(m), len(msg), _p(s), len(sig))
+        ok = self.L.oracle_verify_signature(_p(p), len(pub), _p(m), len(msg), _p(s), len(sig))
+        _rec("verify", bytes(pub), bytes(msg), bytes(sig), ok)
+        return ok
 
     def sender(self, signer, chain_id, sighash, r32, s32, v32, vflags):
         out = np.zeros(20, np.uint8)
         args = [np.frombuffer(bytes(x), np.uint8) for x in (sighash, r32, s32, v32)]
         st = self.L.oracle_sender(_p(out), int(signer), int(chain_id), *[_p(a) for a in args], int(vflags))
+        _rec("sender", int(signer), int(chain_id).to_bytes(8, "little"), *args, int(vflags), st, out)
         return st, out.tobytes()
 
     def pub_to_addr(self, pub65: bytes) -> bytes:
         p = np.frombuffer(bytes(pub65), np.uint8)
         out = np.zeros(20, np.uint8)
         self.L.oracle_pub_to_addr(_p(out), _p(p))
+        _rec("pub_to_addr", p, out)
         return out.tobytes()
 
 
@@ -105,6 +133,7 @@ class RefLib:
         s = np.frombuffer(bytes(sig), np.uint8)
         pub = np.zeros(65, np.uint8)
         r = self.L.eref_ecrecover(_p(pub), _p(s), _p(m))
+        _rec("eref_ecrecover", m, s, r, pub)
         return r, pub.tobytes()
 
     def ecrecover_batch_mt(self, msg, sig, nthreads):
@@ -115,4 +144,5 @@ class RefLib:
         addr = np.zeros((n, 20), np.uint8)
         ret = np.zeros(n, np.int8)
         self.L.eref_ecrecover_batch_mt(n, _p(msg), _p(sig), _p(pub), _p(addr), _p(ret), int(nthreads))
+        _rec("eref_batch_mt", n, msg, sig, int(nthreads), pub, addr, ret)
         return pub, addr, ret

@@ -6,6 +6,11 @@
  * entry point on signed, mutated and random inputs, with the two checked against each other
  * item for item. Any sanitizer report aborts the run (-fno-sanitize-recover); a mismatch
  * exits 1. Without the reference tree it exercises the oracle alone (-DNO_REF).
+ *
+ * `--replay FILE` re-executes, in this sanitized build, every call that tests/test_oracle.py and
+ * tests/test_txoracle.py made through oracle/pyoracle.py (recorded with EGES_ORACLE_RECORD, see
+ * there), each input in an exact-size heap buffer, and checks every output byte for byte
+ * against what the unsanitized libraries returned in the pytest run.
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -207,7 +212,122 @@ static void sender_cases(int n) {
     }
 }
 
+/* ---- replay of recorded Python-test calls */
+typedef struct {
+    unsigned char *p;
+    size_t n;
+} field;
+
+static long long fint(const field *f) {
+    long long v = 0;
+    memcpy(&v, f->p, f->n < 8 ? f->n : 8);
+    return v;
+}
+static unsigned char *dup(const field *f) { /* exact-size copy: any overread is reported */
+    unsigned char *q = malloc(f->n ? f->n : 1);
+    memcpy(q, f->p, f->n);
+    return q;
+}
+static void same(const unsigned char *got, const field *want, const char *what, long rec) {
+    CHECK(!memcmp(got, want->p, want->n), "replay record %ld: %s differs", rec, what);
+}
+
+static long replay(const char *path) {
+    FILE *fh = fopen(path, "rb");
+    if (!fh) { perror(path); exit(2); }
+    fseek(fh, 0, SEEK_END);
+    const long sz = ftell(fh);
+    fseek(fh, 0, SEEK_SET);
+    unsigned char *buf = malloc(sz ? (size_t)sz : 1);
+    if (fread(buf, 1, (size_t)sz, fh) != (size_t)sz) { perror("read"); exit(2); }
+    fclose(fh);
+    long rec = 0, pos = 0;
+    while (pos < sz) {
+        const int op = buf[pos], nf = buf[pos + 1];
+        pos += 2;
+        field f[16];
+        for (int i = 0; i < nf && i < 16; ++i) {
+            uint32_t len;
+            memcpy(&len, buf + pos, 4);
+            f[i].p = buf + pos + 4;
+            f[i].n = len;
+            pos += 4 + len;
+        }
+        unsigned char *a = NULL, *b = NULL, *c = NULL, *d = NULL, *o1 = NULL, *o2 = NULL, *o3 = NULL;
+        switch (op) {
+            case 1: /* keccak256: in -> out32 */
+                a = dup(&f[0]), o1 = malloc(32);
+                oracle_keccak256(a, f[0].n, o1);
+                same(o1, &f[1], "keccak256", rec);
+                break;
+            case 2: /* sponge: in, outlen, rate, ds -> out */
+                a = dup(&f[0]), o1 = malloc((size_t)fint(&f[1]) + 1);
+                oracle_sponge(a, f[0].n, o1, (size_t)fint(&f[1]), (int)fint(&f[2]), (unsigned char)fint(&f[3]));
+                same(o1, &f[4], "sponge", rec);
+                break;
+            case 3: /* recover_pubkey: msg, sig -> st, pub */
+                a = dup(&f[0]), b = dup(&f[1]), o1 = malloc(65);
+                CHECK(oracle_recover_pubkey(o1, b, a) == fint(&f[2]), "replay %ld: recover status", rec);
+                same(o1, &f[3], "recover pub", rec);
+                break;
+            case 4: { /* recover_batch: n, msg, sig -> pub, addr, st */
+                const size_t n = (size_t)fint(&f[0]);
+                a = dup(&f[1]), b = dup(&f[2]), o1 = malloc(65 * n + 1), o2 = malloc(20 * n + 1), o3 = malloc(n + 1);
+                oracle_recover_batch(n, a, b, o1, o2, o3);
+                same(o1, &f[3], "batch pub", rec), same(o2, &f[4], "batch addr", rec), same(o3, &f[5], "batch st", rec);
+                break;
+            }
+            case 5: /* verify: pub, msg, sig -> ok */
+                a = dup(&f[0]), b = dup(&f[1]), c = dup(&f[2]);
+                CHECK(oracle_verify_signature(a, f[0].n, b, f[1].n, c, f[2].n) == fint(&f[3]), "replay %ld: verify", rec);
+                break;
+            case 6: { /* sender: signer, chain, sighash, r, s, v, vflags -> st, addr */
+                u64 chain;
+                memcpy(&chain, f[1].p, 8);
+                a = dup(&f[2]), b = dup(&f[3]), c = dup(&f[4]), d = dup(&f[5]), o1 = malloc(20);
+                CHECK(oracle_sender(o1, (int)fint(&f[0]), chain, a, b, c, d, (int)fint(&f[6])) == fint(&f[7]),
+                      "replay %ld: sender status", rec);
+                same(o1, &f[8], "sender addr", rec);
+                break;
+            }
+            case 7: /* pub_to_addr */
+                a = dup(&f[0]), o1 = malloc(20);
+                oracle_pub_to_addr(o1, a);
+                same(o1, &f[1], "pub_to_addr", rec);
+                break;
+#ifndef NO_REF
+            case 8: /* eref_ecrecover: msg, sig -> r, pub */
+                a = dup(&f[0]), b = dup(&f[1]), o1 = calloc(65, 1);
+                CHECK(eref_ecrecover(o1, b, a) == fint(&f[2]), "replay %ld: eref rc", rec);
+                same(o1, &f[3], "eref pub", rec);
+                break;
+            case 9: { /* eref_batch_mt: n, msg, sig, nthreads -> pub, addr, ret */
+                const size_t n = (size_t)fint(&f[0]);
+                a = dup(&f[1]), b = dup(&f[2]), o1 = calloc(65 * n + 1, 1), o2 = calloc(20 * n + 1, 1), o3 = calloc(n + 1, 1);
+                eref_ecrecover_batch_mt(n, a, b, o1, o2, (signed char *)o3, (int)fint(&f[3]));
+                same(o1, &f[4], "eref batch pub", rec), same(o2, &f[5], "eref batch addr", rec);
+                same(o3, &f[6], "eref batch ret", rec);
+                break;
+            }
+#endif
+            default:
+                fprintf(stderr, "replay: unknown op %d (record %ld)\n", op, rec);
+                exit(2);
+        }
+        free(a), free(b), free(c), free(d), free(o1), free(o2), free(o3);
+        ++rec;
+    }
+    free(buf);
+    return rec;
+}
+
 int main(int argc, char **argv) {
+    if (argc > 2 && !strcmp(argv[1], "--replay")) {
+        const long recs = replay(argv[2]);
+        printf("sanitize_main --replay: %ld recorded test calls re-run, %ld checks, %ld mismatches\n", recs, g_checks,
+               g_fail);
+        return g_fail ? 1 : 0;
+    }
     const int n = argc > 1 ? atoi(argv[1]) : 200;
     keccak_cases();
     sender_cases(n);

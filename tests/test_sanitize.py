@@ -15,7 +15,7 @@ ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPT
 
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="gcc absent")
 def test_oracle_under_asan_ubsan():
-    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "sanitize", "N=12"], capture_output=True,
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "sanitize", "N=12", "NO_REPLAY=1"], capture_output=True,
                        text=True, env=ENV, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 mismatches" in r.stdout and "ERROR: AddressSanitizer" not in r.stderr
