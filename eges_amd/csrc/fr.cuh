@@ -183,8 +183,19 @@ template <int M, int SH = 0>
 DEV fr fr_sqr_sub(fr a, fr c) { return fr_mul_sub<M, SH>(a, a, c); }
 
 // ------------------------------------------------------------------ conversions
-// row form -> lane-serial form (every lane of the row gets all 9 limbs)
+// row form -> lane-serial form. Values outside a quad step are replicated over the four rows,
+// so row 0's limbs are the value: v_readlane puts each in an SGPR, and everything computed from
+// them (normalisation, the variable-time inversion, serialisation, Keccak) is wave-uniform and
+// compiles to scalar-ALU code, which runs beside the row-form VALU work instead of as a
+// latency-bound single-lane VALU chain.
 DEV fe fr_to_fe(fr a) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < FE_LIMBS; ++i) r.v[i] = __builtin_amdgcn_readlane(a.v, i);
+  return r;
+}
+// per-row form of the same (each row its own value; the self-test runs one item per row)
+DEV fe fr_to_fe_row(fr a) {
   fe r;
   r.v[0] = bcast<0>(a.v);
   r.v[1] = bcast<1>(a.v);

@@ -347,7 +347,7 @@ __global__ void fr_selftest_kernel(int op, uint32_t n, const uint32_t* A, const 
     }
     default: r = a;
   }
-  const fe o = fe_normalize(fr_to_fe(r));
+  const fe o = fe_normalize(fr_to_fe_row(r));
   uint32_t x[8];
   fe_to_u256(x, o);
   if (in && (threadIdx.x & (op >= FR_QUAD ? 63 : 15)) == 0) {

@@ -102,6 +102,44 @@ __global__ void __launch_bounds__(256) kern(uint32_t* out, uint64_t* clk, uint32
 #define M(i) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a[i]) : "v"(b), "v"(c));
       REP16(M)
 #undef M
+    } else if constexpr (OP == 19) {  // v_lshrrev_b64
+#define M(i) asm volatile("v_lshrrev_b64 %0, 29, %0" : "+v"(w[i]));
+      REP16(M)
+#undef M
+    } else if constexpr (OP == 20) {  // v_and_b32
+#define M(i) asm volatile("v_and_b32 %0, %0, %1" : "+v"(a[i]) : "v"(b));
+      REP16(M)
+#undef M
+    } else if constexpr (OP == 21) {  // v_lshrrev_b32
+#define M(i) asm volatile("v_lshrrev_b32 %0, 29, %0" : "+v"(a[i]));
+      REP16(M)
+#undef M
+    } else if constexpr (OP == 22) {  // v_bfe_u32
+#define M(i) asm volatile("v_bfe_u32 %0, %0, 3, 29" : "+v"(a[i]));
+      REP16(M)
+#undef M
+    } else if constexpr (OP == 23) {  // v_mov_b32
+#define M(i) asm volatile("v_mov_b32 %0, %1" : "=v"(a[i]) : "v"(a[(i + 1) & 15]));
+      REP16(M)
+#undef M
+    } else if constexpr (OP == 24) {  // v_cndmask_b32 with an SGPR-pair mask that no VALU writes
+      uint64_t msk = 0x5555555555555555ull ^ b;
+      asm volatile("s_mov_b64 %0, %0" : "+s"(msk));
+#define M(i) asm volatile("v_cndmask_b32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "s"(msk));
+      REP16(M)
+#undef M
+    } else if constexpr (OP == 25) {  // carry step as compiled: and + 64-bit shift + 64-bit add
+#define M(i) asm volatile("v_and_b32 %1, 0x1fffffff, %1\n\tv_lshrrev_b64 %0, 29, %0\n\tv_lshl_add_u64 %0, %0, 0, %2" : "+v"(w[i]), "+v"(a[i]) : "v"(w[(i + 1) & 15]));
+      REP16(M)
+#undef M
+    } else if constexpr (OP == 26) {  // v_lshlrev_b64
+#define M(i) asm volatile("v_lshlrev_b64 %0, 3, %0" : "+v"(w[i]));
+      REP16(M)
+#undef M
+    } else if constexpr (OP == 27) {  // v_sub_co_u32 + v_subb_co_u32 (64-bit subtract)
+#define M(i) asm volatile("v_sub_co_u32 %0, vcc, %0, %1\n\tv_subb_co_u32 %2, vcc, %2, %1, vcc" : "+v"(a[i]), "+v"(b), "+v"(c) :: "vcc");
+      REP16(M)
+#undef M
     } else if constexpr (OP == 18) {  // v_pk_mad? -> v_mad_u64_u32 interleaved 1:2 with v_add_u32
 #define M(i) { uint64_t cy; asm volatile("v_mad_u64_u32 %0, %2, %3, %4, %0\n\tv_add_u32 %1, %1, %3\n\tv_add_u32 %1, %1, %4" : "+v"(w[i]), "+v"(a[i]), "=s"(cy) : "v"(b), "v"(c)); }
       REP16(M)
@@ -173,6 +211,15 @@ int main() {
     run<16>("v_bfi_b32", 1, 16, bpc);
     run<17>("v_bitop3_b32(xor3)", 1, 16, bpc);
     run<18>("mad64+2add mix", 3, 16, bpc);
+    run<19>("v_lshrrev_b64", 1, 16, bpc);
+    run<26>("v_lshlrev_b64", 1, 16, bpc);
+    run<20>("v_and_b32", 1, 16, bpc);
+    run<21>("v_lshrrev_b32", 1, 16, bpc);
+    run<22>("v_bfe_u32", 1, 16, bpc);
+    run<23>("v_mov_b32", 1, 16, bpc);
+    run<24>("v_cndmask_b32(sgpr)", 1, 16, bpc);
+    run<25>("carry step (3 ops)", 3, 16, bpc);
+    run<27>("sub_co+subb_co", 2, 16, bpc);
   }
   printf("--- latency (1 chain, 1 wave/SIMD) ---\n");
   run<14>("v_mad_u64_u32 dep", 1, 1, 1);
