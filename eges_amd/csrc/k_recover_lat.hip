@@ -13,11 +13,13 @@
 //   table {1..16}R on one global Z ....... co-Z dblu / zaddu + backward rescale (as core.cuh)
 //   Strauss over 26 windows ............. unchecked adds, exact redo if the
 //                                          accumulator was poisoned (Z == 0 and not infinity)
-//   Z^-1 (safegcd, lane-serial), affine, serialize, Keccak address; lane 0 stores.
+//   Z^-1 (safegcd: divsteps on the scalar ALU, matrix updates limb-parallel), affine,
+//   serialize, Keccak address (scalar ALU); lane 0 stores.
 #include <type_traits>
 
 #include "core.cuh"
 #include "frg.cuh"
+#include "modinv_row.cuh"
 
 namespace eges {
 
@@ -299,7 +301,7 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   ok = ok && !qinf;  // main_impl.h:120
   // --- affine, serialize, address
   const fr zq = fr_select(ok, Q.z, fr_one());
-  const fr zi = fe_to_fr(fe_inv_var(fr_to_fe(zq)));
+  const fr zi = fr_inv_var(zq);  // row-parallel safegcd (modinv_row.cuh)
   fr zi2, zi3;
   zi2 = fr_sqr(zi);
   fr X1, Y1;

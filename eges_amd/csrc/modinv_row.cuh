@@ -1,0 +1,135 @@
+#pragma once
+// Variable-time safegcd for the latency kernel (one signature per wave): the divsteps run on the
+// scalar ALU (wave-uniform data), and the 2x2 transition-matrix update of the four 270-bit
+// states f, g, d, e runs limb-parallel over a 16-lane row (lane L = signed radix-2^30 limb L,
+// lanes 9..15 zero), so a batch costs a few dependent VALU steps instead of a 9-limb serial
+// carry chain per state. Same algorithm and values as modinv.cuh's modinv256_var (Bernstein-Yang
+// divsteps; update_de_30's md / me correction by M^-1 mod 2^30, after upstream libsecp256k1's
+// modinv32, MIT).
+//
+// Limbs are kept "almost normalised" instead of exact: after each update, two parallel carry
+// rounds (DPP row_shl / row_shr by one lane) leave limbs 0..7 in [-4, 2^30 + 4] and the top
+// limb signed and small, so every product of the next update (|u|, |v| <= 2^30) fits its 64-bit
+// lane. The low 30 bits of limb 0 are the value's low 30 bits, which is all the divsteps read.
+// Two consequences of the redundancy, both handled exactly:
+//   - g == 0 is detected as "all limbs zero"; a zero held in another form runs on to the cap
+//     (26 batches >= 741 divsteps, the bound for 256-bit inputs), where further batches leave
+//     the value unchanged;
+//   - the sign terms of md / me read the top limb, which can disagree with the value's sign
+//     near zero; d, e then stay within a few M of the usual (-2M, M), and the final reduction
+//     on the scalar ALU brings d into [0, M) by exact comparison.
+#include "fr.cuh"
+#include "modinv.cuh"
+
+namespace eges {
+
+// t / 2^30 (exact: lane 0's low 30 bits are zero) as almost-normalised limbs (see above)
+DEV int32_t row_shift30(int64_t t) {
+  const uint32_t L = row_lane();
+  const int64_t h = t >> 30;                                // |h| <= 2^32
+  const uint32_t ln = shl<1>((uint32_t)t & (uint32_t)M30);  // limb L+1's low 30 bits
+  const int64_t r = h + (int64_t)ln;                        // weight 2^(30 L) of t / 2^30
+  const int32_t h2 = (int32_t)(r >> 30);                    // in [-4, 5]
+  const int32_t hp = (int32_t)shr<1>((uint32_t)h2);         // limb L-1's carry (0 into lane 0)
+  const int32_t keep = L == 8 ? (int32_t)r : (int32_t)((uint32_t)r & (uint32_t)M30);
+  return L <= 8 ? keep + hp : 0;
+}
+
+// canonical signed radix-2^30 (limbs 0..7 in [0, 2^30), limb 8 signed); wave-uniform
+DEV void s30_carry(s30& a) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    a.v[i + 1] += a.v[i] >> 30;
+    a.v[i] &= M30;
+  }
+}
+// a >= b for canonical values
+DEV bool s30_ge(const s30& a, const s30& b) {
+#pragma unroll
+  for (int i = 8; i >= 0; --i)
+    if (a.v[i] != b.v[i]) return a.v[i] > b.v[i];
+  return true;
+}
+
+// x^-1 mod M for x in [0, M), x wave-uniform (0 maps to 0)
+template <class Mod>
+DEV void modinv256_row_var(uint32_t out[8], const uint32_t x[8]) {
+  const uint32_t L = row_lane();
+  const s30 xs = s30_from_u256(x);
+  int32_t f = 0, g = 0, m = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    f = L == (uint32_t)i ? Mod::m[i] : f;
+    g = L == (uint32_t)i ? xs.v[i] : g;
+  }
+  m = f;
+  int32_t d = 0, e = L == 0 ? 1 : 0;
+  int32_t eta = -1;
+#pragma unroll 1
+  for (int it = 0; it < 26; ++it) {
+    trans2x2 t;
+    eta = divsteps_30_var(eta, (uint32_t)__builtin_amdgcn_readlane(f, 0), (uint32_t)__builtin_amdgcn_readlane(g, 0), t);
+    // update_de_30's correction, from lane 0's limbs and the top limbs' signs
+    const int32_t d0 = __builtin_amdgcn_readlane(d, 0), e0 = __builtin_amdgcn_readlane(e, 0);
+    const int32_t sd = __builtin_amdgcn_readlane(d, 8) >> 31, se = __builtin_amdgcn_readlane(e, 8) >> 31;
+    int32_t md = (t.u & sd) + (t.v & se);
+    int32_t me = (t.q & sd) + (t.r & se);
+    const int64_t cd0 = (int64_t)t.u * d0 + (int64_t)t.v * e0;
+    const int64_t ce0 = (int64_t)t.q * d0 + (int64_t)t.r * e0;
+    md -= (int32_t)((Mod::minv * (uint32_t)cd0 + (uint32_t)md) & (uint32_t)M30);
+    me -= (int32_t)((Mod::minv * (uint32_t)ce0 + (uint32_t)me) & (uint32_t)M30);
+    // the four states, limb-parallel
+    const int64_t cf = (int64_t)t.u * f + (int64_t)t.v * g;
+    const int64_t cg = (int64_t)t.q * f + (int64_t)t.r * g;
+    const int64_t cd = (int64_t)t.u * d + (int64_t)t.v * e + (int64_t)m * md;
+    const int64_t ce = (int64_t)t.q * d + (int64_t)t.r * e + (int64_t)m * me;
+    f = row_shift30(cf);
+    g = row_shift30(cg);
+    d = row_shift30(cd);
+    e = row_shift30(ce);
+    if (!__any(g != 0)) break;
+  }
+  // exact values on the scalar ALU: f = +-1, d == +-x^-1 (mod M)
+  s30 fv, dv, mv;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    fv.v[i] = __builtin_amdgcn_readlane(f, i);
+    dv.v[i] = __builtin_amdgcn_readlane(d, i);
+    mv.v[i] = Mod::m[i];
+  }
+  s30_carry(fv);
+  s30_carry(dv);
+#pragma unroll 1
+  while (dv.v[8] < 0) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) dv.v[i] += mv.v[i];
+    s30_carry(dv);
+  }
+#pragma unroll 1
+  while (s30_ge(dv, mv)) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) dv.v[i] -= mv.v[i];
+    s30_carry(dv);
+  }
+  if (fv.v[8] < 0) {  // f == -1: negate (M - d, or 0)
+    bool z = true;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) z = z && dv.v[i] == 0;
+    if (!z) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) dv.v[i] = mv.v[i] - dv.v[i];
+      s30_carry(dv);
+    }
+  }
+  s30_to_u256(out, dv);
+}
+
+// Z^-1 in the latency kernel: value replicated over the rows in, same out (row form)
+DEV fr fr_inv_var(fr a) {
+  uint32_t x[8], y[8];
+  fe_to_u256(x, fe_normalize(fr_to_fe(a)));
+  modinv256_row_var<ModP>(y, x);
+  return fe_to_fr(fe_from_u256(y));
+}
+
+}  // namespace eges

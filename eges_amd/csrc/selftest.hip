@@ -290,6 +290,7 @@ extern "C" double eges_opbench(int op, int reps) {
 // ---------------------------------------------------------------- row-form field (fr.cuh)
 // One item per 16-lane row; canonical 256-bit words in and out, as eges_selftest.
 #include "fr.cuh"
+#include "modinv_row.cuh"
 namespace eges {
 enum : int {
   FR_MUL = 0,      // a * b
@@ -301,6 +302,7 @@ enum : int {
   FR_CHAIN = 6,    // 64 squarings of a, then * b
   FR_QUAD = 7,     // fr_mul4 (a*b, b*c, c*a, a*a in one pass): out = (ab + 2bc + 3ca) * a^2
   FR_QUAD2 = 8,    // fr_mul2 (a*b, c*c): out = ab + 2c^2
+  FR_INV = 9,      // fr_inv_var (row-parallel safegcd): out = a^-1
 };
 __global__ void fr_selftest_kernel(int op, uint32_t n, const uint32_t* A, const uint32_t* B, const uint32_t* C,
                                    uint32_t* out) {
@@ -345,6 +347,7 @@ __global__ void fr_selftest_kernel(int op, uint32_t n, const uint32_t* A, const 
       r = fr_add(q0, fr_mul_small(q1, 2));
       break;
     }
+    case FR_INV: r = fr_inv_var(a); break;
     default: r = a;
   }
   const fe o = fe_normalize(fr_to_fe_row(r));

@@ -14,7 +14,7 @@ from conftest import ROOT
 from test_gpu_field import P, dec, enc, samples
 
 pytestmark = pytest.mark.gpu
-FR = dict(MUL=0, SQR=1, MULSUB=2, SUB=3, LAZY=4, NORMW=5, CHAIN=6, QUAD=7, QUAD2=8)
+FR = dict(MUL=0, SQR=1, MULSUB=2, SUB=3, LAZY=4, NORMW=5, CHAIN=6, QUAD=7, QUAD2=8, INV=9)
 
 
 @pytest.fixture(scope="module")
@@ -55,6 +55,8 @@ def expect(op, a, b, c):
         return (a * b + 2 * b * c + 3 * c * a) * a * a % P
     if op == "QUAD2":
         return (a * b + 2 * c * c) % P
+    if op == "INV":  # row-parallel safegcd (modinv_row.cuh); 0 -> 0
+        return pow(a % P, P - 2, P)
 
 
 @pytest.mark.parametrize("op", list(FR))
@@ -66,6 +68,15 @@ def test_fr_ops(st, op):
     got = run(st, op, a, b, c)
     bad = [i for i in range(n) if got[i] != expect(op, a[i], b[i], c[i])]
     assert not bad, [(i, hex(a[i]), hex(b[i]), hex(got[i])) for i in bad[:5]]
+
+
+def test_fr_inv_edges(st):
+    """Inverses of 0, 1, p - 1, p (weak zero), small and near-2^256 values, powers of two."""
+    vals = [0, 1, 2, 3, P - 1, P - 2, P, P + 1, 2**255, 2**256 - 1 - P, (P + 1) // 2] + [2**k for k in range(0, 256, 17)]
+    vals = [v for v in vals if v < 2**256]
+    got = run(st, "INV", vals, vals, vals)
+    bad = [(hex(v), hex(g)) for v, g in zip(vals, got) if g != expect("INV", v, 0, 0)]
+    assert not bad, bad[:5]
 
 
 def test_fr_latency_record(st):
