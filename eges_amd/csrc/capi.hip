@@ -282,12 +282,12 @@ static hipError_t stamp_buf(size_t waves, hipStream_t st) {
 
 hipError_t launch_recover_pass(Dev& d, const RecoverParams& p, hipStream_t st) {
 #ifdef EGES_PHASE_STAMPS
-  if (p.n <= lat_max()) {
+  if (p.n <= lat_max() || p.raw_sig) {
     hipError_t e = stamp_buf(lat_waves(p.n), st);
     return e != hipSuccess ? e : launch_recover_lat_stamped(p, st, g_stamps);
   }
 #endif
-  if (p.n <= lat_max()) return launch_recover_lat(p, st);
+  if (p.n <= lat_max() || p.raw_sig) return launch_recover_lat(p, st);
   return launch_recover(p, d.mb_recover, d.ws_blocks, st);
 }
 
@@ -349,9 +349,14 @@ int run_recover_dev(Dev& d, const uint8_t* msg, const uint8_t* sig, size_t n, ui
   Serial ser(d, st);
   for (size_t off = 0; off < n; off += CHUNK) {
     const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
-    HIPCHK(launch_prep_ecrecover(msg + off * 32, sig + off * 65, m, (uint32_t)n_pad, rec, st));
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr ? addr + off * 20 : nullptr, pub ? pub + off * 65 : nullptr,
                     d.gtab, d.ws};
+    if (m <= lat_max()) {  // the latency kernel parses the bytes itself
+      p.raw_msg = msg + off * 32;
+      p.raw_sig = sig + off * 65;
+    } else {
+      HIPCHK(launch_prep_ecrecover(msg + off * 32, sig + off * 65, m, (uint32_t)n_pad, rec, st));
+    }
 #ifdef EGES_PHASE_STAMPS
     if (p.n > lat_max()) {
       HIPCHK(stamp_buf((size_t)d.ws_blocks * 4 /* waves per block */, st));
@@ -564,6 +569,14 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
     int rc_ = flush_in(B);          \
     if (rc_) return rc_;            \
   } while (0)
+  // the kernels wait for their inputs' copies (a single chunk uses one stream: nothing to join)
+#define JOIN_IN(r)                                      \
+  do {                                                  \
+    if (sx != st) {                                     \
+      HIPCHK(hipEventRecord(ev_in[r], sx));             \
+      HIPCHK(hipStreamWaitEvent(st, ev_in[r], 0));      \
+    }                                                   \
+  } while (0)
   struct Pending {
     size_t base, m;
     int r;
@@ -576,7 +589,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
     uint8_t* o_pub = q.B + q.g.o_out;
     uint8_t* o_addr = o_pub + q.m * 65;
     uint8_t* o_st = o_addr + q.m * 32;
-    HIPCHK(hipStreamWaitEvent(sx, ev_k[q.r], 0));
+    if (sx != st) HIPCHK(hipStreamWaitEvent(sx, ev_k[q.r], 0));
     if (pinned) {  // outputs are already in the pinned buffer; the signing hashes are not
       if (j.kind == HostJob::SENDER_RAW && j.sighash)
         HIPCHK(hipMemcpyAsync(pin + sighash_off(q), q.B + sighash_off(q), q.m * 32, hipMemcpyDeviceToHost, sx));
@@ -619,11 +632,15 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       H2D(B, dm, j.a + base * 32, m * 32);
       H2D(B, ds, j.b + base * 65, m * 65);
       FLUSH_IN(B);
-      HIPCHK(hipEventRecord(ev_in[r], sx));
-      HIPCHK(hipStreamWaitEvent(st, ev_in[r], 0));
-      HIPCHK(launch_prep_ecrecover(dm, ds, (uint32_t)m, (uint32_t)m_pad, rec, st));
+      JOIN_IN(r);
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, j.addr ? o_addr : nullptr, j.pub ? o_pub : nullptr,
                       d.gtab, d.ws};
+      if (m <= lat_max()) {  // the latency kernel parses the bytes itself
+        p.raw_msg = dm;
+        p.raw_sig = ds;
+      } else {
+        HIPCHK(launch_prep_ecrecover(dm, ds, (uint32_t)m, (uint32_t)m_pad, rec, st));
+      }
       HIPCHK(launch_recover_pass(d, p, st));
     } else if (j.kind == HostJob::SENDER) {
       uint8_t* dh = I;
@@ -637,8 +654,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       H2D(B, dv, j.d + base * 32, m * 32);
       if (j.e) H2D(B, df, j.e + base, m);
       FLUSH_IN(B);
-      HIPCHK(hipEventRecord(ev_in[r], sx));
-      HIPCHK(hipStreamWaitEvent(st, ev_in[r], 0));
+      JOIN_IN(r);
       HIPCHK(launch_prep_sender(dh, dr, dsv, dv, j.e ? df : nullptr, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id,
                                 rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
@@ -649,8 +665,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       H2D(B, din, j.a + base * 128, m * 128);
       if (j.inlen) H2D(B, reinterpret_cast<uint8_t*>(dlen), j.inlen + base, m * 4);
       FLUSH_IN(B);
-      HIPCHK(hipEventRecord(ev_in[r], sx));
-      HIPCHK(hipStreamWaitEvent(st, ev_in[r], 0));
+      JOIN_IN(r);
       if (pinned) std::memset(o_addr, 0, m * 32);
       else HIPCHK(hipMemsetAsync(o_addr, 0, m * 32, st));
       HIPCHK(launch_prep_precompile(din, j.inlen ? dlen : nullptr, (uint32_t)m, (uint32_t)m_pad, rec, st));
@@ -667,8 +682,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       if (rg.raw_len) H2D(B, draw, j.a + rg.raw_lo, rg.raw_len);
       H2D(B, reinterpret_cast<uint8_t*>(doff), j.offsets + base, 8 * (m + 1));
       FLUSH_IN(B);
-      HIPCHK(hipEventRecord(ev_in[r], sx));
-      HIPCHK(hipStreamWaitEvent(st, ev_in[r], 0));
+      JOIN_IN(r);
       HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, vf, st));
       HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
@@ -683,13 +697,12 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       H2D(B, dm, j.c + base * 32, m * 32);
       H2D(B, ds, j.d + base * 64, m * 64);
       FLUSH_IN(B);
-      HIPCHK(hipEventRecord(ev_in[r], sx));
-      HIPCHK(hipStreamWaitEvent(st, ev_in[r], 0));
+      JOIN_IN(r);
       VerifyParams p{dp, dl, dm, ds, (uint32_t)m, o_st, d.gtab, d.ws};
       verify_scratch_bind(p, B + rg.o_rec, m_pad);
       HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
     }
-    HIPCHK(hipEventRecord(ev_k[r], st));
+    if (sx != st) HIPCHK(hipEventRecord(ev_k[r], st));
     // --- the previous chunk's outputs, while this chunk computes
     if (have_prev) {
       rc = outputs(prev);
@@ -708,6 +721,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
   return EGES_SUCCESS;
 #undef H2D
 #undef FLUSH_IN
+#undef JOIN_IN
 }
 
 // Contiguous index shards across the engine's devices.

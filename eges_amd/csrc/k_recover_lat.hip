@@ -250,10 +250,20 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   const uint32_t np = prm.n_pad;
   // --- parse (every lane reads the same record)
   uint32_t rl[8], sl[8], zl[8];
-  rec_get(prm, 8, idx, rl);
-  rec_get(prm, 16, idx, sl);
-  rec_get(prm, 0, idx, zl);
-  const uint32_t meta = prm.rec[(size_t)24 * np + idx];
+  uint32_t meta;
+  if (prm.raw_sig) {  // fused prep: prep_ecrecover_kernel's parse (k_prep.hip), same record
+    const uint8_t* sg = prm.raw_sig + (size_t)idx * 65;
+    limbs_from_be32(zl, prm.raw_msg + (size_t)idx * 32);
+    limbs_from_be32(rl, sg);
+    limbs_from_be32(sl, sg + 32);
+    const uint32_t v = sg[64];
+    meta = v >= 4 ? (ST_INVALID_RECOVERY_ID << 8) : v;  // checkSignature, secp256.go:171-179
+  } else {
+    rec_get(prm, 8, idx, rl);
+    rec_get(prm, 16, idx, sl);
+    rec_get(prm, 0, idx, zl);
+    meta = prm.rec[(size_t)24 * np + idx];
+  }
   const uint32_t recid = meta & 3u;
   bool ok = ((meta >> 8) & 0xffu) == ST_OK;
   bool ovr, ovs, ovz;

@@ -32,6 +32,10 @@ struct RecoverParams {
   const uint32_t* gtab;
   uint32_t* ws;
   uint32_t addr_stride = 20;  // bytes between consecutive addresses (32 for the EVM precompile's word)
+  // latency kernel only: parse msg (n*32) / sig (n*65) bytes itself instead of reading rec rows
+  // (prep_ecrecover_kernel fused away for small ecrecover calls)
+  const uint8_t* raw_msg = nullptr;
+  const uint8_t* raw_sig = nullptr;
 };
 
 struct VerifyParams {
