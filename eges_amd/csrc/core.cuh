@@ -307,11 +307,17 @@ DEV ge neg_if(const ge& p, bool neg) {  // y magnitude <= 2 afterwards
   return r;
 }
 
+#ifndef EGES_PF
+#define EGES_PF 0  // measured ±0 % (DESIGN.md §6 "tried"); kept as an A/B knob
+#endif
 struct CoreLds {
   int8_t rdig[2][RWIN][WG];    // R / lambda R digits
   gdig_t gdig[2][GWIN][WG];    // G / 2^128 G digits
   uint32_t inv_scratch[2 * NWAVES * 10];
   uint32_t zeta[FE_LIMBS][WG];  // per-lane global Z of the R table
+#if EGES_PF
+  uint4 pf[2][PT_WORDS / 4][WG];  // the next window's two R-table entries (LDS-DMA prefetch)
+#endif
 };
 
 template <int N>
@@ -390,11 +396,48 @@ struct Stamper {
   }
 };
 
+#if EGES_PF
+// LDS-DMA prefetch of one R-table entry per lane (global_load_lds_dwordx4, no VGPRs in flight):
+// part q of the entry lands at pf[q][tid], written by the lane's own wave (wave-uniform LDS base
+// + lane x 16 B), so only the wave's own vmcnt orders it. Issued after a window's additions for
+// the next window, it is in flight during the 5 doublings between them.
+DEV void pf_issue(const uint32_t* src, uint4 (*pf)[WG]) {
+  const int wave_base = threadIdx.x & ~63;
+#pragma unroll
+  for (int q = 0; q < PT_WORDS / 4; ++q)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 4 * q),
+                                     (__attribute__((address_space(3))) void*)&pf[q][wave_base], 16, 0, 0);
+}
+DEV ge pf_read(const uint4 (*pf)[WG]) {
+  uint32_t w[PT_WORDS];
+#pragma unroll
+  for (int q = 0; q < PT_WORDS / 4; ++q) {
+    const uint4 u = pf[q][threadIdx.x];
+    w[4 * q] = u.x;
+    w[4 * q + 1] = u.y;
+    w[4 * q + 2] = u.z;
+    w[4 * q + 3] = u.w;
+  }
+  ge p;
+  pt_unpack(w, p.x, p.y);
+  return p;
+}
+DEV int rdig_entry(const CoreLds& L, int j, int w) {
+  const int d = L.rdig[j][w][threadIdx.x];
+  const int a = d < 0 ? -d : d;
+  return a > 0 ? a - 1 : 0;
+}
+#endif
+
 // Strauss-Shamir over the digits in L and the tables (per-lane R table at `base`, G / lambda G
 // in gtab): acc = sum of the window contributions on the R table's isomorphic curve.
 template <bool CHECKED>
 DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab, CoreLds& L) {
   const int tid = threadIdx.x;
+#if EGES_PF
+#pragma unroll
+  for (int j = 0; j < 2; ++j) pf_issue(base + (size_t)(rdig_entry(L, j, RWIN - 1) * WG + tid) * PT_WORDS, L.pf[j]);
+#endif
   // RWIN windows of RBITS bits (R, lambda R) interleaved with GWIN windows of GBITS bits
   // (G, 2^128 G) every GSTEP-th window.
   inf = true;
@@ -408,6 +451,9 @@ DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab
       for (int k = 0; k < RBITS; ++k) acc = gej_double(acc);
     }
     const int nadd = (w % GSTEP) == 0 ? 4 : 2;
+#if EGES_PF
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this window's prefetched entries
+#endif
 #pragma unroll 1
     for (int j = 0; j < nadd; ++j) {
       int d;
@@ -416,7 +462,11 @@ DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab
       const int a = d < 0 ? -d : d;
       const int e = a > 0 ? a - 1 : 0;
       ge p;
+#if EGES_PF
+      if (j < 2) p = pf_read(L.pf[j]);
+#else
       if (j < 2) p = load_pt(base + (size_t)(e * WG + tid) * PT_WORDS);
+#endif
       else p = load_pt(gtab + ((size_t)(j - 2) * GTAB + e) * PT_WORDS);
       if (j == 1) p.x = fe_mul(p.x, fe_const(FE_BETA));
       if (j < 2) {
@@ -429,6 +479,13 @@ DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab
         else add_step_zinv_fast(acc, inf, neg_if(p, d < 0), d != 0, z);
       }
     }
+#if EGES_PF
+    if (w > 0) {  // the next window's entries; this window's LDS reads have completed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < 2; ++j) pf_issue(base + (size_t)(rdig_entry(L, j, w - 1) * WG + tid) * PT_WORDS, L.pf[j]);
+    }
+#endif
   }
 }
 
