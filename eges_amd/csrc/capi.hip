@@ -447,7 +447,8 @@ int run_verify_dev(Dev& d, const uint8_t* pub, const uint8_t* publen, const uint
     const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
     VerifyParams p{pub + off * 65, publen + off, msg + off * 32, sig + off * 64, m, ok + off, d.gtab, d.ws};
     verify_scratch_bind(p, d.buf, n_pad);
-    HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
+    if (m <= lat_max()) HIPCHK(launch_verify_lat(p, st));
+    else HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
   }
   return EGES_SUCCESS;
 }
@@ -507,7 +508,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
   const bool pinned = nreg == 1 && worst <= PIN_BYTES;
   // Small calls on the latency kernel (no shared workspace) run on one of the device's lanes,
   // concurrently with each other; everything else on the device's main resources, in order.
-  const bool small = pinned && cnt <= lat_max() && j.kind != HostJob::VERIFY;
+  const bool small = pinned && cnt <= lat_max();
   Lane* lane = nullptr;
   std::unique_lock<std::mutex> lk;
   if (small) {
@@ -700,7 +701,9 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       JOIN_IN(r);
       VerifyParams p{dp, dl, dm, ds, (uint32_t)m, o_st, d.gtab, d.ws};
       verify_scratch_bind(p, B + rg.o_rec, m_pad);
-      HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
+      // small (lane) calls must not touch the device's shared workspace: latency kernel
+      if (small || m <= lat_max()) HIPCHK(launch_verify_lat(p, st));
+      else HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
     }
     if (sx != st) HIPCHK(hipEventRecord(ev_k[r], st));
     // --- the previous chunk's outputs, while this chunk computes

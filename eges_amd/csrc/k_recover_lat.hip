@@ -1,4 +1,4 @@
-// Latency kernel for small recover batches: one signature per wave.
+// Latency kernels for small batches: one signature per wave (recover; verify at the end).
 //
 // Same path and same outputs as recover_kernel (k_recover.hip; recovery/main_impl.h:38-191,
 // ecmult_impl.h:286-404, eckey_impl.h:36-52, crypto.go:194-197), for batches too small to fill
@@ -349,6 +349,96 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
       for (int i = 0; i < 8; ++i) stamps[(size_t)blockIdx.x * 8 + i] = st_.acc[i];
     }
   }
+}
+
+// ------------------------------------------------------------------ verify, one item per wave
+// crypto.VerifySignature for small batches (verify_kernel's checks, k_verify.hip; ext.h:58-75,
+// eckey_impl.h:17-34, secp256k1.c:293-308, ecdsa_impl.h:203-271): wave 1 computes s^-1
+// (variable-time safegcd), u1 = z/s, u2 = r/s and the digits while wave 0 parses the public key
+// (the square root for 33-byte keys, the curve equation for 65-byte ones); then Q = u2 P + u1 G
+// and x(Q) == r checked projectively (r Z^2 == X), no field inversion.
+DEV void verify_lat_body(const VerifyParams& prm) {
+  __shared__ LatLds S;
+  NoStamp st_;
+  const uint32_t idx = blockIdx.x;  // grid = n
+  uint32_t l[8];
+  bool ovr, ovs, ovz;
+  limbs_from_be32(l, prm.sig + (size_t)idx * 64);
+  const sc R = sc_from_limbs(l, ovr);
+  limbs_from_be32(l, prm.sig + (size_t)idx * 64 + 32);
+  const sc Sv = sc_from_limbs(l, ovs);
+  limbs_from_be32(l, prm.msg + (size_t)idx * 32);
+  const sc Z = sc_from_limbs(l, ovz);  // the message reduced mod n
+  // parse_compact overflow, high s (ecdsa_verify), r or s zero (sig_verify)
+  const bool sig_ok = !ovr && !ovs && !sc_is_high(Sv) && !sc_is_zero(R) && !sc_is_zero(Sv);
+  if (threadIdx.x >= 64) {  // wave 1
+    const sc sinv = sc_inv_var(sc_select(sig_ok, Sv, sc_one()));
+    const sc u1 = sc_mul(sinv, Z);
+    const sc u2 = sc_select(sig_ok, sc_mul(sinv, R), sc_one());
+    recode_digits(u2, u1, S);
+    __syncthreads();  // digits ready
+    return;
+  }
+  // --- public key (eckey_impl.h:17-34)
+  const uint32_t plen = prm.publen[idx];
+  const uint8_t* pk = prm.pub + (size_t)idx * 65;
+  const uint32_t pfx = pk[0];
+  uint32_t px[8], py[8];
+  limbs_from_be32(px, pk + 1);
+  if (plen == 65) {
+    limbs_from_be32(py, pk + 33);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) py[q] = 0;
+  }
+  const bool x_ok = !u256_ge(px, FE_P), y_ok = !u256_ge(py, FE_P);
+  const bool c33 = plen == 33 && (pfx == 2 || pfx == 3);
+  const bool c65 = plen == 65 && (pfx == 4 || pfx == 6 || pfx == 7);
+  const fr X = fe_to_fr(fe_from_u256(px)), Y = fe_to_fr(fe_from_u256(py));
+  ger P;
+  bool pk_ok;
+  if (c33) {  // wave-uniform
+    pk_ok = ger_set_xo(P, X, pfx == 3) && x_ok;
+  } else {
+    const bool hybrid_bad = (pfx == 6 || pfx == 7) && ((py[0] & 1u) != (pfx == 7 ? 1u : 0u));
+    const bool on = fr_equal(fr_add(fr_mul(fr_sqr(X), X), fr_small(7)), fr_sqr(Y));
+    pk_ok = c65 && x_ok && y_ok && !hybrid_bad && on;
+    P.x = X;
+    P.y = Y;
+  }
+  bool ok = sig_ok && pk_ok;
+  // failed items carry the generator, so every later step stays well-defined
+  const ge G = gen_point();
+  P.x = fr_select(ok, P.x, fe_to_fr(G.x));
+  P.y = fr_select(ok, P.y, fe_to_fr(G.y));
+  const fr beta = fe_to_fr(fe_const(FE_BETA));
+  gejr Q;
+  bool qinf;
+  ecmult_wave(Q, qinf, P, prm.gtab, S, beta, &st_);
+  ok = ok && !qinf;
+  // x(Q) mod n == r  <=>  r Z^2 == X  or  (r < p - n and (r + n) Z^2 == X)  (ecdsa_impl.h:246-270)
+  const fr z2 = fr_sqr(Q.z);
+  bool eq = fr_equal(Q.x, fr_mul(fe_to_fr(fe_from_u256(R.v)), z2));
+  if (!eq && !u256_ge(R.v, P_MINUS_N)) {
+    uint32_t rn[8];
+    uint64_t c = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      c += (uint64_t)R.v[q] + SC_N[q];
+      rn[q] = (uint32_t)c;
+      c >>= 32;
+    }
+    eq = fr_equal(Q.x, fr_mul(fe_to_fr(fe_from_u256(rn)), z2));
+  }
+  if (lane_id() == 0) prm.ok[idx] = (ok && eq) ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(LAT_WG) verify_lat_kernel(VerifyParams prm) { verify_lat_body(prm); }
+
+hipError_t launch_verify_lat(const VerifyParams& p, hipStream_t st) {
+  if (p.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(verify_lat_kernel, dim3(p.n), dim3(LAT_WG), 0, st, p);
+  return hipGetLastError();
 }
 
 __global__ void __launch_bounds__(LAT_WG) recover_lat_kernel(RecoverParams prm) {

@@ -1,5 +1,5 @@
-"""The latency kernel (k_recover_lat.hip: one signature per 16-lane row) against the throughput
-kernel and the golden fixtures. Batches up to EGES_LAT_MAX signatures take the latency kernel;
+"""The latency kernels (k_recover_lat.hip: one signature per wave, recover and verify) against the
+throughput kernels and the golden fixtures. Batches up to EGES_LAT_MAX signatures take the latency kernel;
 EGES_LAT_MAX=0 forces the lane-serial kernel (capi.hip lat_max is read per call), so every
 case runs both ways and must agree byte for byte, and with the reference-generated fixtures."""
 import os
@@ -50,6 +50,46 @@ def test_lat_kernel_golden_sender(engine):
             addr, st = engine.sender_batch(g["sighash"][sel], g["r"][sel], g["s"][sel], g["v"][sel], g["vflags"][sel],
                                            signer, cid)
         assert np.array_equal(st, g["status"][sel]) and np.array_equal(addr, g["addr"][sel])
+
+
+def test_lat_verify_golden(engine):
+    """VerifySignature's 591 golden items (every key encoding and reject class) through the
+    verify latency kernel and through the lane-serial verify kernel."""
+    g = load_golden("verify.npz")
+    names = list(g["kind_names"])
+    with lat_max(1 << 20):
+        ok = engine.verify_batch(g["pub"], g["publen"], g["msg"], g["sig"])
+    bad = np.nonzero(ok != g["ok"])[0]
+    assert bad.size == 0, [(int(i), names[g["kind"][i]], int(ok[i]), int(g["ok"][i])) for i in bad[:20]]
+    with lat_max(0):
+        ok2 = engine.verify_batch(g["pub"], g["publen"], g["msg"], g["sig"])
+    assert np.array_equal(ok, ok2)
+
+
+@pytest.mark.parametrize("n", [1, 3, 64, 1000])
+def test_lat_verify_sizes(engine, n):
+    """Synthetic signatures, compressed and uncompressed keys, every 3rd message altered; both
+    kernels agree and match the construction."""
+    import torch
+    msg, sig, _ = engine.synth_sign_dev(52_000 + n, n, 0)
+    torch.cuda.synchronize()
+    mh, sh = msg.cpu().numpy(), sig.cpu().numpy()
+    pub, _, st = engine.ecrecover_batch(mh, sh)
+    assert (st == 0).all()
+    pk = pub.copy()
+    lens = np.full(n, 65, np.uint8)
+    comp = np.arange(n) % 2 == 1  # odd items as 33-byte keys
+    pk[comp, 0] = 2 + (pub[comp, 64] & 1)
+    pk[comp, 33:] = 0
+    lens[comp] = 33
+    mm = mh.copy()
+    mm[::3, 0] ^= 1
+    with lat_max(1 << 20):
+        ok = engine.verify_batch(pk, lens, mm, sh[:, :64])
+    with lat_max(0):
+        ok2 = engine.verify_batch(pk, lens, mm, sh[:, :64])
+    assert np.array_equal(ok, ok2)
+    assert ok.tolist() == [0 if i % 3 == 0 else 1 for i in range(n)]
 
 
 @pytest.mark.parametrize("n", [1, 2, 15, 16, 17, 1000, 4097])

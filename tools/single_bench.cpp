@@ -1,5 +1,6 @@
-// Native-thread benchmark of the single-item C-ABI entry (eges_ecdsa_recover), the call a Go
-// caller makes per crypto.Ecrecover: T threads x M calls each, every result
+// Native-thread benchmark of the single-item C-ABI entries (eges_ecdsa_recover, the call a Go
+// caller makes per crypto.Ecrecover, and eges_ecdsa_verify per crypto.VerifySignature;
+// INTEGRATION.md §2): one-caller latencies, then T threads x M recover calls, every result
 // checked against the synthetic signer's address. Prints one JSON line.
 //   build: hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/single_bench.cpp -Iinclude
 //          -Leges_amd -leges -Wl,-rpath,'$ORIGIN/../eges_amd' -o tools/single_bench
@@ -54,6 +55,18 @@ int main(int argc, char** argv) {
   }
   std::sort(lat.begin() + 20, lat.end());
   const double p50 = lat[20 + (lat.size() - 20) / 2], p99 = lat[20 + (lat.size() - 20) * 99 / 100];
+  // one caller: eges_ecdsa_verify (crypto.VerifySignature's seam) against the recovered keys
+  std::vector<double> vlat;
+  for (int k = 0; k < 300; ++k) {
+    const size_t i = (size_t)k % n;
+    uint8_t pub[65];
+    if (eges_ecdsa_recover(pub, &sig[i * 65], &msg[i * 32]) != 1) ++bad;
+    const auto t0 = clk::now();
+    if (eges_ecdsa_verify(&sig[i * 65], &msg[i * 32], pub, 65) != 1) ++bad;
+    vlat.push_back(std::chrono::duration<double, std::milli>(clk::now() - t0).count());
+  }
+  std::sort(vlat.begin() + 20, vlat.end());
+  const double vp50 = vlat[20 + (vlat.size() - 20) / 2];
   // T callers
   std::vector<std::thread> th;
   const auto t0 = clk::now();
@@ -64,8 +77,9 @@ int main(int argc, char** argv) {
   for (auto& x : th) x.join();
   const double dt = std::chrono::duration<double>(clk::now() - t0).count();
   std::printf("{\"metric\": \"single-item eges_ecdsa_recover\", \"p50_ms_one_caller\": %.4f, \"p99_ms_one_caller\": %.4f, "
-              "\"threads\": %d, \"calls_per_thread\": %d, \"recoveries_per_s\": %.1f, \"errors\": %ld}\n",
-              p50, p99, T, M, (double)T * M / dt, bad.load());
+              "\"verify_p50_ms_one_caller\": %.4f, \"threads\": %d, \"calls_per_thread\": %d, \"recoveries_per_s\": %.1f, "
+              "\"errors\": %ld}\n",
+              p50, p99, vp50, T, M, (double)T * M / dt, bad.load());
   eges_shutdown();
   return bad.load() ? 2 : 0;
 }
