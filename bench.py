@@ -91,10 +91,11 @@ def host_cpus():
     return {"nproc": nproc, "affinity": aff, "cgroup_cpus": quota, "threads": threads}
 
 
-def cpu_baseline(msg_h, sig_h, target_s):
+def cpu_baseline(msg_h, sig_h, target_s, gpu_addr=None):
     """Reference libsecp256k1 (compiled in place, oracle/_ref) on the host cores: the
     goroutine-parallel types.Sender/Ecrecover path restated as one pthread per granted CPU.
-    Returns the cpu_baseline object or None."""
+    With gpu_addr (the addresses the timed GPU steps wrote), the reference's addresses for the
+    sample are compared with them item for item. Returns the cpu_baseline object or None."""
     try:
         from oracle import Oracle, RefLib, have_ref
     except Exception:
@@ -110,11 +111,16 @@ def cpu_baseline(msg_h, sig_h, target_s):
         dt = time.perf_counter() - t0
         n = int(min(len(msg_h), max(n0, n0 * target_s / max(dt, 1e-6))))
         t0 = time.perf_counter()
-        _, _, ret = ref.ecrecover_batch_mt(msg_h[:n], sig_h[:n], threads)
+        _, addr_ref, ret = ref.ecrecover_batch_mt(msg_h[:n], sig_h[:n], threads)
         dt = time.perf_counter() - t0
         assert (ret == 1).all()
+        agree = None
+        if gpu_addr is not None:
+            bad = int((addr_ref != gpu_addr[:n]).any(axis=1).sum())
+            agree = {"items": n, "mismatches": bad,
+                     "note": "the timed GPU steps' addresses vs the reference libsecp256k1's, item for item"}
         return {"value": round(n / dt, 1), "unit": "sigs/s", "cores": threads, "kind": "reference",
-                "host": dict(host, threads=threads),
+                "reference_check": agree, "host": dict(host, threads=threads),
                 "ratio_basis": "the GPU/CPU ratio is per granted CPU set of the host (all threads above), "
                                "not per core",
                 "sample": f"first {n} signatures of the same synthetic batch: reference libsecp256k1 ecrecover "
@@ -298,7 +304,9 @@ def run_throughput(c, strong):
     per_gpu_rate = B / (kern_ms / 1e3)  # from HIP events on the launch stream
     cpu = None
     if c.rank == 0 and not a.no_cpu_baseline and c.world == 1 and not strong:
-        cpu = cpu_baseline(msg.cpu().numpy(), sig.cpu().numpy(), a.cpu_seconds)
+        cpu = cpu_baseline(msg.cpu().numpy(), sig.cpu().numpy(), a.cpu_seconds, gpu_addr=addr.cpu().numpy())
+        if cpu and (cpu.get("reference_check") or {}).get("mismatches"):
+            ok = False
     wl = ("configs[3]: 64M-signature batch sharded by index across the GPUs, batch ecrecover + Keccak address"
           if strong else "configs[1]: 1M random-key secp256k1 signatures, batch ecrecover + Keccak address per "
           "MI355X (inputs resident in HBM)")
