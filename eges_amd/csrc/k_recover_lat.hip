@@ -289,7 +289,7 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
     // --- u1 = -z / r, u2 = s / r (main_impl.h:114-117), digits into LDS. A signature whose R
     // fails to lift is recovered from G instead (wave 0); its scalars stay well-defined either way.
     R = sc_select(ok, R, sc_one());
-    const sc rinv = sc_inv_var(R);  // wave-uniform data: variable-time safegcd
+    const sc rinv = sc_inv_row_var(R);  // wave-uniform data: variable-time safegcd, limb-parallel
     const sc u1 = sc_neg(sc_mul(rinv, Z));
     const sc u2 = sc_select(ok, sc_mul(rinv, Sv), sc_one());
     recode_digits(u2, u1, S);
@@ -372,7 +372,7 @@ DEV void verify_lat_body(const VerifyParams& prm) {
   // parse_compact overflow, high s (ecdsa_verify), r or s zero (sig_verify)
   const bool sig_ok = !ovr && !ovs && !sc_is_high(Sv) && !sc_is_zero(R) && !sc_is_zero(Sv);
   if (threadIdx.x >= 64) {  // wave 1
-    const sc sinv = sc_inv_var(sc_select(sig_ok, Sv, sc_one()));
+    const sc sinv = sc_inv_row_var(sc_select(sig_ok, Sv, sc_one()));
     const sc u1 = sc_mul(sinv, Z);
     const sc u2 = sc_select(sig_ok, sc_mul(sinv, R), sc_one());
     recode_digits(u2, u1, S);

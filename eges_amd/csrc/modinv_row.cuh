@@ -20,6 +20,7 @@
 //     on the scalar ALU brings d into [0, M) by exact comparison.
 #include "fr.cuh"
 #include "modinv.cuh"
+#include "sc.cuh"
 
 namespace eges {
 
@@ -122,6 +123,13 @@ DEV void modinv256_row_var(uint32_t out[8], const uint32_t x[8]) {
     }
   }
   s30_to_u256(out, dv);
+}
+
+// r^-1 / s^-1 mod n in the latency kernels (wave-uniform scalar in and out)
+DEV sc sc_inv_row_var(const sc& a) {
+  sc r;
+  modinv256_row_var<ModN>(r.v, a.v);
+  return r;
 }
 
 // Z^-1 in the latency kernel: value replicated over the rows in, same out (row form)
