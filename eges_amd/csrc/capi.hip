@@ -280,7 +280,10 @@ static hipError_t stamp_buf(size_t waves, hipStream_t st) {
 }
 #endif
 
-hipError_t launch_recover_pass(Dev& d, const RecoverParams& p, hipStream_t st) {
+hipError_t launch_recover_pass(Dev& d, const RecoverParams& p0, hipStream_t st) {
+  RecoverParams p = p0;
+  // the wide form (three waves per signature) while the batch leaves SIMDs idle
+  p.wide = p.n <= (uint32_t)env_int("EGES_LAT_WIDE_MAX", 256) ? 1u : 0u;
 #ifdef EGES_PHASE_STAMPS
   if (p.n <= lat_max() || p.raw_sig) {
     hipError_t e = stamp_buf(lat_waves(p.n), st);

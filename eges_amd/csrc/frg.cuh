@@ -103,6 +103,41 @@ DEV fr gejq_zaddu(ger& t, ger& b) {
   return dx;
 }
 
+// General Jacobian addition a + b (add-2007-bl, 11M + 5S in 5 quad levels), both points in the
+// same coordinates, with infinity flags in and out; wave-uniform exceptional cases resolved
+// exactly (a == b doubles, a == -b is infinity). Used once per signature to join the partial
+// sums of the wide latency kernel. In: X m1, Y <= 2, Z <= 2. Out: X, Y m1, Z m2.
+DEV gejr gejq_add(const gejr& a, bool ainf, const gejr& b, bool binf, bool& rinf) {
+  fr Z1Z1, Z2Z2, Y1Z2, Y2Z1;
+  fr_mul4(Z1Z1, Z2Z2, Y1Z2, Y2Z1, a.z, a.z, b.z, b.z, a.y, b.z, b.y, a.z);
+  fr U1, U2, S1, S2;
+  fr_mul4(U1, U2, S1, S2, a.x, Z2Z2, b.x, Z1Z1, Y1Z2, Z2Z2, Y2Z1, Z1Z1);
+  const fr H = fr_normalize_weak(fr_sub<1>(U2, U1));
+  const fr Rd = fr_normalize_weak(fr_sub<1>(S2, S1));
+  const fr H2 = fr_add(H, H), R2 = fr_add(Rd, Rd);  // r = 2 (S2 - S1)
+  fr I, RR, Z1Z2;
+  fr_mul3(I, RR, Z1Z2, H2, H2, R2, R2, a.z, b.z);   // (2H)^2, r^2, Z1 Z2
+  fr J, V, ZH;
+  fr_mul3(J, V, ZH, H, I, U1, I, Z1Z2, H);
+  gejr r;
+  r.x = fr_normalize_weak(fr_sub<2>(RR, fr_add(J, fr_add(V, V))));  // r^2 - J - 2V
+  fr W, SJ;
+  fr_mul2(W, SJ, R2, fr_sub<1>(V, r.x), S1, J);
+  r.y = fr_normalize_weak(fr_sub<2>(W, fr_add(SJ, SJ)));             // r (V - X3) - 2 S1 J
+  r.z = fr_add(ZH, ZH);                                               // 2 Z1 Z2 H
+  rinf = false;
+  if (ainf) {
+    rinf = binf;
+    return b;
+  }
+  if (binf) return a;
+  if (fr_is_zero(H)) {  // same x: a == b or a == -b
+    if (fr_is_zero(Rd)) return gejq_double(a);
+    rinf = true;
+  }
+  return r;
+}
+
 DEV gejr gejr_select(bool c, const gejr& a, const gejr& b) {
   gejr r;
   r.x = fr_select(c, a.x, b.x);

@@ -32,6 +32,9 @@ struct LatLds {
   uint32_t zr[PTAB][16];      // Z ratios while the table is built
   int8_t rdig[2][RWIN];
   gdig_t gdig[2][GWIN];
+  uint32_t part[3][3][16];  // wide kernel: the R, lambda R and G partial sums (X, Y, Z)
+  uint32_t pinf[3];         //   and their infinity flags
+  uint32_t zeta[16];        //   the table's global Z
 };
 
 // signed fixed-window recoding (core.cuh recode) into this row's digit array
@@ -164,6 +167,67 @@ DEV void strauss_wave(gejr& acc, bool& inf, LatLds& S, const uint32_t* gtab, con
   }
 }
 
+// Wide kernel: one GLV half against the R table (j = 0: R, j = 1: lambda R), on the table's
+// isomorphic curve; the same windows and doublings as strauss_wave, without the other terms.
+template <bool CHECKED>
+DEV void strauss_r_part(gejr& acc, bool& inf, const LatLds& S, int j, const fr& beta) {
+  inf = true;
+  acc.x = fr_zero();
+  acc.y = fr_zero();
+  acc.z = fr_zero();
+#pragma unroll 1
+  for (int w = RWIN - 1; w >= 0; --w) {
+    if (w != RWIN - 1) {
+#pragma unroll 1
+      for (int k = 0; k < RBITS; ++k) acc = gejq_double(acc);
+    }
+    const int d = (int)S.rdig[j][w];
+    const int a = d < 0 ? -d : d;
+    ger p = lds_pt(S.tab[a > 0 ? a - 1 : 0]);
+    if (j == 1) p.x = fr_mul(p.x, beta);
+    add_r<CHECKED>(acc, inf, ger_neg_if(p, d < 0), d != 0);
+  }
+}
+// Wide kernel: u_g G on the true curve from the two 20-bit-window tables (G, 2^128 G), Horner
+// order: 20 doublings between windows (the joint loop's GSTEP R windows).
+template <bool CHECKED>
+DEV void strauss_g_part(gejr& acc, bool& inf, const LatLds& S, const uint32_t* gtab) {
+  inf = true;
+  acc.x = fr_zero();
+  acc.y = fr_zero();
+  acc.z = fr_zero();
+#pragma unroll 1
+  for (int w = GWIN - 1; w >= 0; --w) {
+    if (w != GWIN - 1) {
+#pragma unroll 1
+      for (int k = 0; k < GBITS; ++k) acc = gejq_double(acc);
+    }
+#pragma unroll 1
+    for (int t = 0; t < 2; ++t) {
+      const int d = (int)S.gdig[t][w];
+      const int a = d < 0 ? -d : d;
+      const ger p = gtab_pt(gtab + ((size_t)t * GTAB + (a > 0 ? a - 1 : 0)) * PT_WORDS);
+      add_r<CHECKED>(acc, inf, ger_neg_if(p, d < 0), d != 0);
+    }
+  }
+}
+DEV void put_part(LatLds& S, int k, const gejr& a, bool inf) {
+  const uint32_t L = row_lane();
+  S.part[k][0][L] = a.x.v;
+  S.part[k][1][L] = a.y.v;
+  S.part[k][2][L] = a.z.v;
+  if (lane_id() == 0) S.pinf[k] = inf ? 1u : 0u;
+}
+DEV gejr get_part(const LatLds& S, int k, bool& inf) {
+  const uint32_t L = row_lane();
+  gejr a;
+  a.x.v = S.part[k][0][L];
+  a.y.v = S.part[k][1][L];
+  a.z.v = S.part[k][2][L];
+  inf = S.pinf[k] != 0;
+  return a;
+}
+
 // Q = u_r * P + u_g * G for this wave's signature (core.cuh ecmult_core, quad form)
 // GLV split of u_r and signed windows of both scalars (core.cuh ecmult_core's digits)
 DEV void recode_digits(const sc& u_r, const sc& u_g, LatLds& S) {
@@ -187,9 +251,8 @@ DEV void recode_digits(const sc& u_r, const sc& u_g, LatLds& S) {
 
 // Q = u_r * P + u_g * G for this workgroup's signature (core.cuh ecmult_core, quad form); the
 // digits come from wave 1 (recode_digits), the barrier below is where wave 0 picks them up.
-template <class ST>
-DEV void ecmult_wave(gejr& acc, bool& inf, const ger& P, const uint32_t* gtab, LatLds& S, const fr& beta, ST* st) {
-  // table {1..PTAB} * P on one global Z (co-Z additions, backward rescale; core.cuh)
+// table {1..PTAB} * P on one global Z (co-Z additions, backward rescale; core.cuh); returns zeta
+DEV fr build_table_wave(const ger& P, LatLds& S) {
   fr zeta;
   {
     const uint32_t L = row_lane();
@@ -230,6 +293,12 @@ DEV void ecmult_wave(gejr& acc, bool& inf, const ger& P, const uint32_t* gtab, L
     }
     zeta = rho;  // rho_0 = Z_PTAB / Z_1 with Z_1 = 1
   }
+  return zeta;
+}
+
+template <class ST>
+DEV void ecmult_wave(gejr& acc, bool& inf, const ger& P, const uint32_t* gtab, LatLds& S, const fr& beta, ST* st) {
+  const fr zeta = build_table_wave(P, S);
   st->mark(3);
   __syncthreads();  // wave 1's digits
   st->mark(1);
@@ -241,7 +310,12 @@ DEV void ecmult_wave(gejr& acc, bool& inf, const ger& P, const uint32_t* gtab, L
 
 // Phase marks of wave 0 (diagnostic build only): 0 parse + lift, 3 table, 1 wait for wave 1's
 // r^-1 / u1 / u2 / digits, 4 Strauss, 5 Z^-1 + affine, 6 Keccak + stores.
-template <class ST>
+// WIDE (small batches, one workgroup of three waves per signature): wave 0 lifts R, builds the
+// table and sums the R half; wave 1 does the scalar work, then the lambda R half; wave 2 the
+// u1 G part (Horner over the 20-bit windows). Wave 0 joins the three partial sums with two
+// general additions. Each wave's doubling chain is its own, so the critical path loses the
+// other two terms' additions (~40 % of the joint loop's additions).
+template <class ST, bool WIDE>
 DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   __shared__ LatLds S;
   ST st_;
@@ -284,8 +358,8 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
       c >>= 32;
     }
   }
-  const bool wave1 = threadIdx.x >= 64;
-  if (wave1) {
+  const uint32_t wv = threadIdx.x >> 6;
+  if (wv == 1) {
     // --- u1 = -z / r, u2 = s / r (main_impl.h:114-117), digits into LDS. A signature whose R
     // fails to lift is recovered from G instead (wave 0); its scalars stay well-defined either way.
     R = sc_select(ok, R, sc_one());
@@ -293,7 +367,26 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
     const sc u1 = sc_neg(sc_mul(rinv, Z));
     const sc u2 = sc_select(ok, sc_mul(rinv, Sv), sc_one());
     recode_digits(u2, u1, S);
+    __syncthreads();  // digits ready (and, WIDE, the table)
+    if constexpr (WIDE) {
+      const fr beta = fe_to_fr(fe_const(FE_BETA));
+      gejr A;
+      bool ainf;
+      strauss_r_part<false>(A, ainf, S, 1, beta);
+      if (__any(!ainf && fr_is_zero(A.z))) strauss_r_part<true>(A, ainf, S, 1, beta);
+      put_part(S, 1, A, ainf);
+      __syncthreads();  // partial sums ready
+    }
+    return;
+  }
+  if (WIDE && wv == 2) {
     __syncthreads();  // digits ready
+    gejr A;
+    bool ainf;
+    strauss_g_part<false>(A, ainf, S, prm.gtab);
+    if (__any(!ainf && fr_is_zero(A.z))) strauss_g_part<true>(A, ainf, S, prm.gtab);
+    put_part(S, 2, A, ainf);
+    __syncthreads();  // partial sums ready
     return;
   }
   ger Rp;
@@ -307,7 +400,26 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   const fr beta = fe_to_fr(fe_const(FE_BETA));
   gejr Q;
   bool qinf;
-  ecmult_wave(Q, qinf, Rp, prm.gtab, S, beta, st);
+  if constexpr (WIDE) {
+    const fr zeta = build_table_wave(Rp, S);
+    st->mark(3);
+    __syncthreads();  // digits ready; the table is wave 1's too
+    st->mark(1);
+    gejr A;
+    bool ainf;
+    strauss_r_part<false>(A, ainf, S, 0, beta);
+    if (__any(!ainf && fr_is_zero(A.z))) strauss_r_part<true>(A, ainf, S, 0, beta);
+    __syncthreads();  // partial sums ready
+    bool linf, ginf, qi;
+    const gejr Lp = get_part(S, 1, linf);
+    const gejr Gp = get_part(S, 2, ginf);
+    Q = gejq_add(A, ainf, Lp, linf, qi);  // on the table's isomorphic curve
+    Q.z = fr_mul(Q.z, zeta);              // the true curve
+    Q = gejq_add(Q, qi, Gp, ginf, qinf);
+    st->mark(4);
+  } else {
+    ecmult_wave(Q, qinf, Rp, prm.gtab, S, beta, st);
+  }
   ok = ok && !qinf;  // main_impl.h:120
   // --- affine, serialize, address
   const fr zq = fr_select(ok, Q.z, fr_one());
@@ -441,23 +553,33 @@ hipError_t launch_verify_lat(const VerifyParams& p, hipStream_t st) {
   return hipGetLastError();
 }
 
+constexpr int LAT_WG_WIDE = 192;
+
 __global__ void __launch_bounds__(LAT_WG) recover_lat_kernel(RecoverParams prm) {
-  recover_lat_body<NoStamp>(prm, nullptr);
+  recover_lat_body<NoStamp, false>(prm, nullptr);
+}
+__global__ void __launch_bounds__(LAT_WG_WIDE) recover_lat_wide_kernel(RecoverParams prm) {
+  recover_lat_body<NoStamp, true>(prm, nullptr);
 }
 
 hipError_t launch_recover_lat(const RecoverParams& p, hipStream_t st) {
   if (p.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(recover_lat_kernel, dim3(p.n), dim3(LAT_WG), 0, st, p);
+  if (p.wide) hipLaunchKernelGGL(recover_lat_wide_kernel, dim3(p.n), dim3(LAT_WG_WIDE), 0, st, p);
+  else hipLaunchKernelGGL(recover_lat_kernel, dim3(p.n), dim3(LAT_WG), 0, st, p);
   return hipGetLastError();
 }
 
 #ifdef EGES_PHASE_STAMPS
 __global__ void __launch_bounds__(LAT_WG) recover_lat_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
-  recover_lat_body<Stamper>(prm, stamps);
+  recover_lat_body<Stamper, false>(prm, stamps);
+}
+__global__ void __launch_bounds__(LAT_WG_WIDE) recover_lat_wide_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
+  recover_lat_body<Stamper, true>(prm, stamps);
 }
 hipError_t launch_recover_lat_stamped(const RecoverParams& p, hipStream_t st, uint64_t* stamps) {
   if (p.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(recover_lat_kernel_stamped, dim3(p.n), dim3(LAT_WG), 0, st, p, stamps);
+  if (p.wide) hipLaunchKernelGGL(recover_lat_wide_kernel_stamped, dim3(p.n), dim3(LAT_WG_WIDE), 0, st, p, stamps);
+  else hipLaunchKernelGGL(recover_lat_kernel_stamped, dim3(p.n), dim3(LAT_WG), 0, st, p, stamps);
   return hipGetLastError();
 }
 size_t lat_waves(uint32_t n) { return n; }

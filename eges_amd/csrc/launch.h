@@ -36,6 +36,8 @@ struct RecoverParams {
   // (prep_ecrecover_kernel fused away for small ecrecover calls)
   const uint8_t* raw_msg = nullptr;
   const uint8_t* raw_sig = nullptr;
+  // latency kernel only: three waves per signature (R / lambda R / G partial sums in parallel)
+  uint32_t wide = 0;
 };
 
 struct VerifyParams {

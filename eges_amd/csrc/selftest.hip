@@ -290,6 +290,7 @@ extern "C" double eges_opbench(int op, int reps) {
 // ---------------------------------------------------------------- row-form field (fr.cuh)
 // One item per 16-lane row; canonical 256-bit words in and out, as eges_selftest.
 #include "fr.cuh"
+#include "frg.cuh"
 #include "modinv_row.cuh"
 namespace eges {
 enum : int {
@@ -303,6 +304,7 @@ enum : int {
   FR_QUAD = 7,     // fr_mul4 (a*b, b*c, c*a, a*a in one pass): out = (ab + 2bc + 3ca) * a^2
   FR_QUAD2 = 8,    // fr_mul2 (a*b, c*c): out = ab + 2c^2
   FR_INV = 9,      // fr_inv_var (row-parallel safegcd): out = a^-1
+  FR_GADD = 10,    // gejq_add of lift(a, even) on Z = c and lift(b, parity of c) on Z = c^2: x of the sum
 };
 __global__ void fr_selftest_kernel(int op, uint32_t n, const uint32_t* A, const uint32_t* B, const uint32_t* C,
                                    uint32_t* out) {
@@ -348,6 +350,26 @@ __global__ void fr_selftest_kernel(int op, uint32_t n, const uint32_t* A, const 
       break;
     }
     case FR_INV: r = fr_inv_var(a); break;
+    case FR_GADD: {
+      ger P, Q;
+      ger_set_xo(P, fr_normalize(a), false);
+      const bool odd = (__builtin_amdgcn_readlane(c.v, 0) & 1u) != 0;
+      ger_set_xo(Q, fr_normalize(b), odd);
+      const fr z1 = fr_normalize(c), z2 = fr_sqr(z1);
+      gejr A, B;
+      fr t1, t2, u1, u2;
+      fr_mul2(t1, t2, z1, z1, z2, z2);  // Z1^2, Z2^2
+      fr_mul4(A.x, A.y, B.x, B.y, P.x, t1, P.y, fr_mul(t1, z1), Q.x, t2, Q.y, fr_mul(t2, z2));
+      (void)u1;
+      (void)u2;
+      A.z = z1;
+      B.z = z2;
+      bool rinf;
+      const gejr S = gejq_add(A, false, B, false, rinf);
+      const fr zi = fr_inv_var(S.z);
+      r = rinf ? fr_zero() : fr_mul(S.x, fr_sqr(zi));
+      break;
+    }
     default: r = a;
   }
   const fe o = fe_normalize(fr_to_fe_row(r));

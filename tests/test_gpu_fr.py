@@ -14,7 +14,7 @@ from conftest import ROOT
 from test_gpu_field import P, dec, enc, samples
 
 pytestmark = pytest.mark.gpu
-FR = dict(MUL=0, SQR=1, MULSUB=2, SUB=3, LAZY=4, NORMW=5, CHAIN=6, QUAD=7, QUAD2=8, INV=9)
+FR = dict(MUL=0, SQR=1, MULSUB=2, SUB=3, LAZY=4, NORMW=5, CHAIN=6, QUAD=7, QUAD2=8, INV=9, GADD=10)
 
 
 @pytest.fixture(scope="module")
@@ -59,7 +59,55 @@ def expect(op, a, b, c):
         return pow(a % P, P - 2, P)
 
 
-@pytest.mark.parametrize("op", list(FR))
+def _lift(x, odd):
+    y = pow((x**3 + 7) % P, (P + 1) // 4, P)
+    assert y * y % P == (x**3 + 7) % P
+    return (x, y if (y & 1) == odd else P - y)
+
+
+def _add(p, q):
+    if p is None:
+        return q
+    if q is None:
+        return p
+    if p[0] == q[0]:
+        if (p[1] + q[1]) % P == 0:
+            return None
+        lam = 3 * p[0] * p[0] * pow(2 * p[1], P - 2, P) % P
+    else:
+        lam = (q[1] - p[1]) * pow(q[0] - p[0], P - 2, P) % P
+    x = (lam * lam - p[0] - q[0]) % P
+    return (x, (lam * (p[0] - x) - p[1]) % P)
+
+
+def test_fr_general_add(st):
+    """gejq_add (the wide latency kernel's join) on points with different Z: random sums,
+    a == b (doubling), a == -b (infinity), against big-integer affine addition."""
+    rnd = random.Random(77)
+    xs = []
+    while len(xs) < 300:
+        x = rnd.randrange(1, P)
+        if pow((x**3 + 7) % P, (P - 1) // 2, P) == 1:
+            xs.append(x)
+    a, b, c = [], [], []
+    for i in range(300):
+        xa = xs[i]
+        kind = i % 3
+        xb = xs[(i * 7 + 1) % 300] if kind == 0 else xa
+        zc = rnd.randrange(2, P)
+        if kind == 1:  # b == a: same parity as a's even y
+            zc -= zc & 1
+        if kind == 2:  # b == -a
+            zc |= 1
+        a.append(xa), b.append(xb), c.append(zc)
+    got = run(st, "GADD", a, b, c)
+    for i in range(300):
+        s = _add(_lift(a[i], 0), _lift(b[i], c[i] & 1))
+        exp = 0 if s is None else s[0]
+        assert got[i] == exp, (i, i % 3)
+
+
+@pytest.mark.parametrize("op", [o for o in FR if o != "GADD"])
 def test_fr_ops(st, op):
     rnd = random.Random(1234 + FR[op])
     n = 1500

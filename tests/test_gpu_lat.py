@@ -13,19 +13,53 @@ from conftest import load_golden
 pytestmark = pytest.mark.gpu
 
 
-class lat_max:
+class env_knob:
+    """Sets an engine knob (read per call by capi.hip) for the duration of a with-block."""
+    name = None
+
     def __init__(self, v):
         self.v = v
 
     def __enter__(self):
-        self.old = os.environ.get("EGES_LAT_MAX")
-        os.environ["EGES_LAT_MAX"] = str(self.v)
+        self.old = os.environ.get(self.name)
+        os.environ[self.name] = str(self.v)
 
     def __exit__(self, *a):
         if self.old is None:
-            os.environ.pop("EGES_LAT_MAX", None)
+            os.environ.pop(self.name, None)
         else:
-            os.environ["EGES_LAT_MAX"] = self.old
+            os.environ[self.name] = self.old
+
+
+class lat_max(env_knob):  # batches up to this size take the latency kernels
+    name = "EGES_LAT_MAX"
+
+
+class wide_max(env_knob):  # latency batches up to this size use the wide (3-wave) recover form
+    name = "EGES_LAT_WIDE_MAX"
+
+
+def test_wide_kernel_golden_recover(engine):
+    """Every golden recovery item (all reject classes) through the wide form, the narrow form
+    and the lane-serial kernel: byte for byte the same, and the fixtures'."""
+    g = load_golden("recover.npz")
+    with lat_max(1 << 20), wide_max(1 << 20):
+        pub, addr, st = engine.ecrecover_batch(g["msg"], g["sig"])
+    names = list(g["kind_names"])
+    bad = np.nonzero(st != g["status"])[0]
+    assert bad.size == 0, [(int(i), names[g["kind"][i]], int(st[i]), int(g["status"][i])) for i in bad[:20]]
+    assert np.array_equal(pub, g["pub"])
+    with lat_max(1 << 20), wide_max(0):
+        pub2, addr2, st2 = engine.ecrecover_batch(g["msg"], g["sig"])
+    assert np.array_equal(pub, pub2) and np.array_equal(addr, addr2) and np.array_equal(st, st2)
+    g2 = load_golden("sender.npz")
+    keys = sorted(set(zip(g2["signer"].tolist(), g2["chain_id"].tolist())))
+    for signer, cid in keys:
+        sel = np.nonzero((g2["signer"] == signer) & (g2["chain_id"] == cid))[0]
+        with lat_max(1 << 20), wide_max(1 << 20):
+            a, s_ = engine.sender_batch(g2["sighash"][sel], g2["r"][sel], g2["s"][sel], g2["v"][sel],
+                                        g2["vflags"][sel], signer, cid)
+        assert np.array_equal(s_, g2["status"][sel]) and np.array_equal(a, g2["addr"][sel])
 
 
 def test_lat_kernel_golden_recover(engine):
@@ -106,7 +140,10 @@ def test_lat_kernel_sizes_and_adversarial(engine, n):
         p1, a1, s1 = engine.ecrecover_batch(mh, sig_h)
     with lat_max(0):
         p2, a2, s2 = engine.ecrecover_batch(mh, sig_h)
+    with lat_max(1 << 20), wide_max(1 << 20):
+        p3, a3, s3 = engine.ecrecover_batch(mh, sig_h)
     assert np.array_equal(s1, s2) and np.array_equal(p1, p2) and np.array_equal(a1, a2)
+    assert np.array_equal(s1, s3) and np.array_equal(p1, p3) and np.array_equal(a1, a3)
     assert np.array_equal(s1, workloads.expected_status(kind, "ecrecover"))
     ok = s1 == 0
     assert np.array_equal(a1[ok], exp.cpu().numpy()[ok])
