@@ -450,7 +450,7 @@ int run_verify_dev(Dev& d, const uint8_t* pub, const uint8_t* publen, const uint
     const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
     VerifyParams p{pub + off * 65, publen + off, msg + off * 32, sig + off * 64, m, ok + off, d.gtab, d.ws};
     verify_scratch_bind(p, d.buf, n_pad);
-    if (m <= lat_max()) HIPCHK(launch_verify_lat(p, st));
+    if (m <= lat_max()) HIPCHK(launch_verify_lat(p, p.n <= (uint32_t)env_int("EGES_LAT_WIDE_MAX", 256), st));
     else HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
   }
   return EGES_SUCCESS;
@@ -705,7 +705,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       VerifyParams p{dp, dl, dm, ds, (uint32_t)m, o_st, d.gtab, d.ws};
       verify_scratch_bind(p, B + rg.o_rec, m_pad);
       // small (lane) calls must not touch the device's shared workspace: latency kernel
-      if (small || m <= lat_max()) HIPCHK(launch_verify_lat(p, st));
+      if (small || m <= lat_max()) HIPCHK(launch_verify_lat(p, p.n <= (uint32_t)env_int("EGES_LAT_WIDE_MAX", 256), st));
       else HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
     }
     if (sx != st) HIPCHK(hipEventRecord(ev_k[r], st));

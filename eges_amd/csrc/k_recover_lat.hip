@@ -228,6 +228,22 @@ DEV gejr get_part(const LatLds& S, int k, bool& inf) {
   return a;
 }
 
+// Wide form, waves 1 and 2 after the first barrier (digits and table ready): the lambda R half
+// (wave 1) or the u_g G part (wave 2) into LDS, then the second barrier.
+DEV void wide_part_wave(uint32_t wv, LatLds& S, const uint32_t* gtab) {
+  gejr A;
+  bool ainf;
+  if (wv == 1) {
+    const fr beta = fe_to_fr(fe_const(FE_BETA));
+    strauss_r_part<false>(A, ainf, S, 1, beta);
+    if (__any(!ainf && fr_is_zero(A.z))) strauss_r_part<true>(A, ainf, S, 1, beta);
+  } else {
+    strauss_g_part<false>(A, ainf, S, gtab);
+    if (__any(!ainf && fr_is_zero(A.z))) strauss_g_part<true>(A, ainf, S, gtab);
+  }
+  put_part(S, (int)wv, A, ainf);
+  __syncthreads();  // partial sums ready
+}
 // Q = u_r * P + u_g * G for this wave's signature (core.cuh ecmult_core, quad form)
 // GLV split of u_r and signed windows of both scalars (core.cuh ecmult_core's digits)
 DEV void recode_digits(const sc& u_r, const sc& u_g, LatLds& S) {
@@ -308,6 +324,27 @@ DEV void ecmult_wave(gejr& acc, bool& inf, const ger& P, const uint32_t* gtab, L
   st->mark(4);
 }
 
+// Wide form, wave 0: table, first barrier, the R half, second barrier, join (true curve out).
+template <class ST>
+DEV void ecmult_wide(gejr& Q, bool& qinf, const ger& P, LatLds& S, const fr& beta, ST* st) {
+  const fr zeta = build_table_wave(P, S);
+  st->mark(3);
+  __syncthreads();  // digits ready; the table is wave 1's too
+  st->mark(1);
+  gejr A;
+  bool ainf;
+  strauss_r_part<false>(A, ainf, S, 0, beta);
+  if (__any(!ainf && fr_is_zero(A.z))) strauss_r_part<true>(A, ainf, S, 0, beta);
+  __syncthreads();  // partial sums ready
+  bool linf, ginf, qi;
+  const gejr Lp = get_part(S, 1, linf);
+  const gejr Gp = get_part(S, 2, ginf);
+  Q = gejq_add(A, ainf, Lp, linf, qi);  // on the table's isomorphic curve
+  Q.z = fr_mul(Q.z, zeta);              // the true curve
+  Q = gejq_add(Q, qi, Gp, ginf, qinf);
+  st->mark(4);
+}
+
 // Phase marks of wave 0 (diagnostic build only): 0 parse + lift, 3 table, 1 wait for wave 1's
 // r^-1 / u1 / u2 / digits, 4 Strauss, 5 Z^-1 + affine, 6 Keccak + stores.
 // WIDE (small batches, one workgroup of three waves per signature): wave 0 lifts R, builds the
@@ -368,25 +405,12 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
     const sc u2 = sc_select(ok, sc_mul(rinv, Sv), sc_one());
     recode_digits(u2, u1, S);
     __syncthreads();  // digits ready (and, WIDE, the table)
-    if constexpr (WIDE) {
-      const fr beta = fe_to_fr(fe_const(FE_BETA));
-      gejr A;
-      bool ainf;
-      strauss_r_part<false>(A, ainf, S, 1, beta);
-      if (__any(!ainf && fr_is_zero(A.z))) strauss_r_part<true>(A, ainf, S, 1, beta);
-      put_part(S, 1, A, ainf);
-      __syncthreads();  // partial sums ready
-    }
+    if constexpr (WIDE) wide_part_wave(1, S, prm.gtab);
     return;
   }
   if (WIDE && wv == 2) {
     __syncthreads();  // digits ready
-    gejr A;
-    bool ainf;
-    strauss_g_part<false>(A, ainf, S, prm.gtab);
-    if (__any(!ainf && fr_is_zero(A.z))) strauss_g_part<true>(A, ainf, S, prm.gtab);
-    put_part(S, 2, A, ainf);
-    __syncthreads();  // partial sums ready
+    wide_part_wave(2, S, prm.gtab);
     return;
   }
   ger Rp;
@@ -400,26 +424,8 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   const fr beta = fe_to_fr(fe_const(FE_BETA));
   gejr Q;
   bool qinf;
-  if constexpr (WIDE) {
-    const fr zeta = build_table_wave(Rp, S);
-    st->mark(3);
-    __syncthreads();  // digits ready; the table is wave 1's too
-    st->mark(1);
-    gejr A;
-    bool ainf;
-    strauss_r_part<false>(A, ainf, S, 0, beta);
-    if (__any(!ainf && fr_is_zero(A.z))) strauss_r_part<true>(A, ainf, S, 0, beta);
-    __syncthreads();  // partial sums ready
-    bool linf, ginf, qi;
-    const gejr Lp = get_part(S, 1, linf);
-    const gejr Gp = get_part(S, 2, ginf);
-    Q = gejq_add(A, ainf, Lp, linf, qi);  // on the table's isomorphic curve
-    Q.z = fr_mul(Q.z, zeta);              // the true curve
-    Q = gejq_add(Q, qi, Gp, ginf, qinf);
-    st->mark(4);
-  } else {
-    ecmult_wave(Q, qinf, Rp, prm.gtab, S, beta, st);
-  }
+  if constexpr (WIDE) ecmult_wide(Q, qinf, Rp, S, beta, st);
+  else ecmult_wave(Q, qinf, Rp, prm.gtab, S, beta, st);
   ok = ok && !qinf;  // main_impl.h:120
   // --- affine, serialize, address
   const fr zq = fr_select(ok, Q.z, fr_one());
@@ -469,6 +475,7 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
 // (variable-time safegcd), u1 = z/s, u2 = r/s and the digits while wave 0 parses the public key
 // (the square root for 33-byte keys, the curve equation for 65-byte ones); then Q = u2 P + u1 G
 // and x(Q) == r checked projectively (r Z^2 == X), no field inversion.
+template <bool WIDE>
 DEV void verify_lat_body(const VerifyParams& prm) {
   __shared__ LatLds S;
   NoStamp st_;
@@ -483,12 +490,18 @@ DEV void verify_lat_body(const VerifyParams& prm) {
   const sc Z = sc_from_limbs(l, ovz);  // the message reduced mod n
   // parse_compact overflow, high s (ecdsa_verify), r or s zero (sig_verify)
   const bool sig_ok = !ovr && !ovs && !sc_is_high(Sv) && !sc_is_zero(R) && !sc_is_zero(Sv);
-  if (threadIdx.x >= 64) {  // wave 1
+  if ((threadIdx.x >> 6) == 1) {  // wave 1
     const sc sinv = sc_inv_row_var(sc_select(sig_ok, Sv, sc_one()));
     const sc u1 = sc_mul(sinv, Z);
     const sc u2 = sc_select(sig_ok, sc_mul(sinv, R), sc_one());
     recode_digits(u2, u1, S);
+    __syncthreads();  // digits ready (and, WIDE, the table)
+    if constexpr (WIDE) wide_part_wave(1, S, prm.gtab);
+    return;
+  }
+  if (WIDE && threadIdx.x >= 128) {
     __syncthreads();  // digits ready
+    wide_part_wave(2, S, prm.gtab);
     return;
   }
   // --- public key (eckey_impl.h:17-34)
@@ -526,7 +539,8 @@ DEV void verify_lat_body(const VerifyParams& prm) {
   const fr beta = fe_to_fr(fe_const(FE_BETA));
   gejr Q;
   bool qinf;
-  ecmult_wave(Q, qinf, P, prm.gtab, S, beta, &st_);
+  if constexpr (WIDE) ecmult_wide(Q, qinf, P, S, beta, &st_);
+  else ecmult_wave(Q, qinf, P, prm.gtab, S, beta, &st_);
   ok = ok && !qinf;
   // x(Q) mod n == r  <=>  r Z^2 == X  or  (r < p - n and (r + n) Z^2 == X)  (ecdsa_impl.h:246-270)
   const fr z2 = fr_sqr(Q.z);
@@ -545,15 +559,17 @@ DEV void verify_lat_body(const VerifyParams& prm) {
   if (lane_id() == 0) prm.ok[idx] = (ok && eq) ? 1 : 0;
 }
 
-__global__ void __launch_bounds__(LAT_WG) verify_lat_kernel(VerifyParams prm) { verify_lat_body(prm); }
+constexpr int LAT_WG_WIDE = 192;
 
-hipError_t launch_verify_lat(const VerifyParams& p, hipStream_t st) {
+__global__ void __launch_bounds__(LAT_WG) verify_lat_kernel(VerifyParams prm) { verify_lat_body<false>(prm); }
+__global__ void __launch_bounds__(LAT_WG_WIDE) verify_lat_wide_kernel(VerifyParams prm) { verify_lat_body<true>(prm); }
+
+hipError_t launch_verify_lat(const VerifyParams& p, bool wide, hipStream_t st) {
   if (p.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(verify_lat_kernel, dim3(p.n), dim3(LAT_WG), 0, st, p);
+  if (wide) hipLaunchKernelGGL(verify_lat_wide_kernel, dim3(p.n), dim3(LAT_WG_WIDE), 0, st, p);
+  else hipLaunchKernelGGL(verify_lat_kernel, dim3(p.n), dim3(LAT_WG), 0, st, p);
   return hipGetLastError();
 }
-
-constexpr int LAT_WG_WIDE = 192;
 
 __global__ void __launch_bounds__(LAT_WG) recover_lat_kernel(RecoverParams prm) {
   recover_lat_body<NoStamp, false>(prm, nullptr);

@@ -98,8 +98,9 @@ hipError_t launch_recover(const RecoverParams& p, int max_blocks, int ws_blocks,
 // Same inputs (prep records) and outputs as launch_recover; no workspace.
 hipError_t launch_recover_lat(const RecoverParams& p, hipStream_t st);
 hipError_t launch_verify(const VerifyParams& p, int max_blocks, int ws_blocks, hipStream_t st);
-// one item per 128-thread workgroup (k_recover_lat.hip); uses pub/publen/msg/sig/n/ok/gtab only
-hipError_t launch_verify_lat(const VerifyParams& p, hipStream_t st);
+// one item per 128-thread workgroup (k_recover_lat.hip; wide: 192 threads, three partial sums);
+// uses pub/publen/msg/sig/n/ok/gtab only
+hipError_t launch_verify_lat(const VerifyParams& p, bool wide, hipStream_t st);
 // Blocks the lane-serial kernels may need for a pass of n signatures at a resident grid of
 // max_blocks (grid_for_lane_serial: more than resident when n > max_blocks * WG * MAX_SLOTS).
 int lane_serial_grid(uint32_t n, int max_blocks);

@@ -98,6 +98,9 @@ def test_lat_verify_golden(engine):
     with lat_max(0):
         ok2 = engine.verify_batch(g["pub"], g["publen"], g["msg"], g["sig"])
     assert np.array_equal(ok, ok2)
+    with lat_max(1 << 20), wide_max(1 << 20):
+        ok3 = engine.verify_batch(g["pub"], g["publen"], g["msg"], g["sig"])
+    assert np.array_equal(ok, ok3)
 
 
 @pytest.mark.parametrize("n", [1, 3, 64, 1000])
@@ -122,7 +125,9 @@ def test_lat_verify_sizes(engine, n):
         ok = engine.verify_batch(pk, lens, mm, sh[:, :64])
     with lat_max(0):
         ok2 = engine.verify_batch(pk, lens, mm, sh[:, :64])
-    assert np.array_equal(ok, ok2)
+    with lat_max(1 << 20), wide_max(1 << 20):
+        ok3 = engine.verify_batch(pk, lens, mm, sh[:, :64])
+    assert np.array_equal(ok, ok2) and np.array_equal(ok, ok3)
     assert ok.tolist() == [0 if i % 3 == 0 else 1 for i in range(n)]
 
 
