@@ -35,6 +35,7 @@ struct LatLds {
   uint32_t part[3][3][16];  // wide kernel: the R, lambda R and G partial sums (X, Y, Z)
   uint32_t pinf[3];         //   and their infinity flags
   uint32_t zeta[16];        //   the table's global Z
+  uint32_t btab[PTAB][16];  //   beta x of the table entries (wave 1's lambda R half)
 };
 
 // signed fixed-window recoding (core.cuh recode) into this row's digit array
@@ -183,8 +184,9 @@ DEV void strauss_r_part(gejr& acc, bool& inf, const LatLds& S, int j, const fr& 
     }
     const int d = (int)S.rdig[j][w];
     const int a = d < 0 ? -d : d;
-    ger p = lds_pt(S.tab[a > 0 ? a - 1 : 0]);
-    if (j == 1) p.x = fr_mul(p.x, beta);
+    const int e = a > 0 ? a - 1 : 0;
+    ger p = lds_pt(S.tab[e]);
+    if (j == 1) p.x.v = S.btab[e][row_lane()];  // lambda (x, y) = (beta x, y)
     add_r<CHECKED>(acc, inf, ger_neg_if(p, d < 0), d != 0);
   }
 }
@@ -235,6 +237,18 @@ DEV void wide_part_wave(uint32_t wv, LatLds& S, const uint32_t* gtab) {
   bool ainf;
   if (wv == 1) {
     const fr beta = fe_to_fr(fe_const(FE_BETA));
+    // beta x of every table entry, four per quad step (wave 1 alone reads them)
+#pragma unroll 1
+    for (int i = 0; i < PTAB; i += 4) {
+      fr b0, b1, b2, b3;
+      fr_mul4(b0, b1, b2, b3, lds_pt(S.tab[i]).x, beta, lds_pt(S.tab[i + 1]).x, beta, lds_pt(S.tab[i + 2]).x, beta,
+              lds_pt(S.tab[i + 3]).x, beta);
+      const uint32_t L = row_lane();
+      S.btab[i][L] = b0.v;
+      S.btab[i + 1][L] = b1.v;
+      S.btab[i + 2][L] = b2.v;
+      S.btab[i + 3][L] = b3.v;
+    }
     strauss_r_part<false>(A, ainf, S, 1, beta);
     if (__any(!ainf && fr_is_zero(A.z))) strauss_r_part<true>(A, ainf, S, 1, beta);
   } else {
