@@ -17,4 +17,6 @@ timeout -k 10 200 python bench.py --config c3raw > gpurun_out/bench_c3raw.json 2
 timeout -k 10 200 python bench.py --config c1 > gpurun_out/bench_c1.json 2> gpurun_out/bench_c1.err
 timeout -k 10 200 tools/single_bench 8 2000 > gpurun_out/single.json 2> gpurun_out/single.err
 timeout -k 10 200 tools/single_bench 16 2000 > gpurun_out/single16.json 2> gpurun_out/single16.err
+ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 timeout -k 10 300 tools/asan/sanitize_host 5000 > gpurun_out/sanitize_gpu.log 2>&1
 cat gpurun_out/bench_c3raw.json gpurun_out/bench_c1.json gpurun_out/single.json gpurun_out/single16.json
+tail -1 gpurun_out/sanitize_gpu.log
