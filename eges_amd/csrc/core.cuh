@@ -47,6 +47,10 @@ constexpr int GBITS = EGES_GBITS;                 // multiple of RBITS: aligned 
 constexpr int GSTEP = GBITS / RBITS;              // R windows per G window
 constexpr int GWIN = (RWIN + GSTEP - 1) / GSTEP;  // G windows
 constexpr int GTAB = 1 << (GBITS - 1);
+// Comb table of the latency kernels (after the two GTAB tables in the same allocation):
+// entry (k, i) = (i + 1) 2^(16 k) G, k < 16, i < 2^16 - 1, so u G = sum_k T_k[digit_k - 1] over
+// the 16 unsigned 16-bit digits of u: 16 additions and no doublings.
+constexpr int CBITS = 16, CWIN = 16, CTAB = (1 << CBITS) - 1;
 static_assert(GBITS % RBITS == 0 && GWIN * GBITS >= 129, "G windows must cover a 128-bit half + carry");
 using gdig_t = std::conditional_t<(GBITS > 16), int32_t, int16_t>;
 

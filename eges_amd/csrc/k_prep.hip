@@ -30,6 +30,34 @@ __global__ void __launch_bounds__(256) init_gtab_kernel(uint32_t* gtab) {
   store_pt(gtab + (size_t)i * PT_WORDS, a);
 }
 
+// Comb table (core.cuh CBITS / CWIN / CTAB): gcomb[k][i] = (i + 1) 2^(16 k) G, affine; one
+// thread per entry, double-and-add then 16 k doublings (never exceptional: multiples of G
+// below n), once per device.
+__global__ void __launch_bounds__(256) init_gcomb_kernel(uint32_t* gcomb) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= CWIN * CTAB) return;
+  const int k = t / CTAB;
+  const uint32_t m = (uint32_t)(t % CTAB) + 1;
+  ge g;
+  g.x = fe_const(GEN_X);
+  g.y = fe_const(GEN_Y);
+  gej acc = gej_from_ge(g);
+  for (int b = 30 - __clz(m); b >= 0; --b) {
+    acc = gej_double(acc);
+    if ((m >> b) & 1u) {
+      bool hz, rz;
+      acc = gej_add_ge(acc, g, hz, rz);
+    }
+  }
+  for (int d = 0; d < CBITS * k; ++d) acc = gej_double(acc);
+  const fe zi = fe_inv(acc.z);
+  const fe zi2 = fe_sqr(zi);
+  ge a;
+  a.x = fe_normalize(fe_mul(acc.x, zi2));
+  a.y = fe_normalize(fe_mul(acc.y, fe_mul(zi2, zi)));
+  store_pt(gcomb + (size_t)t * PT_WORDS, a);
+}
+
 // ------------------------------------------------------------------ prep kernels
 // Record layout consumed by the recover kernel (SoA, stride n_pad words):
 //   z[8], r[8], s[8] little-endian limbs of the raw 256-bit values; meta = recid | status << 8
@@ -201,6 +229,8 @@ __global__ void __launch_bounds__(256) prep_precompile_kernel(const uint8_t* __r
 
 // ------------------------------------------------------------------ launchers
 hipError_t launch_init_gtab(uint32_t* gtab, hipStream_t st) {
+  hipLaunchKernelGGL(init_gcomb_kernel, dim3((CWIN * CTAB + 255) / 256), dim3(256), 0, st,
+                     gtab + (size_t)2 * GTAB * PT_WORDS);
   hipLaunchKernelGGL(init_gtab_kernel, dim3((2 * GTAB + 255) / 256), dim3(256), 0, st, gtab);
   return hipGetLastError();
 }
@@ -226,7 +256,7 @@ hipError_t launch_prep_precompile(const uint8_t* input, const uint32_t* inlen, u
 }
 
 size_t ws_bytes_per_block() { return WS_WORDS * sizeof(uint32_t); }
-size_t gtab_bytes() { return (size_t)2 * GTAB * PT_WORDS * sizeof(uint32_t); }
+size_t gtab_bytes() { return ((size_t)2 * GTAB + (size_t)CWIN * CTAB) * PT_WORDS * sizeof(uint32_t); }
 int threads_per_block() { return WG; }
 
 }  // namespace eges

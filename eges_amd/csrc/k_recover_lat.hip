@@ -8,12 +8,14 @@
 // compute the independent products of each formula level together (quad steps, frg.cuh), so
 // a 1000-signature block spreads over 1000 waves and each signature's chain is ~4x shorter.
 //
-//   parse, x = r (+n), R = lift_x(x) ...... row form (fr_sqrt), failures carry G and r = 1
-//   r^-1, u1 = -z/r, u2 = s/r, GLV split . wave 1, lane-serial code, concurrent with the lift
-//   table {1..16}R on one global Z ....... co-Z dblu / zaddu + backward rescale (as core.cuh)
-//   Strauss over 26 windows ............. unchecked adds, exact redo if the
-//                                          accumulator was poisoned (Z == 0 and not infinity)
-//   Z^-1 (safegcd: divsteps on the scalar ALU, matrix updates limb-parallel), affine,
+//   parse, x = r (+n), c = x^3 + 7 ........ R' = (c x, c^2): R's image on E': y^2 = x^3 + 7 c^3
+//                                            (no square root on wave 0's path)
+//   r^-1, u1 = -z/r, u2 = s/r, GLV split .. wave 1 (scalar ALU + limb-parallel safegcd)
+//   table {1..16}R' on one global Z ...... co-Z dblu / zaddu + backward rescale (as core.cuh)
+//   Strauss over 26 windows (u2 R') ...... unchecked adds, exact redo if the accumulator was
+//                                            poisoned (Z == 0 and not infinity)
+//   y = sqrt(c), u1 G by a comb table .... the helper wave, beside the Strauss loop
+//   back to E: (X, Y, Z) -> (X, Y, Z y); + u1 G; Z^-1 (limb-parallel safegcd), affine,
 //   serialize, Keccak address (scalar ALU); lane 0 stores.
 #include <type_traits>
 
@@ -23,19 +25,19 @@
 
 namespace eges {
 
-// One signature per workgroup of two waves: wave 0 lifts R (square root) and builds the table
-// while wave 1 computes r^-1 (safegcd), u1, u2 and the window digits; they meet at one barrier.
+// One signature per workgroup of two waves (narrow form; wide: three, LAT_WG_WIDE).
 constexpr int LAT_WG = 128;
 
 struct LatLds {
-  uint32_t tab[PTAB][2][16];  // {1..16} * R (x, y), row form (all four rows read the same words)
+  uint32_t tab[PTAB][2][16];  // {1..16} * R' (x, y), row form (all four rows read the same words)
   uint32_t zr[PTAB][16];      // Z ratios while the table is built
-  int8_t rdig[2][RWIN];
-  gdig_t gdig[2][GWIN];
-  uint32_t part[3][3][16];  // wide kernel: the R, lambda R and G partial sums (X, Y, Z)
-  uint32_t pinf[3];         //   and their infinity flags
-  uint32_t zeta[16];        //   the table's global Z
-  uint32_t btab[PTAB][16];  //   beta x of the table entries (wave 1's lambda R half)
+  uint32_t btab[PTAB][16];    // beta x of the table entries (the lambda R' additions)
+  int8_t rdig[2][RWIN];       // R / lambda R window digits
+  uint16_t cdig[CWIN];        // comb digits of u_g
+  uint32_t part[3][3][16];    // partial sums (X, Y, Z): [1] lambda R half (wide), [2] u_g G
+  uint32_t pinf[3];           //   and their infinity flags
+  uint32_t ylift[16];         // y of R (the square root, from the helper wave)
+  uint32_t yok;
 };
 
 // signed fixed-window recoding (core.cuh recode) into this row's digit array
@@ -110,177 +112,18 @@ DEV void add_r(gejr& acc, bool& inf, const ger& p, bool use) {
   acc = gejr_select(use, s, acc);
   inf = use ? (inf ? false : to_inf) : inf;
 }
-// acc (on the table's isomorphic curve, global Z = zeta) += p (true curve)
-template <bool CHECKED>
-DEV void add_r_zinv(gejr& acc, bool& inf, const ger& p, bool use, const fr& zeta) {
-  gejr s;
-  bool to_inf = false;
-  if (CHECKED) {
-    bool hz, rz;
-    s = gejq_add_ge_t<ADD_ZINV, true>(acc, p, &zeta, hz, rz);
-    const bool exc = use && !inf && hz;
-    if (__any(exc)) s = gejr_select(exc && rz, gejq_double(acc), s);
-    to_inf = exc && !rz;
-  } else {
-    bool h, r;
-    s = gejq_add_ge_t<ADD_ZINV, false>(acc, p, &zeta, h, r);
-  }
-  if (__any(use && inf)) {  // acc = p mapped onto the isomorphic curve: (x zeta^2, y zeta^3, 1)
-    const fr z2 = fr_sqr(zeta);
-    const fr z3 = fr_mul(z2, zeta);
-    gejr pj;
-    pj.x = fr_mul(p.x, z2);
-    pj.y = fr_mul(p.y, z3);
-    pj.z = fr_one();
-    s = gejr_select(inf, pj, s);
-  }
-  acc = gejr_select(use, s, acc);
-  inf = use ? (inf ? false : to_inf) : inf;
-}
 
-template <bool CHECKED>
-DEV void strauss_wave(gejr& acc, bool& inf, LatLds& S, const uint32_t* gtab, const fr& zeta, const fr& beta) {
-  inf = true;
-  acc.x = fr_zero();
-  acc.y = fr_zero();
-  acc.z = fr_zero();
-#pragma unroll 1
-  for (int w = RWIN - 1; w >= 0; --w) {
-    if (w != RWIN - 1) {
-#pragma unroll 1
-      for (int k = 0; k < RBITS; ++k) acc = gejq_double(acc);
-    }
-    const int nadd = (w % GSTEP) == 0 ? 4 : 2;
-#pragma unroll 1
-    for (int j = 0; j < nadd; ++j) {
-      const int d = j < 2 ? (int)S.rdig[j][w] : (int)S.gdig[j - 2][w / GSTEP];
-      const int a = d < 0 ? -d : d;
-      const int e = a > 0 ? a - 1 : 0;
-      if (j < 2) {
-        ger p = lds_pt(S.tab[e]);
-        if (j == 1) p.x = fr_mul(p.x, beta);
-        add_r<CHECKED>(acc, inf, ger_neg_if(p, d < 0), d != 0);
-      } else {
-        const ger p = gtab_pt(gtab + ((size_t)(j - 2) * GTAB + e) * PT_WORDS);
-        add_r_zinv<CHECKED>(acc, inf, ger_neg_if(p, d < 0), d != 0, zeta);
-      }
-    }
-  }
-}
-
-// Wide kernel: one GLV half against the R table (j = 0: R, j = 1: lambda R), on the table's
-// isomorphic curve; the same windows and doublings as strauss_wave, without the other terms.
-template <bool CHECKED>
-DEV void strauss_r_part(gejr& acc, bool& inf, const LatLds& S, int j, const fr& beta) {
-  inf = true;
-  acc.x = fr_zero();
-  acc.y = fr_zero();
-  acc.z = fr_zero();
-#pragma unroll 1
-  for (int w = RWIN - 1; w >= 0; --w) {
-    if (w != RWIN - 1) {
-#pragma unroll 1
-      for (int k = 0; k < RBITS; ++k) acc = gejq_double(acc);
-    }
-    const int d = (int)S.rdig[j][w];
-    const int a = d < 0 ? -d : d;
-    const int e = a > 0 ? a - 1 : 0;
-    ger p = lds_pt(S.tab[e]);
-    if (j == 1) p.x.v = S.btab[e][row_lane()];  // lambda (x, y) = (beta x, y)
-    add_r<CHECKED>(acc, inf, ger_neg_if(p, d < 0), d != 0);
-  }
-}
-// Wide kernel: u_g G on the true curve from the two 20-bit-window tables (G, 2^128 G), Horner
-// order: 20 doublings between windows (the joint loop's GSTEP R windows).
-template <bool CHECKED>
-DEV void strauss_g_part(gejr& acc, bool& inf, const LatLds& S, const uint32_t* gtab) {
-  inf = true;
-  acc.x = fr_zero();
-  acc.y = fr_zero();
-  acc.z = fr_zero();
-#pragma unroll 1
-  for (int w = GWIN - 1; w >= 0; --w) {
-    if (w != GWIN - 1) {
-#pragma unroll 1
-      for (int k = 0; k < GBITS; ++k) acc = gejq_double(acc);
-    }
-#pragma unroll 1
-    for (int t = 0; t < 2; ++t) {
-      const int d = (int)S.gdig[t][w];
-      const int a = d < 0 ? -d : d;
-      const ger p = gtab_pt(gtab + ((size_t)t * GTAB + (a > 0 ? a - 1 : 0)) * PT_WORDS);
-      add_r<CHECKED>(acc, inf, ger_neg_if(p, d < 0), d != 0);
-    }
-  }
-}
-DEV void put_part(LatLds& S, int k, const gejr& a, bool inf) {
-  const uint32_t L = row_lane();
-  S.part[k][0][L] = a.x.v;
-  S.part[k][1][L] = a.y.v;
-  S.part[k][2][L] = a.z.v;
-  if (lane_id() == 0) S.pinf[k] = inf ? 1u : 0u;
-}
-DEV gejr get_part(const LatLds& S, int k, bool& inf) {
-  const uint32_t L = row_lane();
-  gejr a;
-  a.x.v = S.part[k][0][L];
-  a.y.v = S.part[k][1][L];
-  a.z.v = S.part[k][2][L];
-  inf = S.pinf[k] != 0;
-  return a;
-}
-
-// Wide form, waves 1 and 2 after the first barrier (digits and table ready): the lambda R half
-// (wave 1) or the u_g G part (wave 2) into LDS, then the second barrier.
-DEV void wide_part_wave(uint32_t wv, LatLds& S, const uint32_t* gtab) {
-  gejr A;
-  bool ainf;
-  if (wv == 1) {
-    const fr beta = fe_to_fr(fe_const(FE_BETA));
-    // beta x of every table entry, four per quad step (wave 1 alone reads them)
-#pragma unroll 1
-    for (int i = 0; i < PTAB; i += 4) {
-      fr b0, b1, b2, b3;
-      fr_mul4(b0, b1, b2, b3, lds_pt(S.tab[i]).x, beta, lds_pt(S.tab[i + 1]).x, beta, lds_pt(S.tab[i + 2]).x, beta,
-              lds_pt(S.tab[i + 3]).x, beta);
-      const uint32_t L = row_lane();
-      S.btab[i][L] = b0.v;
-      S.btab[i + 1][L] = b1.v;
-      S.btab[i + 2][L] = b2.v;
-      S.btab[i + 3][L] = b3.v;
-    }
-    strauss_r_part<false>(A, ainf, S, 1, beta);
-    if (__any(!ainf && fr_is_zero(A.z))) strauss_r_part<true>(A, ainf, S, 1, beta);
-  } else {
-    strauss_g_part<false>(A, ainf, S, gtab);
-    if (__any(!ainf && fr_is_zero(A.z))) strauss_g_part<true>(A, ainf, S, gtab);
-  }
-  put_part(S, (int)wv, A, ainf);
-  __syncthreads();  // partial sums ready
-}
-// Q = u_r * P + u_g * G for this wave's signature (core.cuh ecmult_core, quad form)
-// GLV split of u_r and signed windows of both scalars (core.cuh ecmult_core's digits)
+// GLV split of u_r into signed 5-bit windows (core.cuh ecmult_core's digits), u_g for the comb
 DEV void recode_digits(const sc& u_r, const sc& u_g, LatLds& S) {
   glv_half h1, h2;
   glv_split(h1, h2, u_r);
   recode_row<RBITS, RWIN, int8_t>(h1, S.rdig[0]);
   recode_row<RBITS, RWIN, int8_t>(h2, S.rdig[1]);
-  glv_half g0, g1;
-  g0.neg = false;
-  g1.neg = false;
+  // u_g in unsigned 16-bit digits for the comb (every lane writes the same values)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    g0.mag[i] = u_g.v[i];
-    g1.mag[i] = u_g.v[4 + i];
-  }
-  g0.mag[4] = 0;
-  g1.mag[4] = 0;
-  recode_row<GBITS, GWIN, gdig_t>(g0, S.gdig[0]);
-  recode_row<GBITS, GWIN, gdig_t>(g1, S.gdig[1]);
+  for (int k = 0; k < CWIN; ++k) S.cdig[k] = (uint16_t)(u_g.v[k >> 1] >> (16 * (k & 1)));
 }
 
-// Q = u_r * P + u_g * G for this workgroup's signature (core.cuh ecmult_core, quad form); the
-// digits come from wave 1 (recode_digits), the barrier below is where wave 0 picks them up.
 // table {1..PTAB} * P on one global Z (co-Z additions, backward rescale; core.cuh); returns zeta
 DEV fr build_table_wave(const ger& P, LatLds& S) {
   fr zeta;
@@ -326,46 +169,185 @@ DEV fr build_table_wave(const ger& P, LatLds& S) {
   return zeta;
 }
 
-template <class ST>
-DEV void ecmult_wave(gejr& acc, bool& inf, const ger& P, const uint32_t* gtab, LatLds& S, const fr& beta, ST* st) {
-  const fr zeta = build_table_wave(P, S);
-  st->mark(3);
-  __syncthreads();  // wave 1's digits
-  st->mark(1);
-  strauss_wave<false>(acc, inf, S, gtab, zeta, beta);
-  if (__any(!inf && fr_is_zero(acc.z))) strauss_wave<true>(acc, inf, S, gtab, zeta, beta);
-  acc.z = fr_mul(acc.z, zeta);
-  st->mark(4);
+// ---- Strauss parts. R' = (c x, c^2) lives on E': y^2 = x^3 + 7 c^3 with c = x^3 + 7 (the image
+// of R = (x, y) under the isomorphism (x, y) -> (y^2 x, y^3 y), which needs no square root); the
+// R' table on E''s isomorphic curve with global Z = zeta; the G comb on the true curve.
+
+// Both GLV halves against the R' table in one loop (narrow form): 26 windows of 5 doublings and
+// two additions (R', lambda R' with beta x from btab).
+template <bool CHECKED>
+DEV void strauss_rr(gejr& acc, bool& inf, const LatLds& S) {
+  inf = true;
+  acc.x = fr_zero();
+  acc.y = fr_zero();
+  acc.z = fr_zero();
+#pragma unroll 1
+  for (int w = RWIN - 1; w >= 0; --w) {
+    if (w != RWIN - 1) {
+#pragma unroll 1
+      for (int k = 0; k < RBITS; ++k) acc = gejq_double(acc);
+    }
+#pragma unroll 1
+    for (int j = 0; j < 2; ++j) {
+      const int d = (int)S.rdig[j][w];
+      const int a = d < 0 ? -d : d;
+      const int e = a > 0 ? a - 1 : 0;
+      ger p = lds_pt(S.tab[e]);
+      if (j == 1) p.x.v = S.btab[e][row_lane()];  // lambda (x, y) = (beta x, y)
+      add_r<CHECKED>(acc, inf, ger_neg_if(p, d < 0), d != 0);
+    }
+  }
+}
+// One GLV half (wide form: j = 0 on wave 0, j = 1 on wave 1).
+template <bool CHECKED>
+DEV void strauss_r_part(gejr& acc, bool& inf, const LatLds& S, int j) {
+  inf = true;
+  acc.x = fr_zero();
+  acc.y = fr_zero();
+  acc.z = fr_zero();
+#pragma unroll 1
+  for (int w = RWIN - 1; w >= 0; --w) {
+    if (w != RWIN - 1) {
+#pragma unroll 1
+      for (int k = 0; k < RBITS; ++k) acc = gejq_double(acc);
+    }
+    const int d = (int)S.rdig[j][w];
+    const int a = d < 0 ? -d : d;
+    const int e = a > 0 ? a - 1 : 0;
+    ger p = lds_pt(S.tab[e]);
+    if (j == 1) p.x.v = S.btab[e][row_lane()];
+    add_r<CHECKED>(acc, inf, ger_neg_if(p, d < 0), d != 0);
+  }
+}
+// u_g G from the comb table: one addition per 16-bit digit, no doublings (true curve).
+template <bool CHECKED>
+DEV void strauss_gcomb(gejr& acc, bool& inf, const LatLds& S, const uint32_t* gcomb) {
+  inf = true;
+  acc.x = fr_zero();
+  acc.y = fr_zero();
+  acc.z = fr_zero();
+#pragma unroll 1
+  for (int k = 0; k < CWIN; ++k) {
+    const int d = (int)S.cdig[k];
+    const ger p = gtab_pt(gcomb + ((size_t)k * CTAB + (d > 0 ? d - 1 : 0)) * PT_WORDS);
+    add_r<CHECKED>(acc, inf, p, d != 0);
+  }
+}
+DEV void put_part(LatLds& S, int k, const gejr& a, bool inf) {
+  const uint32_t L = row_lane();
+  S.part[k][0][L] = a.x.v;
+  S.part[k][1][L] = a.y.v;
+  S.part[k][2][L] = a.z.v;
+  if (lane_id() == 0) S.pinf[k] = inf ? 1u : 0u;
+}
+DEV gejr get_part(const LatLds& S, int k, bool& inf) {
+  const uint32_t L = row_lane();
+  gejr a;
+  a.x.v = S.part[k][0][L];
+  a.y.v = S.part[k][1][L];
+  a.z.v = S.part[k][2][L];
+  inf = S.pinf[k] != 0;
+  return a;
+}
+// beta x of the 16 table entries, four per quad step
+DEV void build_btab(LatLds& S) {
+  const fr beta = fe_to_fr(fe_const(FE_BETA));
+  const uint32_t L = row_lane();
+#pragma unroll 1
+  for (int i = 0; i < PTAB; i += 4) {
+    fr b0, b1, b2, b3;
+    fr_mul4(b0, b1, b2, b3, lds_pt(S.tab[i]).x, beta, lds_pt(S.tab[i + 1]).x, beta, lds_pt(S.tab[i + 2]).x, beta,
+            lds_pt(S.tab[i + 3]).x, beta);
+    S.btab[i][L] = b0.v;
+    S.btab[i + 1][L] = b1.v;
+    S.btab[i + 2][L] = b2.v;
+    S.btab[i + 3][L] = b3.v;
+  }
+}
+// c = x^3 + 7 (magnitude 1)
+DEV fr curve_rhs(const fr& x) { return fr_add(fr_mul(fr_sqr(x), x), fr_small(7)); }
+// y with y^2 = c and the requested parity (ge_set_xo_var's root); false for a non-residue
+DEV bool lift_y(fr& y, const fr& c, bool odd) {
+  const bool ok = fr_sqrt(y, c);
+  fe yl = fe_normalize(fr_to_fe(y));
+  const bool flip = ((yl.v[0] & 1u) != 0) != odd;
+  yl = fe_select(flip, fe_normalize(fe_neg<1>(yl)), yl);
+  y = fe_to_fr(yl);
+  return ok;
 }
 
-// Wide form, wave 0: table, first barrier, the R half, second barrier, join (true curve out).
-template <class ST>
-DEV void ecmult_wide(gejr& Q, bool& qinf, const ger& P, LatLds& S, const fr& beta, ST* st) {
-  const fr zeta = build_table_wave(P, S);
+// Helper wave, after the first barrier: the square root (when the point came compressed) and
+// the u_g G comb part into LDS, then the second barrier. Both run beside wave 0's table and
+// Strauss loop instead of ahead of them.
+DEV void helper_wave(LatLds& S, const uint32_t* gcomb, bool need_y, const fr& c, bool odd) {
+  if (need_y) {
+    fr y;
+    const bool ok = lift_y(y, c, odd);
+    S.ylift[row_lane()] = y.v;
+    if (lane_id() == 0) S.yok = ok ? 1u : 0u;
+  }
+  gejr A;
+  bool ainf;
+  strauss_gcomb<false>(A, ainf, S, gcomb);
+  if (__any(!ainf && fr_is_zero(A.z))) strauss_gcomb<true>(A, ainf, S, gcomb);
+  put_part(S, 2, A, ainf);
+  __syncthreads();  // partial sums and y ready
+}
+// Wide form, wave 1 after the first barrier: the lambda R' half.
+DEV void lambda_half_wave(LatLds& S) {
+  build_btab(S);
+  gejr A;
+  bool ainf;
+  strauss_r_part<false>(A, ainf, S, 1);
+  if (__any(!ainf && fr_is_zero(A.z))) strauss_r_part<true>(A, ainf, S, 1);
+  put_part(S, 1, A, ainf);
+  __syncthreads();  // partial sums ready
+}
+
+// Wave 0: u_r * (x, y) + u_g G with y deferred. R' = (c x, c^2) on E', its table, the first
+// barrier (digits), the R' Strauss sum(s), the second barrier (the other parts and y), then
+// back to the true curve: an E' Jacobian point (X, Y, Z) is (X, Y, Z y) on E, and the table's
+// isomorphic curve adds the factor zeta. y comes from LDS (helper wave) or is given.
+template <class ST, bool WIDE>
+DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, const fr& y_given, bool y_in_lds,
+                         LatLds& S, ST* st) {
+  ger Rp;
+  fr_mul2(Rp.x, Rp.y, c, x, c, c);  // (c x, c^2)
+  const fr zeta = build_table_wave(Rp, S);
+  if (!WIDE) build_btab(S);
   st->mark(3);
-  __syncthreads();  // digits ready; the table is wave 1's too
+  __syncthreads();  // digits ready (wide: the table is wave 1's too)
   st->mark(1);
   gejr A;
   bool ainf;
-  strauss_r_part<false>(A, ainf, S, 0, beta);
-  if (__any(!ainf && fr_is_zero(A.z))) strauss_r_part<true>(A, ainf, S, 0, beta);
-  __syncthreads();  // partial sums ready
-  bool linf, ginf, qi;
-  const gejr Lp = get_part(S, 1, linf);
+  if constexpr (WIDE) {
+    strauss_r_part<false>(A, ainf, S, 0);
+    if (__any(!ainf && fr_is_zero(A.z))) strauss_r_part<true>(A, ainf, S, 0);
+  } else {
+    strauss_rr<false>(A, ainf, S);
+    if (__any(!ainf && fr_is_zero(A.z))) strauss_rr<true>(A, ainf, S);
+  }
+  __syncthreads();  // partial sums (and y) ready
+  if constexpr (WIDE) {
+    bool linf;
+    const gejr Lp = get_part(S, 1, linf);
+    A = gejq_add(A, ainf, Lp, linf, ainf);  // both halves on the isomorphic curve of E'
+  }
+  const fr y = y_in_lds ? fr{S.ylift[row_lane()]} : y_given;
+  A.z = fr_mul(A.z, fr_mul(zeta, y));  // the true curve
+  bool ginf;
   const gejr Gp = get_part(S, 2, ginf);
-  Q = gejq_add(A, ainf, Lp, linf, qi);  // on the table's isomorphic curve
-  Q.z = fr_mul(Q.z, zeta);              // the true curve
-  Q = gejq_add(Q, qi, Gp, ginf, qinf);
+  Q = gejq_add(A, ainf, Gp, ginf, qinf);
   st->mark(4);
 }
 
-// Phase marks of wave 0 (diagnostic build only): 0 parse + lift, 3 table, 1 wait for wave 1's
-// r^-1 / u1 / u2 / digits, 4 Strauss, 5 Z^-1 + affine, 6 Keccak + stores.
-// WIDE (small batches, one workgroup of three waves per signature): wave 0 lifts R, builds the
-// table and sums the R half; wave 1 does the scalar work, then the lambda R half; wave 2 the
-// u1 G part (Horner over the 20-bit windows). Wave 0 joins the three partial sums with two
-// general additions. Each wave's doubling chain is its own, so the critical path loses the
-// other two terms' additions (~40 % of the joint loop's additions).
+// Phase marks of wave 0 (diagnostic build only): 0 parse + x, c, 3 table, 1 wait for wave 1's
+// r^-1 / u1 / u2 / digits, 4 Strauss + join (including the wait for the other parts and y),
+// 5 Z^-1 + affine, 6 Keccak + stores.
+// Narrow form (two waves): wave 0 table + both GLV halves; wave 1 the scalar work, then the
+// square root and the u1 G comb part. WIDE (small batches, three waves): wave 1 takes the
+// lambda R' half after its scalar work, wave 2 the square root and the comb part; wave 0 joins
+// the three partial sums with two general additions.
 template <class ST, bool WIDE>
 DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   __shared__ LatLds S;
@@ -409,38 +391,37 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
       c >>= 32;
     }
   }
+  // R's x; signatures that fail the parse carry the generator's x (even y), so every later step
+  // stays well-defined. c = x^3 + 7 = y^2 (ge_set_xo_var, group_impl.h:216-237).
+  const ge G = gen_point();
+  const fr x = fr_select(ok, fe_to_fr(fe_from_u256(xr)), fe_to_fr(G.x));
+  const bool odd = ok && (recid & 1u) != 0;
+  const fr c = curve_rhs(x);
+  const uint32_t* gcomb = prm.gtab + (size_t)2 * GTAB * PT_WORDS;
   const uint32_t wv = threadIdx.x >> 6;
   if (wv == 1) {
-    // --- u1 = -z / r, u2 = s / r (main_impl.h:114-117), digits into LDS. A signature whose R
-    // fails to lift is recovered from G instead (wave 0); its scalars stay well-defined either way.
+    // --- u1 = -z / r, u2 = s / r (main_impl.h:114-117), digits into LDS
     R = sc_select(ok, R, sc_one());
     const sc rinv = sc_inv_row_var(R);  // wave-uniform data: variable-time safegcd, limb-parallel
     const sc u1 = sc_neg(sc_mul(rinv, Z));
     const sc u2 = sc_select(ok, sc_mul(rinv, Sv), sc_one());
     recode_digits(u2, u1, S);
-    __syncthreads();  // digits ready (and, WIDE, the table)
-    if constexpr (WIDE) wide_part_wave(1, S, prm.gtab);
+    __syncthreads();  // digits ready (and the table)
+    if constexpr (WIDE) lambda_half_wave(S);
+    else helper_wave(S, gcomb, true, c, odd);
     return;
   }
   if (WIDE && wv == 2) {
     __syncthreads();  // digits ready
-    wide_part_wave(2, S, prm.gtab);
+    helper_wave(S, gcomb, true, c, odd);
     return;
   }
-  ger Rp;
-  ok = ger_set_xo(Rp, fe_to_fr(fe_from_u256(xr)), (recid & 1u) != 0) && ok;
-  // failed signatures carry the generator, so every later step stays well-defined
-  const ge G = gen_point();
-  Rp.x = fr_select(ok, Rp.x, fe_to_fr(G.x));
-  Rp.y = fr_select(ok, Rp.y, fe_to_fr(G.y));
   st->mark(0);
-  // --- Q = u2 R + u1 G
-  const fr beta = fe_to_fr(fe_const(FE_BETA));
+  // --- Q = u2 R + u1 G, R's y (the square root) computed beside the Strauss loop
   gejr Q;
   bool qinf;
-  if constexpr (WIDE) ecmult_wide(Q, qinf, Rp, S, beta, st);
-  else ecmult_wave(Q, qinf, Rp, prm.gtab, S, beta, st);
-  ok = ok && !qinf;  // main_impl.h:120
+  ecmult_deferred<ST, WIDE>(Q, qinf, x, c, fr_zero(), true, S, st);
+  ok = ok && S.yok != 0 && !qinf;  // ge_set_xo_var failure, main_impl.h:120
   // --- affine, serialize, address
   const fr zq = fr_select(ok, Q.z, fr_one());
   const fr zi = fr_inv_var(zq);  // row-parallel safegcd (modinv_row.cuh)
@@ -504,20 +485,6 @@ DEV void verify_lat_body(const VerifyParams& prm) {
   const sc Z = sc_from_limbs(l, ovz);  // the message reduced mod n
   // parse_compact overflow, high s (ecdsa_verify), r or s zero (sig_verify)
   const bool sig_ok = !ovr && !ovs && !sc_is_high(Sv) && !sc_is_zero(R) && !sc_is_zero(Sv);
-  if ((threadIdx.x >> 6) == 1) {  // wave 1
-    const sc sinv = sc_inv_row_var(sc_select(sig_ok, Sv, sc_one()));
-    const sc u1 = sc_mul(sinv, Z);
-    const sc u2 = sc_select(sig_ok, sc_mul(sinv, R), sc_one());
-    recode_digits(u2, u1, S);
-    __syncthreads();  // digits ready (and, WIDE, the table)
-    if constexpr (WIDE) wide_part_wave(1, S, prm.gtab);
-    return;
-  }
-  if (WIDE && threadIdx.x >= 128) {
-    __syncthreads();  // digits ready
-    wide_part_wave(2, S, prm.gtab);
-    return;
-  }
   // --- public key (eckey_impl.h:17-34)
   const uint32_t plen = prm.publen[idx];
   const uint8_t* pk = prm.pub + (size_t)idx * 65;
@@ -533,29 +500,36 @@ DEV void verify_lat_body(const VerifyParams& prm) {
   const bool x_ok = !u256_ge(px, FE_P), y_ok = !u256_ge(py, FE_P);
   const bool c33 = plen == 33 && (pfx == 2 || pfx == 3);
   const bool c65 = plen == 65 && (pfx == 4 || pfx == 6 || pfx == 7);
-  const fr X = fe_to_fr(fe_from_u256(px)), Y = fe_to_fr(fe_from_u256(py));
-  ger P;
-  bool pk_ok;
-  if (c33) {  // wave-uniform
-    pk_ok = ger_set_xo(P, X, pfx == 3) && x_ok;
-  } else {
-    const bool hybrid_bad = (pfx == 6 || pfx == 7) && ((py[0] & 1u) != (pfx == 7 ? 1u : 0u));
-    const bool on = fr_equal(fr_add(fr_mul(fr_sqr(X), X), fr_small(7)), fr_sqr(Y));
-    pk_ok = c65 && x_ok && y_ok && !hybrid_bad && on;
-    P.x = X;
-    P.y = Y;
-  }
-  bool ok = sig_ok && pk_ok;
-  // failed items carry the generator, so every later step stays well-defined
+  const bool hybrid_bad = (pfx == 6 || pfx == 7) && ((py[0] & 1u) != (pfx == 7 ? 1u : 0u));
+  // keys that fail the parse carry the generator, so every later step stays well-defined
   const ge G = gen_point();
-  P.x = fr_select(ok, P.x, fe_to_fr(G.x));
-  P.y = fr_select(ok, P.y, fe_to_fr(G.y));
-  const fr beta = fe_to_fr(fe_const(FE_BETA));
+  const bool use_key = (c33 || c65) && x_ok;
+  const fr x = fr_select(use_key, fe_to_fr(fe_from_u256(px)), fe_to_fr(G.x));
+  const fr Y = fr_select(use_key && c65, fe_to_fr(fe_from_u256(py)), fe_to_fr(G.y));
+  const fr c = curve_rhs(x);
+  const uint32_t* gcomb = prm.gtab + (size_t)2 * GTAB * PT_WORDS;
+  const uint32_t wv = threadIdx.x >> 6;
+  if (wv == 1) {
+    const sc sinv = sc_inv_row_var(sc_select(sig_ok, Sv, sc_one()));
+    const sc u1 = sc_mul(sinv, Z);
+    const sc u2 = sc_select(sig_ok, sc_mul(sinv, R), sc_one());
+    recode_digits(u2, u1, S);
+    __syncthreads();  // digits ready (and the table)
+    if constexpr (WIDE) lambda_half_wave(S);
+    else helper_wave(S, gcomb, c33, c, pfx == 3);  // the square root only for 33-byte keys
+    return;
+  }
+  if (WIDE && wv == 2) {
+    __syncthreads();  // digits ready
+    helper_wave(S, gcomb, c33, c, pfx == 3);
+    return;
+  }
+  const bool on = fr_equal(c, fr_sqr(Y));  // 65-byte keys: on the curve
   gejr Q;
   bool qinf;
-  if constexpr (WIDE) ecmult_wide(Q, qinf, P, S, beta, &st_);
-  else ecmult_wave(Q, qinf, P, prm.gtab, S, beta, &st_);
-  ok = ok && !qinf;
+  ecmult_deferred<NoStamp, WIDE>(Q, qinf, x, c, Y, c33, S, &st_);
+  const bool pk_ok = c33 ? (x_ok && S.yok != 0) : (c65 && x_ok && y_ok && !hybrid_bad && on);
+  bool ok = sig_ok && pk_ok && !qinf;
   // x(Q) mod n == r  <=>  r Z^2 == X  or  (r < p - n and (r + n) Z^2 == X)  (ecdsa_impl.h:246-270)
   const fr z2 = fr_sqr(Q.z);
   bool eq = fr_equal(Q.x, fr_mul(fe_to_fr(fe_from_u256(R.v)), z2));
@@ -573,7 +547,7 @@ DEV void verify_lat_body(const VerifyParams& prm) {
   if (lane_id() == 0) prm.ok[idx] = (ok && eq) ? 1 : 0;
 }
 
-constexpr int LAT_WG_WIDE = 192;
+constexpr int LAT_WG_WIDE = 192;  // three waves
 
 __global__ void __launch_bounds__(LAT_WG) verify_lat_kernel(VerifyParams prm) { verify_lat_body<false>(prm); }
 __global__ void __launch_bounds__(LAT_WG_WIDE) verify_lat_wide_kernel(VerifyParams prm) { verify_lat_body<true>(prm); }

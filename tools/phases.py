@@ -27,7 +27,7 @@ PHASES = ["parse+sqrt", "r^-1 batch+u1/u2", "GLV+digits", "R table+affine", "Str
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
 if n <= int(os.environ.get("EGES_LAT_MAX", "8192")):  # the latency kernel's phases (k_recover_lat.hip)
-    PHASES = ["parse+lift(sqrt)", "wait: wave 1 r^-1+digits", "-", "R table", "Strauss", "Z^-1+affine",
+    PHASES = ["parse + x, c", "wait: wave 1 r^-1+digits", "-", "R' table", "Strauss + join", "Z^-1+affine",
               "keccak+store", "-"]
 assert lib.eges_init(0, 0) == 0, lib.eges_last_error()
 dev = torch.device("cuda:0")
