@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
@@ -282,7 +283,7 @@ static hipError_t stamp_buf(size_t waves, hipStream_t st) {
 
 hipError_t launch_recover_pass(Dev& d, const RecoverParams& p0, hipStream_t st) {
   RecoverParams p = p0;
-  // the wide form (three waves per signature) while the batch leaves SIMDs idle
+  // the split form (four waves per signature) while the batch leaves SIMDs idle
   p.wide = p.n <= (uint32_t)env_int("EGES_LAT_WIDE_MAX", 256) ? 1u : 0u;
 #ifdef EGES_PHASE_STAMPS
   if (p.n <= lat_max() || p.raw_sig) {
@@ -880,7 +881,8 @@ struct RecoverReq {
   const uint8_t* sig;
   uint8_t* pub;
   int result = 0;
-  bool done = false;
+  std::atomic<bool> done{false};
+  std::atomic<bool> queued{false};
 };
 struct VerifyReq {
   const uint8_t* sig;
@@ -888,7 +890,8 @@ struct VerifyReq {
   const uint8_t* pub;
   uint8_t publen;
   int result = 0;
-  bool done = false;
+  std::atomic<bool> done{false};
+  std::atomic<bool> queued{false};
 };
 
 void run_group(std::vector<RecoverReq*>& g) {
@@ -918,36 +921,89 @@ void run_group(std::vector<VerifyReq*>& g) {
   for (size_t i = 0; i < n; ++i) g[i]->result = (rc == EGES_SUCCESS && ok[i]) ? 1 : 0;
 }
 
+inline void cpu_relax() {
+#if defined(__x86_64__)
+  __builtin_ia32_pause();
+#else
+  std::this_thread::yield();
+#endif
+}
+
 // Up to NLANES groups are in flight at once (one per small-call lane of the device), so a
 // caller that arrives while a group runs does not wait for it to finish before its own starts.
+// Waiting callers spin on their own completion flag (a futex wake-up costs tens of µs against a
+// ~0.15 ms call) and fall back to blocking after EGES_COALESCE_SPIN_US. A new leader gathers for
+// up to EGES_COALESCE_GATHER_US until as many requests are queued as the previous group had: the
+// callers of a group that just finished come back within microseconds, and one launch for all
+// of them beats a launch for the first one and a lane wait for the rest.
 template <class Req>
 struct Coalescer {
   static constexpr size_t MAX_GROUP = 4096;
   std::mutex mu;
   std::condition_variable cv;
-  std::vector<Req*> queue;
-  int inflight = 0;
+  std::vector<Req*> queue;       // guarded by mu
+  std::atomic<size_t> qlen{0};   // queue.size(), for the gathering leader
+  std::atomic<int> inflight{0};  // groups running (changed under mu)
+  std::atomic<size_t> last_group{1};
+
+  static std::chrono::microseconds knob(const char* name, int dflt) {
+    return std::chrono::microseconds(std::max(0, env_int(name, dflt)));
+  }
+
+  // mu held on entry and exit; the caller has counted this group in `inflight`
+  void lead(std::unique_lock<std::mutex>& lk) {
+    static const auto gather = knob("EGES_COALESCE_GATHER_US", 20);
+    const size_t want = std::min(last_group.load(std::memory_order_relaxed), MAX_GROUP);
+    if (queue.size() < want && gather.count() > 0) {
+      lk.unlock();
+      const auto deadline = std::chrono::steady_clock::now() + gather;
+      while (qlen.load(std::memory_order_acquire) < want && std::chrono::steady_clock::now() < deadline) cpu_relax();
+      lk.lock();
+    }
+    std::vector<Req*> g;
+    const size_t take = std::min(queue.size(), MAX_GROUP);
+    g.assign(queue.begin(), queue.begin() + take);
+    queue.erase(queue.begin(), queue.begin() + take);
+    qlen.store(queue.size(), std::memory_order_release);
+    for (Req* q : g) q->queued.store(false, std::memory_order_relaxed);
+    last_group.store(std::max<size_t>(1, take), std::memory_order_relaxed);
+    lk.unlock();
+    run_group(g);
+    // a spinning caller returns as soon as its flag is set: the store is the last touch of q
+    for (Req* q : g) q->done.store(true, std::memory_order_release);
+    lk.lock();
+    --inflight;
+    cv.notify_all();
+  }
 
   void submit(Req* r) {
+    static const auto spin = knob("EGES_COALESCE_SPIN_US", 2000);
+    const auto t0 = std::chrono::steady_clock::now();
     std::unique_lock<std::mutex> lk(mu);
+    r->queued.store(true, std::memory_order_relaxed);
     queue.push_back(r);
-    while (!r->done) {
-      const bool mine_queued = std::find(queue.begin(), queue.end(), r) != queue.end();
-      if (mine_queued && inflight < NLANES) {
+    qlen.store(queue.size(), std::memory_order_release);
+    for (;;) {
+      if (r->done.load(std::memory_order_acquire)) return;
+      if (r->queued.load(std::memory_order_relaxed) && inflight.load() < NLANES) {
         ++inflight;
-        std::vector<Req*> g;
-        const size_t take = std::min(queue.size(), MAX_GROUP);
-        g.assign(queue.begin(), queue.begin() + take);
-        queue.erase(queue.begin(), queue.begin() + take);
-        lk.unlock();
-        run_group(g);
-        lk.lock();
-        for (Req* q : g) q->done = true;
-        --inflight;
-        cv.notify_all();
-      } else {
-        cv.wait(lk);
+        lead(lk);
+        continue;
       }
+      // served by another leader's group, or waiting for a free lane: spin, then block
+      lk.unlock();
+      bool block = false;
+      while (!r->done.load(std::memory_order_acquire)) {
+        if (r->queued.load(std::memory_order_relaxed) && inflight.load(std::memory_order_relaxed) < NLANES) break;
+        if (std::chrono::steady_clock::now() - t0 > spin) {
+          block = true;
+          break;
+        }
+        cpu_relax();
+      }
+      lk.lock();
+      if (block)
+        cv.wait(lk, [&] { return r->done.load() || (r->queued.load() && inflight.load() < NLANES); });
     }
   }
 };

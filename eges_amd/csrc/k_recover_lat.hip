@@ -25,20 +25,46 @@
 
 namespace eges {
 
-// One signature per workgroup of two waves (narrow form; wide: three, LAT_WG_WIDE).
+// One signature per workgroup of two waves (narrow form); the split form has four (LAT_WG_SPLIT).
 constexpr int LAT_WG = 128;
+// Split form: windows [0, SPLIT_W0) of both GLV halves against the R' table on wave 0, windows
+// [SPLIT_W0, RWIN) against a table of D = 2^(RBITS SPLIT_W0) R' on waves 2 (R) and 3 (lambda R).
+#ifndef EGES_SPLIT_W0
+#define EGES_SPLIT_W0 15
+#endif
+constexpr int SPLIT_W0 = EGES_SPLIT_W0;
+static_assert(SPLIT_W0 > 0 && SPLIT_W0 < RWIN, "split point");
+
+// LDS flags of the split form (set once by their producer wave, polled by the consumers)
+enum { F_DIG = 0, F_Y, F_G, F_LHI, F_HI, NFLAGS };
 
 struct LatLds {
   uint32_t tab[PTAB][2][16];  // {1..16} * R' (x, y), row form (all four rows read the same words)
   uint32_t zr[PTAB][16];      // Z ratios while the table is built
   uint32_t btab[PTAB][16];    // beta x of the table entries (the lambda R' additions)
+  uint32_t dtab[2][PTAB][2][16];  // split form: {1..16} * D, one copy per high-part wave
+  uint32_t dzr[2][PTAB][16];
+  uint32_t dbtab[PTAB][16];       //   and beta x for the lambda half (wave 3)
   int8_t rdig[2][RWIN];       // R / lambda R window digits
   uint16_t cdig[CWIN];        // comb digits of u_g
-  uint32_t part[3][3][16];    // partial sums (X, Y, Z): [1] lambda R half (wide), [2] u_g G
-  uint32_t pinf[3];           //   and their infinity flags
+  uint32_t part[5][3][16];    // partial sums (X, Y, Z): [2] u_g G, [3] high parts, [4] lambda high part
+  uint32_t pinf[5];           //   and their infinity flags
   uint32_t ylift[16];         // y of R (the square root, from the helper wave)
   uint32_t yok;
+  uint32_t flag[NFLAGS];
+  uint64_t w1t[2];            // diagnostic build: wave 1's r^-1 and u1 / u2 / GLV / digits ticks
 };
+
+// Producer / consumer hand-off between the waves of one workgroup through LDS (split form): the
+// producer's LDS writes are ordered before the flag by the release fence; consumers poll.
+DEV void flag_set(uint32_t* f) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane_id() == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+DEV void flag_wait(uint32_t* f) {
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
 
 // signed fixed-window recoding (core.cuh recode) into this row's digit array
 template <int W, int NW, class D>
@@ -124,34 +150,39 @@ DEV void recode_digits(const sc& u_r, const sc& u_g, LatLds& S) {
   for (int k = 0; k < CWIN; ++k) S.cdig[k] = (uint16_t)(u_g.v[k >> 1] >> (16 * (k & 1)));
 }
 
-// table {1..PTAB} * P on one global Z (co-Z additions, backward rescale; core.cuh); returns zeta
-DEV fr build_table_wave(const ger& P, LatLds& S) {
+using TabT = uint32_t[PTAB][2][16];
+using ColT = uint32_t[PTAB][16];
+
+// table {1..PTAB} * P on one global Z (co-Z additions, backward rescale; core.cuh); returns zeta.
+// P may be the (X, Y) of a Jacobian point: the formulas do not involve the curve's b, so the
+// entries are then points of the curve y^2 = x^3 + b Z^6 on which (X, Y) is affine.
+DEV fr build_table_wave(const ger& P, TabT& tab, ColT& zrs) {
   fr zeta;
   {
     const uint32_t L = row_lane();
-    lds_put_pt(S.tab[0], P);
+    lds_put_pt(tab[0], P);
     gejr D;
     ger B;
     gejq_dblu(D, B, P);
-    S.zr[0][L] = D.z.v;  // Z_2 / Z_1 = 2y
+    zrs[0][L] = D.z.v;  // Z_2 / Z_1 = 2y
     ger T;
     T.x = D.x;
     T.y = D.y;
-    lds_put_pt(S.tab[1], T);
+    lds_put_pt(tab[1], T);
 #pragma unroll 1
     for (int i = 2; i < PTAB; ++i) {
       const fr zr = gejq_zaddu(T, B);  // T = (i+1) P
-      lds_put_pt(S.tab[i], T);
-      S.zr[i - 1][L] = zr.v;
+      lds_put_pt(tab[i], T);
+      zrs[i - 1][L] = zr.v;
     }
     // entry i (< PTAB - 1) is rescaled by rho_i = prod_{k=i}^{PTAB-2} Z_{k+2}/Z_{k+1} = Z_PTAB / Z_{i+1}:
     // x rho^2, y rho^3, software-pipelined two quad steps per entry
-    fr rho{S.zr[PTAB - 2][L]};
+    fr rho{zrs[PTAB - 2][L]};
     fr s2 = fr_sqr(rho);
 #pragma unroll 1
     for (int i = PTAB - 2; i >= 0; --i) {
-      const ger J = lds_pt(S.tab[i]);
-      const fr zn{S.zr[i > 0 ? i - 1 : 0][L]};
+      const ger J = lds_pt(tab[i]);
+      const fr zn{zrs[i > 0 ? i - 1 : 0][L]};
       fr ax, s3, rho_n;
       fr_mul3(ax, s3, rho_n, J.x, s2, s2, rho, rho, zn);   // x rho^2, rho^3, next rho
       fr ay, s2_n;
@@ -159,7 +190,7 @@ DEV fr build_table_wave(const ger& P, LatLds& S) {
       ger a;
       a.x = ax;
       a.y = ay;
-      lds_put_pt(S.tab[i], a);
+      lds_put_pt(tab[i], a);
       if (i == 0) break;
       rho = rho_n;
       s2 = s2_n;
@@ -173,51 +204,39 @@ DEV fr build_table_wave(const ger& P, LatLds& S) {
 // of R = (x, y) under the isomorphism (x, y) -> (y^2 x, y^3 y), which needs no square root); the
 // R' table on E''s isomorphic curve with global Z = zeta; the G comb on the true curve.
 
-// Both GLV halves against the R' table in one loop (narrow form): 26 windows of 5 doublings and
-// two additions (R', lambda R' with beta x from btab).
+// Windows [wlo, whi) of the GLV halves selected by jmask (bit 0: R digits against tab, bit 1:
+// lambda R digits against (btab, tab.y)), Horner from the top window: 5 doublings per window and
+// one addition per selected half. The narrow form runs [0, RWIN) with both halves.
 template <bool CHECKED>
-DEV void strauss_rr(gejr& acc, bool& inf, const LatLds& S) {
+DEV void strauss_win(gejr& acc, bool& inf, const LatLds& S, const TabT& tab, const ColT& btab, int jmask, int wlo,
+                     int whi) {
   inf = true;
   acc.x = fr_zero();
   acc.y = fr_zero();
   acc.z = fr_zero();
 #pragma unroll 1
-  for (int w = RWIN - 1; w >= 0; --w) {
-    if (w != RWIN - 1) {
+  for (int w = whi - 1; w >= wlo; --w) {
+    if (w != whi - 1) {
 #pragma unroll 1
       for (int k = 0; k < RBITS; ++k) acc = gejq_double(acc);
     }
 #pragma unroll 1
     for (int j = 0; j < 2; ++j) {
+      if (!((jmask >> j) & 1)) continue;
       const int d = (int)S.rdig[j][w];
       const int a = d < 0 ? -d : d;
       const int e = a > 0 ? a - 1 : 0;
-      ger p = lds_pt(S.tab[e]);
-      if (j == 1) p.x.v = S.btab[e][row_lane()];  // lambda (x, y) = (beta x, y)
+      ger p = lds_pt(tab[e]);
+      if (j == 1) p.x.v = btab[e][row_lane()];  // lambda (x, y) = (beta x, y)
       add_r<CHECKED>(acc, inf, ger_neg_if(p, d < 0), d != 0);
     }
   }
 }
-// One GLV half (wide form: j = 0 on wave 0, j = 1 on wave 1).
-template <bool CHECKED>
-DEV void strauss_r_part(gejr& acc, bool& inf, const LatLds& S, int j) {
-  inf = true;
-  acc.x = fr_zero();
-  acc.y = fr_zero();
-  acc.z = fr_zero();
-#pragma unroll 1
-  for (int w = RWIN - 1; w >= 0; --w) {
-    if (w != RWIN - 1) {
-#pragma unroll 1
-      for (int k = 0; k < RBITS; ++k) acc = gejq_double(acc);
-    }
-    const int d = (int)S.rdig[j][w];
-    const int a = d < 0 ? -d : d;
-    const int e = a > 0 ? a - 1 : 0;
-    ger p = lds_pt(S.tab[e]);
-    if (j == 1) p.x.v = S.btab[e][row_lane()];
-    add_r<CHECKED>(acc, inf, ger_neg_if(p, d < 0), d != 0);
-  }
+template <bool UNUSED = false>
+DEV void strauss_win_exact(gejr& acc, bool& inf, const LatLds& S, const TabT& tab, const ColT& btab, int jmask,
+                           int wlo, int whi) {
+  strauss_win<false>(acc, inf, S, tab, btab, jmask, wlo, whi);
+  if (__any(!inf && fr_is_zero(acc.z))) strauss_win<true>(acc, inf, S, tab, btab, jmask, wlo, whi);
 }
 // u_g G from the comb table: one addition per 16-bit digit, no doublings (true curve).
 template <bool CHECKED>
@@ -250,18 +269,18 @@ DEV gejr get_part(const LatLds& S, int k, bool& inf) {
   return a;
 }
 // beta x of the 16 table entries, four per quad step
-DEV void build_btab(LatLds& S) {
+DEV void build_btab(const TabT& tab, ColT& btab) {
   const fr beta = fe_to_fr(fe_const(FE_BETA));
   const uint32_t L = row_lane();
 #pragma unroll 1
   for (int i = 0; i < PTAB; i += 4) {
     fr b0, b1, b2, b3;
-    fr_mul4(b0, b1, b2, b3, lds_pt(S.tab[i]).x, beta, lds_pt(S.tab[i + 1]).x, beta, lds_pt(S.tab[i + 2]).x, beta,
-            lds_pt(S.tab[i + 3]).x, beta);
-    S.btab[i][L] = b0.v;
-    S.btab[i + 1][L] = b1.v;
-    S.btab[i + 2][L] = b2.v;
-    S.btab[i + 3][L] = b3.v;
+    fr_mul4(b0, b1, b2, b3, lds_pt(tab[i]).x, beta, lds_pt(tab[i + 1]).x, beta, lds_pt(tab[i + 2]).x, beta,
+            lds_pt(tab[i + 3]).x, beta);
+    btab[i][L] = b0.v;
+    btab[i + 1][L] = b1.v;
+    btab[i + 2][L] = b2.v;
+    btab[i + 3][L] = b3.v;
   }
 }
 // c = x^3 + 7 (magnitude 1)
@@ -276,16 +295,14 @@ DEV bool lift_y(fr& y, const fr& c, bool odd) {
   return ok;
 }
 
-// Helper wave, after the first barrier: the square root (when the point came compressed) and
-// the u_g G comb part into LDS, then the second barrier. Both run beside wave 0's table and
-// Strauss loop instead of ahead of them.
-DEV void helper_wave(LatLds& S, const uint32_t* gcomb, bool need_y, const fr& c, bool odd) {
-  if (need_y) {
-    fr y;
-    const bool ok = lift_y(y, c, odd);
-    S.ylift[row_lane()] = y.v;
-    if (lane_id() == 0) S.yok = ok ? 1u : 0u;
-  }
+// Narrow form, wave 1 after the barrier: the square root (when the point came compressed) and
+// the u_g G comb part into LDS, then the second barrier. Both run beside wave 0's Strauss loop.
+DEV void helper_wave(LatLds& S, const uint32_t* gcomb, bool need_y, const fr& c, bool odd, const fr& y_given) {
+  fr y = y_given;
+  bool ok = true;
+  if (need_y) ok = lift_y(y, c, odd);
+  S.ylift[row_lane()] = y.v;
+  if (lane_id() == 0) S.yok = ok ? 1u : 0u;
   gejr A;
   bool ainf;
   strauss_gcomb<false>(A, ainf, S, gcomb);
@@ -293,68 +310,108 @@ DEV void helper_wave(LatLds& S, const uint32_t* gcomb, bool need_y, const fr& c,
   put_part(S, 2, A, ainf);
   __syncthreads();  // partial sums and y ready
 }
-// Wide form, wave 1 after the first barrier: the lambda R' half.
-DEV void lambda_half_wave(LatLds& S) {
-  build_btab(S);
+// Split form, wave 1 after its scalar work: y (the square root, or the given y), then u_g G.
+DEV void helper_split(LatLds& S, const uint32_t* gcomb, bool need_y, const fr& c, bool odd, const fr& y_given) {
+  fr y = y_given;
+  bool ok = true;
+  if (need_y) ok = lift_y(y, c, odd);
+  S.ylift[row_lane()] = y.v;
+  if (lane_id() == 0) S.yok = ok ? 1u : 0u;
+  flag_set(&S.flag[F_Y]);
   gejr A;
   bool ainf;
-  strauss_r_part<false>(A, ainf, S, 1);
-  if (__any(!ainf && fr_is_zero(A.z))) strauss_r_part<true>(A, ainf, S, 1);
-  put_part(S, 1, A, ainf);
-  __syncthreads();  // partial sums ready
+  strauss_gcomb<false>(A, ainf, S, gcomb);
+  if (__any(!ainf && fr_is_zero(A.z))) strauss_gcomb<true>(A, ainf, S, gcomb);
+  put_part(S, 2, A, ainf);
+  flag_set(&S.flag[F_G]);
+}
+// Split form, waves 2 (j = 0: R) and 3 (j = 1: lambda R): D = 2^(RBITS SPLIT_W0) R' by doublings
+// (each wave its own copy, no hand-off), the table of D's (X, Y) on the curve where it is affine,
+// the high windows of one GLV half, then back to the true curve: a sum (X, Y, Z) there is the E'
+// point (X, Y, Z zeta_D Z_D) and the E point (X, Y, Z zeta_D Z_D y). Wave 2 joins wave 3's part.
+DEV void high_wave(LatLds& S, const fr& x, const fr& c, int j) {
+  gejr D;
+  fr_mul2(D.x, D.y, c, x, c, c);  // R' = (c x, c^2)
+  D.z = fr_one();
+#pragma unroll 1
+  for (int k = 0; k < RBITS * SPLIT_W0; ++k) D = gejq_double(D);  // R' has odd order: never exceptional
+  ger Dp;
+  Dp.x = D.x;
+  Dp.y = D.y;
+  const fr zd = build_table_wave(Dp, S.dtab[j], S.dzr[j]);
+  if (j == 1) build_btab(S.dtab[1], S.dbtab);
+  const fr scale = fr_mul(zd, D.z);
+  flag_wait(&S.flag[F_DIG]);
+  gejr A;
+  bool ainf;
+  strauss_win_exact(A, ainf, S, S.dtab[j], S.dbtab, 1 << j, SPLIT_W0, RWIN);
+  flag_wait(&S.flag[F_Y]);
+  A.z = fr_mul(A.z, fr_mul(scale, fr{S.ylift[row_lane()]}));
+  if (j == 1) {
+    put_part(S, 4, A, ainf);
+    flag_set(&S.flag[F_LHI]);
+    return;
+  }
+  flag_wait(&S.flag[F_LHI]);
+  bool linf;
+  const gejr Lp = get_part(S, 4, linf);
+  A = gejq_add(A, ainf, Lp, linf, ainf);
+  put_part(S, 3, A, ainf);
+  flag_set(&S.flag[F_HI]);
 }
 
-// Wave 0: u_r * (x, y) + u_g G with y deferred. R' = (c x, c^2) on E', its table, the first
-// barrier (digits), the R' Strauss sum(s), the second barrier (the other parts and y), then
-// back to the true curve: an E' Jacobian point (X, Y, Z) is (X, Y, Z y) on E, and the table's
-// isomorphic curve adds the factor zeta. y comes from LDS (helper wave) or is given.
-template <class ST, bool WIDE>
-DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, const fr& y_given, bool y_in_lds,
-                         LatLds& S, ST* st) {
+// Wave 0: u_r * (x, y) + u_g G with y deferred. R' = (c x, c^2) on E', its table, the digits,
+// the R' Strauss sum(s), then back to the true curve: an E' Jacobian point (X, Y, Z) is (X, Y, Z y)
+// on E, and the table's isomorphic curve adds the factor zeta. y comes from LDS (helper wave).
+// Narrow: both GLV halves over every window here, two barriers. Split: the low windows of both
+// halves here; the high windows' sum (waves 2, 3) and u_g G (wave 1) are joined at the end.
+template <class ST, bool SPLIT>
+DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& S, ST* st) {
   ger Rp;
   fr_mul2(Rp.x, Rp.y, c, x, c, c);  // (c x, c^2)
-  const fr zeta = build_table_wave(Rp, S);
-  if (!WIDE) build_btab(S);
+  const fr zeta = build_table_wave(Rp, S.tab, S.zr);
+  build_btab(S.tab, S.btab);
   st->mark(3);
-  __syncthreads();  // digits ready (wide: the table is wave 1's too)
+  if (SPLIT) flag_wait(&S.flag[F_DIG]);
+  else __syncthreads();  // digits ready
   st->mark(1);
   gejr A;
   bool ainf;
-  if constexpr (WIDE) {
-    strauss_r_part<false>(A, ainf, S, 0);
-    if (__any(!ainf && fr_is_zero(A.z))) strauss_r_part<true>(A, ainf, S, 0);
-  } else {
-    strauss_rr<false>(A, ainf, S);
-    if (__any(!ainf && fr_is_zero(A.z))) strauss_rr<true>(A, ainf, S);
-  }
-  __syncthreads();  // partial sums (and y) ready
-  if constexpr (WIDE) {
-    bool linf;
-    const gejr Lp = get_part(S, 1, linf);
-    A = gejq_add(A, ainf, Lp, linf, ainf);  // both halves on the isomorphic curve of E'
-  }
-  const fr y = y_in_lds ? fr{S.ylift[row_lane()]} : y_given;
-  A.z = fr_mul(A.z, fr_mul(zeta, y));  // the true curve
+  strauss_win_exact(A, ainf, S, S.tab, S.btab, 3, 0, SPLIT ? SPLIT_W0 : RWIN);
+  if (SPLIT) flag_wait(&S.flag[F_Y]);
+  else __syncthreads();  // partial sums (and y) ready
+  A.z = fr_mul(A.z, fr_mul(zeta, fr{S.ylift[row_lane()]}));  // the true curve
   bool ginf;
+  if (SPLIT) flag_wait(&S.flag[F_G]);
   const gejr Gp = get_part(S, 2, ginf);
   Q = gejq_add(A, ainf, Gp, ginf, qinf);
+  if (SPLIT) {
+    flag_wait(&S.flag[F_HI]);
+    bool hinf;
+    const gejr Hp = get_part(S, 3, hinf);
+    Q = gejq_add(Q, qinf, Hp, hinf, qinf);
+  }
   st->mark(4);
 }
 
 // Phase marks of wave 0 (diagnostic build only): 0 parse + x, c, 3 table, 1 wait for wave 1's
-// r^-1 / u1 / u2 / digits, 4 Strauss + join (including the wait for the other parts and y),
+// r^-1 / u1 / u2 / digits, 4 Strauss + join (including the waits for the other parts and y),
 // 5 Z^-1 + affine, 6 Keccak + stores.
 // Narrow form (two waves): wave 0 table + both GLV halves; wave 1 the scalar work, then the
-// square root and the u1 G comb part. WIDE (small batches, three waves): wave 1 takes the
-// lambda R' half after its scalar work, wave 2 the square root and the comb part; wave 0 joins
-// the three partial sums with two general additions.
-template <class ST, bool WIDE>
+// square root and the u1 G comb part. SPLIT (small batches, four waves): wave 1 the scalar work,
+// y and u1 G; waves 2 and 3 the high windows of the two GLV halves against their own table of
+// D = 2^75 R'; wave 0 the low windows of both halves, then joins the three partial sums.
+template <class ST, bool SPLIT>
 DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   __shared__ LatLds S;
   ST st_;
   ST* st = &st_;
   const uint32_t idx = blockIdx.x;  // grid = n: every wave has a signature
   const uint32_t np = prm.n_pad;
+  if (SPLIT) {
+    if (threadIdx.x < NFLAGS) S.flag[threadIdx.x] = 0u;
+    __syncthreads();  // the only barrier of the split form
+  }
   // --- parse (every lane reads the same record)
   uint32_t rl[8], sl[8], zl[8];
   uint32_t meta;
@@ -401,26 +458,36 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   const uint32_t wv = threadIdx.x >> 6;
   if (wv == 1) {
     // --- u1 = -z / r, u2 = s / r (main_impl.h:114-117), digits into LDS
+    constexpr bool stamped = !std::is_same<ST, NoStamp>::value;
+    const uint64_t t0 = stamped ? __builtin_amdgcn_s_memtime() : 0;
     R = sc_select(ok, R, sc_one());
     const sc rinv = sc_inv_row_var(R);  // wave-uniform data: variable-time safegcd, limb-parallel
+    const uint64_t t1 = stamped ? __builtin_amdgcn_s_memtime() : 0;
     const sc u1 = sc_neg(sc_mul(rinv, Z));
     const sc u2 = sc_select(ok, sc_mul(rinv, Sv), sc_one());
     recode_digits(u2, u1, S);
-    __syncthreads();  // digits ready (and the table)
-    if constexpr (WIDE) lambda_half_wave(S);
-    else helper_wave(S, gcomb, true, c, odd);
+    if (stamped && lane_id() == 0) {
+      S.w1t[0] = t1 - t0;
+      S.w1t[1] = __builtin_amdgcn_s_memtime() - t1;
+    }
+    if (SPLIT) {
+      flag_set(&S.flag[F_DIG]);
+      helper_split(S, gcomb, true, c, odd, fr_zero());
+    } else {
+      __syncthreads();  // digits ready (and the table)
+      helper_wave(S, gcomb, true, c, odd, fr_zero());
+    }
     return;
   }
-  if (WIDE && wv == 2) {
-    __syncthreads();  // digits ready
-    helper_wave(S, gcomb, true, c, odd);
+  if (SPLIT && (wv == 2 || wv == 3)) {
+    high_wave(S, x, c, (int)wv - 2);
     return;
   }
   st->mark(0);
   // --- Q = u2 R + u1 G, R's y (the square root) computed beside the Strauss loop
   gejr Q;
   bool qinf;
-  ecmult_deferred<ST, WIDE>(Q, qinf, x, c, fr_zero(), true, S, st);
+  ecmult_deferred<ST, SPLIT>(Q, qinf, x, c, S, st);
   ok = ok && S.yok != 0 && !qinf;  // ge_set_xo_var failure, main_impl.h:120
   // --- affine, serialize, address
   const fr zq = fr_select(ok, Q.z, fr_one());
@@ -457,6 +524,8 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   }
   st->mark(6);
   if constexpr (!std::is_same<ST, NoStamp>::value) {
+    st_.acc[2] = S.w1t[0];  // wave 1's phases in the unused slots (not part of wave 0's total)
+    st_.acc[7] = S.w1t[1];
     if (lane_id() == 0) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) stamps[(size_t)blockIdx.x * 8 + i] = st_.acc[i];
@@ -470,11 +539,15 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
 // (variable-time safegcd), u1 = z/s, u2 = r/s and the digits while wave 0 parses the public key
 // (the square root for 33-byte keys, the curve equation for 65-byte ones); then Q = u2 P + u1 G
 // and x(Q) == r checked projectively (r Z^2 == X), no field inversion.
-template <bool WIDE>
+template <bool SPLIT>
 DEV void verify_lat_body(const VerifyParams& prm) {
   __shared__ LatLds S;
   NoStamp st_;
   const uint32_t idx = blockIdx.x;  // grid = n
+  if (SPLIT) {
+    if (threadIdx.x < NFLAGS) S.flag[threadIdx.x] = 0u;
+    __syncthreads();  // the only barrier of the split form
+  }
   uint32_t l[8];
   bool ovr, ovs, ovz;
   limbs_from_be32(l, prm.sig + (size_t)idx * 64);
@@ -514,20 +587,24 @@ DEV void verify_lat_body(const VerifyParams& prm) {
     const sc u1 = sc_mul(sinv, Z);
     const sc u2 = sc_select(sig_ok, sc_mul(sinv, R), sc_one());
     recode_digits(u2, u1, S);
-    __syncthreads();  // digits ready (and the table)
-    if constexpr (WIDE) lambda_half_wave(S);
-    else helper_wave(S, gcomb, c33, c, pfx == 3);  // the square root only for 33-byte keys
+    // the square root only for 33-byte keys; 65-byte keys give y
+    if (SPLIT) {
+      flag_set(&S.flag[F_DIG]);
+      helper_split(S, gcomb, c33, c, pfx == 3, Y);
+    } else {
+      __syncthreads();  // digits ready (and the table)
+      helper_wave(S, gcomb, c33, c, pfx == 3, Y);
+    }
     return;
   }
-  if (WIDE && wv == 2) {
-    __syncthreads();  // digits ready
-    helper_wave(S, gcomb, c33, c, pfx == 3);
+  if (SPLIT && (wv == 2 || wv == 3)) {
+    high_wave(S, x, c, (int)wv - 2);
     return;
   }
   const bool on = fr_equal(c, fr_sqr(Y));  // 65-byte keys: on the curve
   gejr Q;
   bool qinf;
-  ecmult_deferred<NoStamp, WIDE>(Q, qinf, x, c, Y, c33, S, &st_);
+  ecmult_deferred<NoStamp, SPLIT>(Q, qinf, x, c, S, &st_);
   const bool pk_ok = c33 ? (x_ok && S.yok != 0) : (c65 && x_ok && y_ok && !hybrid_bad && on);
   bool ok = sig_ok && pk_ok && !qinf;
   // x(Q) mod n == r  <=>  r Z^2 == X  or  (r < p - n and (r + n) Z^2 == X)  (ecdsa_impl.h:246-270)
@@ -547,14 +624,14 @@ DEV void verify_lat_body(const VerifyParams& prm) {
   if (lane_id() == 0) prm.ok[idx] = (ok && eq) ? 1 : 0;
 }
 
-constexpr int LAT_WG_WIDE = 192;  // three waves
+constexpr int LAT_WG_SPLIT = 256;  // split form: four waves
 
 __global__ void __launch_bounds__(LAT_WG) verify_lat_kernel(VerifyParams prm) { verify_lat_body<false>(prm); }
-__global__ void __launch_bounds__(LAT_WG_WIDE) verify_lat_wide_kernel(VerifyParams prm) { verify_lat_body<true>(prm); }
+__global__ void __launch_bounds__(LAT_WG_SPLIT) verify_lat_split_kernel(VerifyParams prm) { verify_lat_body<true>(prm); }
 
 hipError_t launch_verify_lat(const VerifyParams& p, bool wide, hipStream_t st) {
   if (p.n == 0) return hipSuccess;
-  if (wide) hipLaunchKernelGGL(verify_lat_wide_kernel, dim3(p.n), dim3(LAT_WG_WIDE), 0, st, p);
+  if (wide) hipLaunchKernelGGL(verify_lat_split_kernel, dim3(p.n), dim3(LAT_WG_SPLIT), 0, st, p);
   else hipLaunchKernelGGL(verify_lat_kernel, dim3(p.n), dim3(LAT_WG), 0, st, p);
   return hipGetLastError();
 }
@@ -562,13 +639,13 @@ hipError_t launch_verify_lat(const VerifyParams& p, bool wide, hipStream_t st) {
 __global__ void __launch_bounds__(LAT_WG) recover_lat_kernel(RecoverParams prm) {
   recover_lat_body<NoStamp, false>(prm, nullptr);
 }
-__global__ void __launch_bounds__(LAT_WG_WIDE) recover_lat_wide_kernel(RecoverParams prm) {
+__global__ void __launch_bounds__(LAT_WG_SPLIT) recover_lat_split_kernel(RecoverParams prm) {
   recover_lat_body<NoStamp, true>(prm, nullptr);
 }
 
 hipError_t launch_recover_lat(const RecoverParams& p, hipStream_t st) {
   if (p.n == 0) return hipSuccess;
-  if (p.wide) hipLaunchKernelGGL(recover_lat_wide_kernel, dim3(p.n), dim3(LAT_WG_WIDE), 0, st, p);
+  if (p.wide) hipLaunchKernelGGL(recover_lat_split_kernel, dim3(p.n), dim3(LAT_WG_SPLIT), 0, st, p);
   else hipLaunchKernelGGL(recover_lat_kernel, dim3(p.n), dim3(LAT_WG), 0, st, p);
   return hipGetLastError();
 }
@@ -577,12 +654,12 @@ hipError_t launch_recover_lat(const RecoverParams& p, hipStream_t st) {
 __global__ void __launch_bounds__(LAT_WG) recover_lat_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
   recover_lat_body<Stamper, false>(prm, stamps);
 }
-__global__ void __launch_bounds__(LAT_WG_WIDE) recover_lat_wide_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
+__global__ void __launch_bounds__(LAT_WG_SPLIT) recover_lat_split_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
   recover_lat_body<Stamper, true>(prm, stamps);
 }
 hipError_t launch_recover_lat_stamped(const RecoverParams& p, hipStream_t st, uint64_t* stamps) {
   if (p.n == 0) return hipSuccess;
-  if (p.wide) hipLaunchKernelGGL(recover_lat_wide_kernel_stamped, dim3(p.n), dim3(LAT_WG_WIDE), 0, st, p, stamps);
+  if (p.wide) hipLaunchKernelGGL(recover_lat_split_kernel_stamped, dim3(p.n), dim3(LAT_WG_SPLIT), 0, st, p, stamps);
   else hipLaunchKernelGGL(recover_lat_kernel_stamped, dim3(p.n), dim3(LAT_WG), 0, st, p, stamps);
   return hipGetLastError();
 }

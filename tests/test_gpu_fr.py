@@ -81,7 +81,7 @@ def _add(p, q):
 
 
 def test_fr_general_add(st):
-    """gejq_add (the wide latency kernel's join) on points with different Z: random sums,
+    """gejq_add (the split latency kernel's joins) on points with different Z: random sums,
     a == b (doubling), a == -b (infinity), against big-integer affine addition."""
     rnd = random.Random(77)
     xs = []

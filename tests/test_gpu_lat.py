@@ -35,12 +35,12 @@ class lat_max(env_knob):  # batches up to this size take the latency kernels
     name = "EGES_LAT_MAX"
 
 
-class wide_max(env_knob):  # latency batches up to this size use the wide (3-wave) recover form
+class wide_max(env_knob):  # latency batches up to this size use the split (4-wave) form
     name = "EGES_LAT_WIDE_MAX"
 
 
 def test_wide_kernel_golden_recover(engine):
-    """Every golden recovery item (all reject classes) through the wide form, the narrow form
+    """Every golden recovery item (all reject classes) through the split form, the narrow form
     and the lane-serial kernel: byte for byte the same, and the fixtures'."""
     g = load_golden("recover.npz")
     with lat_max(1 << 20), wide_max(1 << 20):

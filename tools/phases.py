@@ -22,13 +22,15 @@ for name, (res, args) in _lib.SIGNATURES.items():
 lib.eges_diag_read_stamps.restype = ctypes.c_size_t
 lib.eges_diag_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 
+LAT = False
 PHASES = ["parse+sqrt", "r^-1 batch+u1/u2", "GLV+digits", "R table+affine", "Strauss", "Z^-1 batch",
           "keccak+store", "-"]
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
 if n <= int(os.environ.get("EGES_LAT_MAX", "8192")):  # the latency kernel's phases (k_recover_lat.hip)
-    PHASES = ["parse + x, c", "wait: wave 1 r^-1+digits", "-", "R' table", "Strauss + join", "Z^-1+affine",
-              "keccak+store", "-"]
+    PHASES = ["parse + x, c", "wait: wave 1 r^-1+digits", "(wave 1: r^-1)", "R' table", "Strauss + join",
+              "Z^-1+affine", "keccak+store", "(wave 1: u1,u2,GLV,digits)"]
+    LAT = True
 assert lib.eges_init(0, 0) == 0, lib.eges_last_error()
 dev = torch.device("cuda:0")
 msg = torch.empty(n * 32, dtype=torch.uint8, device=dev)
@@ -53,10 +55,10 @@ lib.eges_diag_read_stamps(buf, waves)
 import numpy as np  # noqa: E402
 
 a = np.frombuffer(buf, dtype=np.uint64).reshape(waves, 8).astype(np.float64)
-tot = a.sum(axis=1)
+tot = (a.sum(axis=1) - a[:, 2] - a[:, 7]) if LAT else a.sum(axis=1)
 print(f"n={n} launch {dt * 1e3:.2f} ms ({n / dt / 1e6:.2f} M sigs/s, stamped build), waves={waves}")
 print(f"per-wave total: mean {tot.mean():.4g} min {tot.min():.4g} max {tot.max():.4g} (s_memtime ticks)")
 tiles_per_wave = max(n / 256 / (waves / 4), 1e-9)
-for i in range(7):
+for i in range(8 if LAT else 7):
     m = a[:, i].mean()
     print(f"  {PHASES[i]:18s} {m:12.4g} ticks/wave  {100 * m / tot.mean():5.1f}%  {m / tiles_per_wave:10.4g}/tile")
