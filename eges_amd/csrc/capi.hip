@@ -40,6 +40,14 @@ constexpr size_t PIN_BYTES = size_t(8) << 20;
 
 thread_local std::string t_err;
 
+inline void cpu_relax() {
+#if defined(__x86_64__)
+  __builtin_ia32_pause();
+#else
+  std::this_thread::yield();
+#endif
+}
+
 int set_err(int rc, const char* fmt, ...) {
   char buf[512];
   va_list ap;
@@ -919,14 +927,6 @@ void run_group(std::vector<VerifyReq*>& g) {
   }
   const int rc = eges_verify_batch(pub.data(), publen.data(), msg.data(), sig.data(), n, ok.data());
   for (size_t i = 0; i < n; ++i) g[i]->result = (rc == EGES_SUCCESS && ok[i]) ? 1 : 0;
-}
-
-inline void cpu_relax() {
-#if defined(__x86_64__)
-  __builtin_ia32_pause();
-#else
-  std::this_thread::yield();
-#endif
 }
 
 // Up to NLANES groups are in flight at once (one per small-call lane of the device), so a
