@@ -932,10 +932,11 @@ void run_group(std::vector<VerifyReq*>& g) {
 // Up to NLANES groups are in flight at once (one per small-call lane of the device), so a
 // caller that arrives while a group runs does not wait for it to finish before its own starts.
 // Waiting callers spin on their own completion flag (a futex wake-up costs tens of µs against a
-// ~0.15 ms call) and fall back to blocking after EGES_COALESCE_SPIN_US. A new leader gathers for
-// up to EGES_COALESCE_GATHER_US until as many requests are queued as the previous group had: the
-// callers of a group that just finished come back within microseconds, and one launch for all
-// of them beats a launch for the first one and a lane wait for the rest.
+// ~0.15 ms call) and fall back to blocking after EGES_COALESCE_SPIN_US. One leader at a time
+// gathers: for up to EGES_COALESCE_GATHER_US it waits until as many requests are queued as the
+// previous group had (the callers of a group that just finished come back within microseconds,
+// and one launch for all of them beats a launch for the first and a lane wait for the rest),
+// while the callers it will take spin instead of leading groups of their own.
 template <class Req>
 struct Coalescer {
   static constexpr size_t MAX_GROUP = 4096;
@@ -943,17 +944,22 @@ struct Coalescer {
   std::condition_variable cv;
   std::vector<Req*> queue;       // guarded by mu
   std::atomic<size_t> qlen{0};   // queue.size(), for the gathering leader
-  std::atomic<int> inflight{0};  // groups running (changed under mu)
-  std::atomic<size_t> last_group{1};
+  std::atomic<int> inflight{0};  // groups running or gathering (changed under mu)
+  std::atomic<bool> gathering{false};  // a leader is gathering (changed under mu)
+  size_t last_group = 1;         // guarded by mu
 
   static std::chrono::microseconds knob(const char* name, int dflt) {
     return std::chrono::microseconds(std::max(0, env_int(name, dflt)));
   }
+  bool may_lead(const Req* r) const {
+    return r->queued.load(std::memory_order_relaxed) && inflight.load(std::memory_order_relaxed) < NLANES &&
+           !gathering.load(std::memory_order_relaxed);
+  }
 
-  // mu held on entry and exit; the caller has counted this group in `inflight`
+  // mu held on entry and exit; the caller has counted this group in `inflight` and set `gathering`
   void lead(std::unique_lock<std::mutex>& lk) {
     static const auto gather = knob("EGES_COALESCE_GATHER_US", 20);
-    const size_t want = std::min(last_group.load(std::memory_order_relaxed), MAX_GROUP);
+    const size_t want = std::min(last_group, MAX_GROUP);
     if (queue.size() < want && gather.count() > 0) {
       lk.unlock();
       const auto deadline = std::chrono::steady_clock::now() + gather;
@@ -961,12 +967,14 @@ struct Coalescer {
       lk.lock();
     }
     std::vector<Req*> g;
-    const size_t take = std::min(queue.size(), MAX_GROUP);
+    const size_t take = std::min(queue.size(), MAX_GROUP);  // >= 1: the leader's own request is queued
     g.assign(queue.begin(), queue.begin() + take);
     queue.erase(queue.begin(), queue.begin() + take);
     qlen.store(queue.size(), std::memory_order_release);
     for (Req* q : g) q->queued.store(false, std::memory_order_relaxed);
-    last_group.store(std::max<size_t>(1, take), std::memory_order_relaxed);
+    last_group = std::max<size_t>(1, take);
+    gathering.store(false, std::memory_order_relaxed);
+    if (!queue.empty()) cv.notify_all();  // a blocked caller may lead the next group
     lk.unlock();
     run_group(g);
     // a spinning caller returns as soon as its flag is set: the store is the last touch of q
@@ -985,8 +993,9 @@ struct Coalescer {
     qlen.store(queue.size(), std::memory_order_release);
     for (;;) {
       if (r->done.load(std::memory_order_acquire)) return;
-      if (r->queued.load(std::memory_order_relaxed) && inflight.load() < NLANES) {
+      if (may_lead(r)) {
         ++inflight;
+        gathering.store(true, std::memory_order_relaxed);
         lead(lk);
         continue;
       }
@@ -994,7 +1003,7 @@ struct Coalescer {
       lk.unlock();
       bool block = false;
       while (!r->done.load(std::memory_order_acquire)) {
-        if (r->queued.load(std::memory_order_relaxed) && inflight.load(std::memory_order_relaxed) < NLANES) break;
+        if (may_lead(r)) break;
         if (std::chrono::steady_clock::now() - t0 > spin) {
           block = true;
           break;
@@ -1002,8 +1011,7 @@ struct Coalescer {
         cpu_relax();
       }
       lk.lock();
-      if (block)
-        cv.wait(lk, [&] { return r->done.load() || (r->queued.load() && inflight.load() < NLANES); });
+      if (block) cv.wait(lk, [&] { return r->done.load() || may_lead(r); });
     }
   }
 };

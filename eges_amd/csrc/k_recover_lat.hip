@@ -21,6 +21,7 @@
 
 #include "core.cuh"
 #include "frg.cuh"
+#include "keccak_wave.cuh"
 #include "modinv_row.cuh"
 
 namespace eges {
@@ -491,7 +492,12 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   ok = ok && S.yok != 0 && !qinf;  // ge_set_xo_var failure, main_impl.h:120
   // --- affine, serialize, address
   const fr zq = fr_select(ok, Q.z, fr_one());
+#ifdef EGES_STAMP_MODINV  // diagnostic: slots 2 / 7 carry Z^-1's divsteps / update ticks instead
+  uint64_t mprof[2] = {0, 0};
+  const fr zi = fr_inv_var(zq, mprof);
+#else
   const fr zi = fr_inv_var(zq);  // row-parallel safegcd (modinv_row.cuh)
+#endif
   fr zi2, zi3;
   zi2 = fr_sqr(zi);
   fr X1, Y1;
@@ -502,7 +508,7 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   fe_to_u256(Y, fe_normalize(fr_to_fe(Y1)));
   st->mark(5);
   uint32_t a[5];
-  pub_address(a, X, Y);
+  pub_address_wave(a, X, Y);  // Keccak across the wave's lanes (keccak_wave.cuh)
   if (lane_id() == 0) {
     const uint32_t pre_st = (meta >> 8) & 0xffu;
     prm.status[idx] = (uint8_t)(pre_st != ST_OK ? pre_st : (ok ? ST_OK : ST_RECOVER_FAILED));
@@ -524,8 +530,13 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   }
   st->mark(6);
   if constexpr (!std::is_same<ST, NoStamp>::value) {
+#ifdef EGES_STAMP_MODINV
+    st_.acc[2] = mprof[0];
+    st_.acc[7] = mprof[1];
+#else
     st_.acc[2] = S.w1t[0];  // wave 1's phases in the unused slots (not part of wave 0's total)
     st_.acc[7] = S.w1t[1];
+#endif
     if (lane_id() == 0) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) stamps[(size_t)blockIdx.x * 8 + i] = st_.acc[i];

@@ -52,9 +52,55 @@ DEV bool s30_ge(const s30& a, const s30& b) {
   return true;
 }
 
+// divsteps_30_var (modinv.cuh) for wave-uniform f, g: the same steps, kept on the scalar ALU (the
+// two-sided min of the lookahead limit would otherwise become a v_min3 and a v_readfirstlane
+// round trip through the VALU in every inner iteration).
+DEV int32_t divsteps_30_var_s(int32_t eta, uint32_t f0, uint32_t g0, trans2x2& t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+  uint32_t f = f0, g = g0;
+  int i = 30;
+#pragma unroll 1
+  for (;;) {
+    const int zeros = __builtin_ctz(g | (0xFFFFFFFFu << i));  // sentinel: at most i
+    g >>= zeros;
+    u <<= zeros;
+    v <<= zeros;
+    eta -= zeros;
+    i -= zeros;
+    if (i == 0) break;
+    if (eta < 0) {  // swap: f, g <- g, -f
+      eta = -eta;
+      const uint32_t tf = f, tu = u, tv = v;
+      f = g;
+      u = q;
+      v = r;
+      g = 0u - tf;
+      q = 0u - tu;
+      r = 0u - tv;
+    }
+    int limit = eta + 1 < i ? eta + 1 : i;
+    asm volatile("" : "+s"(limit));  // s_min_i32, then s_min_i32 (no VALU min3)
+    limit = limit < 12 ? limit : 12;
+    uint32_t x = f;   // f^-1 mod 2^3
+    x *= 2u - f * x;  // mod 2^6
+    x *= 2u - f * x;  // mod 2^12
+    const uint32_t m = (0xFFFFFFFFu >> (32 - limit));
+    const uint32_t w = (g * (0u - x)) & m;
+    g += f * w;
+    q += u * w;
+    r += v * w;
+  }
+  t.u = (int32_t)u;
+  t.v = (int32_t)v;
+  t.q = (int32_t)q;
+  t.r = (int32_t)r;
+  return eta;
+}
+
 // x^-1 mod M for x in [0, M), x wave-uniform (0 maps to 0)
+// prof (diagnostic builds only): accumulates [0] divsteps ticks, [1] state-update ticks
 template <class Mod>
-DEV void modinv256_row_var(uint32_t out[8], const uint32_t x[8]) {
+DEV void modinv256_row_var(uint32_t out[8], const uint32_t x[8], uint64_t* prof = nullptr) {
   const uint32_t L = row_lane();
   const s30 xs = s30_from_u256(x);
   int32_t f = 0, g = 0, m = 0;
@@ -69,7 +115,9 @@ DEV void modinv256_row_var(uint32_t out[8], const uint32_t x[8]) {
 #pragma unroll 1
   for (int it = 0; it < 26; ++it) {
     trans2x2 t;
-    eta = divsteps_30_var(eta, (uint32_t)__builtin_amdgcn_readlane(f, 0), (uint32_t)__builtin_amdgcn_readlane(g, 0), t);
+    const uint64_t p0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+    eta = divsteps_30_var_s(eta, (uint32_t)__builtin_amdgcn_readlane(f, 0), (uint32_t)__builtin_amdgcn_readlane(g, 0), t);
+    const uint64_t p1 = prof ? __builtin_amdgcn_s_memtime() : 0;
     // update_de_30's correction, from lane 0's limbs and the top limbs' signs
     const int32_t d0 = __builtin_amdgcn_readlane(d, 0), e0 = __builtin_amdgcn_readlane(e, 0);
     const int32_t sd = __builtin_amdgcn_readlane(d, 8) >> 31, se = __builtin_amdgcn_readlane(e, 8) >> 31;
@@ -88,7 +136,12 @@ DEV void modinv256_row_var(uint32_t out[8], const uint32_t x[8]) {
     g = row_shift30(cg);
     d = row_shift30(cd);
     e = row_shift30(ce);
-    if (!__any(g != 0)) break;
+    const bool done = !__any(g != 0);
+    if (prof) {
+      prof[0] += p1 - p0;
+      prof[1] += __builtin_amdgcn_s_memtime() - p1;
+    }
+    if (done) break;
   }
   // exact values on the scalar ALU: f = +-1, d == +-x^-1 (mod M)
   s30 fv, dv, mv;
@@ -133,10 +186,10 @@ DEV sc sc_inv_row_var(const sc& a) {
 }
 
 // Z^-1 in the latency kernel: value replicated over the rows in, same out (row form)
-DEV fr fr_inv_var(fr a) {
+DEV fr fr_inv_var(fr a, uint64_t* prof = nullptr) {
   uint32_t x[8], y[8];
   fe_to_u256(x, fe_normalize(fr_to_fe(a)));
-  modinv256_row_var<ModP>(y, x);
+  modinv256_row_var<ModP>(y, x, prof);
   return fe_to_fr(fe_from_u256(y));
 }
 
