@@ -17,6 +17,8 @@
 //   y = sqrt(c), u1 G by a comb table .... the helper wave, beside the Strauss loop
 //   back to E: (X, Y, Z) -> (X, Y, Z y); + u1 G; Z^-1 (limb-parallel safegcd), affine,
 //   serialize, Keccak address (scalar ALU); lane 0 stores.
+#include <atomic>
+#include <cstdlib>
 #include <type_traits>
 
 #include "core.cuh"
@@ -301,7 +303,9 @@ DEV bool lift_y(fr& y, const fr& c, bool odd) {
 DEV void helper_wave(LatLds& S, const uint32_t* gcomb, bool need_y, const fr& c, bool odd, const fr& y_given) {
   fr y = y_given;
   bool ok = true;
+#ifndef EGES_PROBE_NO_SQRT  // diagnostic probe only: the narrow form's time without the root
   if (need_y) ok = lift_y(y, c, odd);
+#endif
   S.ylift[row_lane()] = y.v;
   if (lane_id() == 0) S.yok = ok ? 1u : 0u;
   gejr A;
@@ -366,8 +370,15 @@ DEV void high_wave(LatLds& S, const fr& x, const fr& c, int j) {
 // on E, and the table's isomorphic curve adds the factor zeta. y comes from LDS (helper wave).
 // Narrow: both GLV halves over every window here, two barriers. Split: the low windows of both
 // halves here; the high windows' sum (waves 2, 3) and u_g G (wave 1) are joined at the end.
+DEV void root_fetch(const RecoverParams& prm, uint32_t idx, const fr& c, bool odd, LatLds& S);  // below
+struct RootSrc {  // narrow recover form: where wave 0 finds R's y (root_fetch)
+  const RecoverParams* prm;
+  uint32_t idx;
+  bool odd;
+};
 template <class ST, bool SPLIT>
-DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& S, ST* st) {
+DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& S, ST* st,
+                         const RootSrc* root = nullptr) {
   ger Rp;
   fr_mul2(Rp.x, Rp.y, c, x, c, c);  // (c x, c^2)
   const fr zeta = build_table_wave(Rp, S.tab, S.zr);
@@ -381,6 +392,7 @@ DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& 
   strauss_win_exact(A, ainf, S, S.tab, S.btab, 3, 0, SPLIT ? SPLIT_W0 : RWIN);
   if (SPLIT) flag_wait(&S.flag[F_Y]);
   else __syncthreads();  // partial sums (and y) ready
+  if (root) root_fetch(*root->prm, root->idx, c, root->odd, S);  // (this wave's own LDS words)
   A.z = fr_mul(A.z, fr_mul(zeta, fr{S.ylift[row_lane()]}));  // the true curve
   bool ginf;
   if (SPLIT) flag_wait(&S.flag[F_G]);
@@ -395,6 +407,115 @@ DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& 
   st->mark(4);
 }
 
+// ---- R's y for the narrow form, lane-serially in helper workgroups.
+// At block sizes (n = 1000) two waves share every SIMD and the kernel is bound by total issue;
+// wave 1's row-form square root (253 dependent squarings, one row of four busy) was a fifth of
+// it. Instead the launch's first ceil(n / 128) workgroups give every signature one lane of a
+// lane-serial root (ge_set_xo, ge.cuh) and publish y in the slot rows (unused by this kernel):
+// words 0..7 y, 8 ok, 9 epoch tag, 10 ready tag (release, agent scope: readers may sit on
+// another XCD). Wave 0 reads it after its Strauss loop; if it is not there within a bound, wave 0
+// computes the root itself, so the result never depends on the helpers being scheduled.
+constexpr uint32_t ROOT_TAG = 0x9E3779B9u, ROOT_TAG2 = 0x7F4A7C15u;
+constexpr int ROOT_WORDS = 11;
+constexpr int ROOT_WG = LAT_WG;  // helper lanes per workgroup (same block size as the kernel)
+DEV uint32_t* root_area(const RecoverParams& prm) {
+  return const_cast<uint32_t*>(prm.rec) + (size_t)REC_ROWS * prm.n_pad;
+}
+
+struct LatParse {
+  sc R, Sv, Z;
+  uint32_t xr[8];
+  uint32_t meta, recid;
+  bool ok;
+};
+// the signature's scalars, R's x and the pre-check status (main_impl.h:38-121); wave-uniform in
+// the row-form waves, per lane in the helpers
+DEV LatParse lat_parse(const RecoverParams& prm, uint32_t idx) {
+  LatParse q;
+  uint32_t rl[8], sl[8], zl[8];
+  if (prm.raw_sig) {  // fused prep: prep_ecrecover_kernel's parse (k_prep.hip), same record
+    const uint8_t* sg = prm.raw_sig + (size_t)idx * 65;
+    limbs_from_be32(zl, prm.raw_msg + (size_t)idx * 32);
+    limbs_from_be32(rl, sg);
+    limbs_from_be32(sl, sg + 32);
+    const uint32_t v = sg[64];
+    q.meta = v >= 4 ? (ST_INVALID_RECOVERY_ID << 8) : v;  // checkSignature, secp256.go:171-179
+  } else {
+    rec_get(prm, 8, idx, rl);
+    rec_get(prm, 16, idx, sl);
+    rec_get(prm, 0, idx, zl);
+    q.meta = prm.rec[(size_t)24 * prm.n_pad + idx];
+  }
+  q.recid = q.meta & 3u;
+  q.ok = ((q.meta >> 8) & 0xffu) == ST_OK;
+  bool ovr, ovs, ovz;
+  q.R = sc_from_limbs(rl, ovr);
+  q.Sv = sc_from_limbs(sl, ovs);
+  q.Z = sc_from_limbs(zl, ovz);  // msg mod n (main_impl.h:183)
+  q.ok = q.ok && !ovr && !ovs && !sc_is_zero(q.R) && !sc_is_zero(q.Sv);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q.xr[i] = q.R.v[i];
+  if (q.recid & 2u) {  // x = r + n, only when r < p - n (main_impl.h:101-109)
+    q.ok = q.ok && !u256_ge(q.R.v, P_MINUS_N);
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      c += (uint64_t)q.xr[i] + SC_N[i];
+      q.xr[i] = (uint32_t)c;
+      c >>= 32;
+    }
+  }
+  return q;
+}
+
+DEV void root_helper(const RecoverParams& prm) {
+  const uint32_t j = blockIdx.x * ROOT_WG + threadIdx.x;
+  if (j >= prm.n) return;
+  const LatParse q = lat_parse(prm, j);
+  const ge G = gen_point();
+  const fe x = q.ok ? fe_from_u256(q.xr) : G.x;  // the row-form waves use the same substitute
+  ge r;
+  const bool ok = ge_set_xo(r, x, q.ok && (q.recid & 1u) != 0);
+  uint32_t y[8];
+  fe_to_u256(y, r.y);
+  uint32_t* a = root_area(prm);
+  const size_t np = prm.n_pad;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i * np + j] = y[i];
+  a[8 * np + j] = ok ? 1u : 0u;
+  a[9 * np + j] = prm.epoch ^ ROOT_TAG2;
+  __hip_atomic_store(&a[10 * np + j], prm.epoch ^ ROOT_TAG, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// wave 0 of signature idx: y and ok into LDS, from the helpers or (bounded wait) computed here
+DEV void root_fetch(const RecoverParams& prm, uint32_t idx, const fr& c, bool odd, LatLds& S) {
+  uint32_t* a = root_area(prm);
+  const size_t np = prm.n_pad;
+  bool got = false;
+#pragma unroll 1
+  for (int it = 0; it < 40000; ++it) {  // ~4 ms: the helpers normally finish long before
+    if (__hip_atomic_load(&a[10 * np + idx], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == (prm.epoch ^ ROOT_TAG) &&
+        __hip_atomic_load(&a[9 * np + idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (prm.epoch ^ ROOT_TAG2)) {
+      got = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+  fr y;
+  bool ok;
+  if (got) {
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = __hip_atomic_load(&a[i * np + idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    y = fe_to_fr(fe_from_u256(w));
+    ok = __hip_atomic_load(&a[8 * np + idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  } else {
+    ok = lift_y(y, c, odd);
+  }
+  S.ylift[row_lane()] = y.v;
+  if (lane_id() == 0) S.yok = ok ? 1u : 0u;
+}
+
 // Phase marks of wave 0 (diagnostic build only): 0 parse + x, c, 3 table, 1 wait for wave 1's
 // r^-1 / u1 / u2 / digits, 4 Strauss + join (including the waits for the other parts and y),
 // 5 Z^-1 + affine, 6 Keccak + stores.
@@ -407,48 +528,27 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   __shared__ LatLds S;
   ST st_;
   ST* st = &st_;
-  const uint32_t idx = blockIdx.x;  // grid = n: every wave has a signature
-  const uint32_t np = prm.n_pad;
+  if (!SPLIT && blockIdx.x < prm.n_helpers) {  // narrow form: the lane-serial roots
+    root_helper(prm);
+    return;
+  }
+  const uint32_t idx = blockIdx.x - (SPLIT ? 0u : prm.n_helpers);  // every wave has a signature
+  // the helpers' lane-serial roots are a dense VALU stream: the signature waves (latency-bound
+  // chains) take issue priority over them on a shared SIMD
+  if (!SPLIT) __builtin_amdgcn_s_setprio(2);
   if (SPLIT) {
     if (threadIdx.x < NFLAGS) S.flag[threadIdx.x] = 0u;
     __syncthreads();  // the only barrier of the split form
   }
   // --- parse (every lane reads the same record)
-  uint32_t rl[8], sl[8], zl[8];
-  uint32_t meta;
-  if (prm.raw_sig) {  // fused prep: prep_ecrecover_kernel's parse (k_prep.hip), same record
-    const uint8_t* sg = prm.raw_sig + (size_t)idx * 65;
-    limbs_from_be32(zl, prm.raw_msg + (size_t)idx * 32);
-    limbs_from_be32(rl, sg);
-    limbs_from_be32(sl, sg + 32);
-    const uint32_t v = sg[64];
-    meta = v >= 4 ? (ST_INVALID_RECOVERY_ID << 8) : v;  // checkSignature, secp256.go:171-179
-  } else {
-    rec_get(prm, 8, idx, rl);
-    rec_get(prm, 16, idx, sl);
-    rec_get(prm, 0, idx, zl);
-    meta = prm.rec[(size_t)24 * np + idx];
-  }
-  const uint32_t recid = meta & 3u;
-  bool ok = ((meta >> 8) & 0xffu) == ST_OK;
-  bool ovr, ovs, ovz;
-  sc R = sc_from_limbs(rl, ovr);
-  const sc Sv = sc_from_limbs(sl, ovs);
-  const sc Z = sc_from_limbs(zl, ovz);  // msg mod n (main_impl.h:183)
-  ok = ok && !ovr && !ovs && !sc_is_zero(R) && !sc_is_zero(Sv);
+  const LatParse q = lat_parse(prm, idx);
+  const uint32_t meta = q.meta, recid = q.recid;
+  bool ok = q.ok;
+  sc R = q.R;
+  const sc Sv = q.Sv, Z = q.Z;
   uint32_t xr[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) xr[i] = R.v[i];
-  if (recid & 2u) {  // x = r + n, only when r < p - n (main_impl.h:101-109)
-    ok = ok && !u256_ge(R.v, P_MINUS_N);
-    uint64_t c = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      c += (uint64_t)xr[i] + SC_N[i];
-      xr[i] = (uint32_t)c;
-      c >>= 32;
-    }
-  }
+  for (int i = 0; i < 8; ++i) xr[i] = q.xr[i];
   // R's x; signatures that fail the parse carry the generator's x (even y), so every later step
   // stays well-defined. c = x^3 + 7 = y^2 (ge_set_xo_var, group_impl.h:216-237).
   const ge G = gen_point();
@@ -476,7 +576,7 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
       helper_split(S, gcomb, true, c, odd, fr_zero());
     } else {
       __syncthreads();  // digits ready (and the table)
-      helper_wave(S, gcomb, true, c, odd, fr_zero());
+      helper_wave(S, gcomb, false, c, odd, fr_zero());  // y: the helper workgroups (root_fetch)
     }
     return;
   }
@@ -488,7 +588,8 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   // --- Q = u2 R + u1 G, R's y (the square root) computed beside the Strauss loop
   gejr Q;
   bool qinf;
-  ecmult_deferred<ST, SPLIT>(Q, qinf, x, c, S, st);
+  const RootSrc root{&prm, idx, odd};
+  ecmult_deferred<ST, SPLIT>(Q, qinf, x, c, S, st, SPLIT ? nullptr : &root);
   ok = ok && S.yok != 0 && !qinf;  // ge_set_xo_var failure, main_impl.h:120
   // --- affine, serialize, address
   const fr zq = fr_select(ok, Q.z, fr_one());
@@ -539,7 +640,7 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
 #endif
     if (lane_id() == 0) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) stamps[(size_t)blockIdx.x * 8 + i] = st_.acc[i];
+      for (int i = 0; i < 8; ++i) stamps[(size_t)idx * 8 + i] = st_.acc[i];
     }
   }
 }
@@ -654,10 +755,22 @@ __global__ void __launch_bounds__(LAT_WG_SPLIT) recover_lat_split_kernel(Recover
   recover_lat_body<NoStamp, true>(prm, nullptr);
 }
 
-hipError_t launch_recover_lat(const RecoverParams& p, hipStream_t st) {
-  if (p.n == 0) return hipSuccess;
+// the narrow form's launch: ceil(n / 128) root-helper workgroups first (dispatched before the
+// signatures' workgroups), tagged with a per-launch epoch so stale slot-row words never match
+static std::atomic<uint32_t> g_root_epoch{0};
+static RecoverParams with_helpers(const RecoverParams& p0) {
+  RecoverParams p = p0;
+  p.n_helpers = p.wide ? 0u : (p.n + ROOT_WG - 1) / ROOT_WG;
+  // tests only: no helper workgroups, so every signature wave takes root_fetch's own-root path
+  if (const char* e = std::getenv("EGES_TEST_ROOT_HELPERS"); e && *e == '0') p.n_helpers = 0;
+  p.epoch = g_root_epoch.fetch_add(1) + 1u;
+  return p;
+}
+hipError_t launch_recover_lat(const RecoverParams& p0, hipStream_t st) {
+  if (p0.n == 0) return hipSuccess;
+  const RecoverParams p = with_helpers(p0);
   if (p.wide) hipLaunchKernelGGL(recover_lat_split_kernel, dim3(p.n), dim3(LAT_WG_SPLIT), 0, st, p);
-  else hipLaunchKernelGGL(recover_lat_kernel, dim3(p.n), dim3(LAT_WG), 0, st, p);
+  else hipLaunchKernelGGL(recover_lat_kernel, dim3(p.n_helpers + p.n), dim3(LAT_WG), 0, st, p);
   return hipGetLastError();
 }
 
@@ -668,10 +781,11 @@ __global__ void __launch_bounds__(LAT_WG) recover_lat_kernel_stamped(RecoverPara
 __global__ void __launch_bounds__(LAT_WG_SPLIT) recover_lat_split_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
   recover_lat_body<Stamper, true>(prm, stamps);
 }
-hipError_t launch_recover_lat_stamped(const RecoverParams& p, hipStream_t st, uint64_t* stamps) {
-  if (p.n == 0) return hipSuccess;
+hipError_t launch_recover_lat_stamped(const RecoverParams& p0, hipStream_t st, uint64_t* stamps) {
+  if (p0.n == 0) return hipSuccess;
+  const RecoverParams p = with_helpers(p0);
   if (p.wide) hipLaunchKernelGGL(recover_lat_split_kernel_stamped, dim3(p.n), dim3(LAT_WG_SPLIT), 0, st, p, stamps);
-  else hipLaunchKernelGGL(recover_lat_kernel_stamped, dim3(p.n), dim3(LAT_WG), 0, st, p, stamps);
+  else hipLaunchKernelGGL(recover_lat_kernel_stamped, dim3(p.n_helpers + p.n), dim3(LAT_WG), 0, st, p, stamps);
   return hipGetLastError();
 }
 size_t lat_waves(uint32_t n) { return n; }

@@ -36,8 +36,11 @@ struct RecoverParams {
   // (prep_ecrecover_kernel fused away for small ecrecover calls)
   const uint8_t* raw_msg = nullptr;
   const uint8_t* raw_sig = nullptr;
-  // latency kernel only: three waves per signature (R / lambda R / G partial sums in parallel)
+  // latency kernel only: the split form (four waves per signature, k_recover_lat.hip)
   uint32_t wide = 0;
+  // latency kernel, narrow form: leading workgroups that compute R's y lane-serially (one lane
+  // per signature) into the slot rows, tagged with this launch's epoch (set by the launcher)
+  uint32_t n_helpers = 0, epoch = 0;
 };
 
 struct VerifyParams {

@@ -75,6 +75,24 @@ def test_lat_kernel_golden_recover(engine):
     assert np.array_equal(addr, addr2) and np.array_equal(st, st2)
 
 
+class root_helpers(env_knob):  # 0: the narrow form launches no root-helper workgroups
+    name = "EGES_TEST_ROOT_HELPERS"
+
+
+def test_narrow_root_fetch_fallback_golden(engine):
+    """The narrow form's R.y normally comes from its lane-serial root-helper workgroups
+    (k_recover_lat.hip root_helper / root_fetch). Without them every signature wave waits out
+    root_fetch's bound and takes its own-root path: every golden item must still match the
+    fixtures byte for byte (and the helper path's result)."""
+    g = load_golden("recover.npz")
+    with lat_max(1 << 20), wide_max(0):
+        pub, addr, st = engine.ecrecover_batch(g["msg"], g["sig"])
+        with root_helpers(0):
+            pub2, addr2, st2 = engine.ecrecover_batch(g["msg"], g["sig"])
+    assert np.array_equal(st, g["status"]) and np.array_equal(pub, g["pub"])
+    assert np.array_equal(pub, pub2) and np.array_equal(addr, addr2) and np.array_equal(st, st2)
+
+
 def test_lat_kernel_golden_sender(engine):
     g = load_golden("sender.npz")
     keys = sorted(set(zip(g["signer"].tolist(), g["chain_id"].tolist())))

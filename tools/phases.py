@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from eges_amd import _lib  # noqa: E402
 
-lib = ctypes.CDLL(os.path.join(ROOT, "eges_amd", "libeges_diag.so"))
+lib = ctypes.CDLL(os.path.join(ROOT, "eges_amd", os.environ.get("EGES_DIAG_LIB", "libeges_diag.so")))
 for name, (res, args) in _lib.SIGNATURES.items():
     f = getattr(lib, name)
     f.restype, f.argtypes = res, args
@@ -48,7 +48,8 @@ for it in range(2):
     assert rc == 0, lib.eges_last_error()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-assert bool((addr == exp).all()) and int(status.max()) == 0, "diag build disagrees with synth addresses"
+if not os.environ.get("EGES_PROBE"):  # probe builds compute wrong results on purpose
+    assert bool((addr == exp).all()) and int(status.max()) == 0, "diag build disagrees with synth addresses"
 waves = lib.eges_diag_read_stamps(None, 1 << 30)
 buf = (ctypes.c_uint64 * (waves * 8))()
 lib.eges_diag_read_stamps(buf, waves)
