@@ -37,6 +37,12 @@ constexpr int LAT_WG = 128;
 #endif
 constexpr int SPLIT_W0 = EGES_SPLIT_W0;
 static_assert(SPLIT_W0 > 0 && SPLIT_W0 < RWIN, "split point");
+// the high part (bits from RBITS * SPLIT_W0 up, < 2^(130 - RBITS SPLIT_W0) with the recoding
+// carry) in signed 4-bit windows against an 8-entry table of D: half the table build of a
+// 16-entry one for a few more additions on the high waves' chain
+constexpr int HBITS = 4;
+constexpr int HTAB = 1 << (HBITS - 1);
+constexpr int HWIN = (130 - RBITS * SPLIT_W0 + HBITS) / HBITS;
 
 // LDS flags of the split form (set once by their producer wave, polled by the consumers)
 enum { F_DIG = 0, F_Y, F_G, F_LHI, F_HI, NFLAGS };
@@ -45,10 +51,11 @@ struct LatLds {
   uint32_t tab[PTAB][2][16];  // {1..16} * R' (x, y), row form (all four rows read the same words)
   uint32_t zr[PTAB][16];      // Z ratios while the table is built
   uint32_t btab[PTAB][16];    // beta x of the table entries (the lambda R' additions)
-  uint32_t dtab[2][PTAB][2][16];  // split form: {1..16} * D, one copy per high-part wave
-  uint32_t dzr[2][PTAB][16];
-  uint32_t dbtab[PTAB][16];       //   and beta x for the lambda half (wave 3)
+  uint32_t dtab[2][HTAB][2][16];  // split form: {1..8} * D, one copy per high-part wave
+  uint32_t dzr[2][HTAB][16];
+  uint32_t dbtab[HTAB][16];       //   and beta x for the lambda half (wave 3)
   int8_t rdig[2][RWIN];       // R / lambda R window digits
+  int8_t hdig[2][HWIN];       // split form: the high parts in 4-bit windows
   uint16_t cdig[CWIN];        // comb digits of u_g
   uint32_t part[5][3][16];    // partial sums (X, Y, Z): [2] u_g G, [3] high parts, [4] lambda high part
   uint32_t pinf[5];           //   and their infinity flags
@@ -142,24 +149,57 @@ DEV void add_r(gejr& acc, bool& inf, const ger& p, bool use) {
   inf = use ? (inf ? false : to_inf) : inf;
 }
 
-// GLV split of u_r into signed 5-bit windows (core.cuh ecmult_core's digits), u_g for the comb
+// split form: SPLIT_W0 signed RBITS-bit windows, then (carry included) HWIN signed HBITS-bit ones,
+// so that h = sum lo_w 2^(RBITS w) + 2^(RBITS SPLIT_W0) sum hi_w 2^(HBITS w)
+template <int W>
+DEV void recode_step(uint32_t m[5], int& carry, bool neg, int8_t& out) {
+  int v = (int)(m[0] & ((1u << W) - 1)) + carry;
+  carry = v > (1 << (W - 1)) ? 1 : 0;
+  v -= carry << W;
+  out = (int8_t)(neg ? -v : v);  // every lane writes the same value
+#pragma unroll
+  for (int i = 0; i < 4; ++i) m[i] = (m[i] >> W) | (m[i + 1] << (32 - W));
+  m[4] >>= W;
+}
+DEV void recode_split(const glv_half& h, int8_t* lo, int8_t* hi) {
+  uint32_t m[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) m[i] = h.mag[i];
+  int carry = 0;
+#pragma unroll 1
+  for (int w = 0; w < SPLIT_W0; ++w) recode_step<RBITS>(m, carry, h.neg, lo[w]);
+#pragma unroll 1
+  for (int w = 0; w < HWIN; ++w) recode_step<HBITS>(m, carry, h.neg, hi[w]);
+}
+
+// GLV split of u_r into signed 5-bit windows (core.cuh ecmult_core's digits; the split form's
+// high part in 4-bit ones), u_g for the comb
+template <bool SPLIT>
 DEV void recode_digits(const sc& u_r, const sc& u_g, LatLds& S) {
   glv_half h1, h2;
   glv_split(h1, h2, u_r);
-  recode_row<RBITS, RWIN, int8_t>(h1, S.rdig[0]);
-  recode_row<RBITS, RWIN, int8_t>(h2, S.rdig[1]);
+  if (SPLIT) {
+    recode_split(h1, S.rdig[0], S.hdig[0]);
+    recode_split(h2, S.rdig[1], S.hdig[1]);
+  } else {
+    recode_row<RBITS, RWIN, int8_t>(h1, S.rdig[0]);
+    recode_row<RBITS, RWIN, int8_t>(h2, S.rdig[1]);
+  }
   // u_g in unsigned 16-bit digits for the comb (every lane writes the same values)
 #pragma unroll
   for (int k = 0; k < CWIN; ++k) S.cdig[k] = (uint16_t)(u_g.v[k >> 1] >> (16 * (k & 1)));
 }
 
-using TabT = uint32_t[PTAB][2][16];
-using ColT = uint32_t[PTAB][16];
+template <int NT>
+using TabT = uint32_t[NT][2][16];
+template <int NT>
+using ColT = uint32_t[NT][16];
 
 // table {1..PTAB} * P on one global Z (co-Z additions, backward rescale; core.cuh); returns zeta.
 // P may be the (X, Y) of a Jacobian point: the formulas do not involve the curve's b, so the
 // entries are then points of the curve y^2 = x^3 + b Z^6 on which (X, Y) is affine.
-DEV fr build_table_wave(const ger& P, TabT& tab, ColT& zrs) {
+template <int NT>
+DEV fr build_table_wave(const ger& P, TabT<NT>& tab, ColT<NT>& zrs) {
   fr zeta;
   {
     const uint32_t L = row_lane();
@@ -173,17 +213,17 @@ DEV fr build_table_wave(const ger& P, TabT& tab, ColT& zrs) {
     T.y = D.y;
     lds_put_pt(tab[1], T);
 #pragma unroll 1
-    for (int i = 2; i < PTAB; ++i) {
+    for (int i = 2; i < NT; ++i) {
       const fr zr = gejq_zaddu(T, B);  // T = (i+1) P
       lds_put_pt(tab[i], T);
       zrs[i - 1][L] = zr.v;
     }
-    // entry i (< PTAB - 1) is rescaled by rho_i = prod_{k=i}^{PTAB-2} Z_{k+2}/Z_{k+1} = Z_PTAB / Z_{i+1}:
+    // entry i (< NT - 1) is rescaled by rho_i = prod_{k=i}^{NT-2} Z_{k+2}/Z_{k+1} = Z_NT / Z_{i+1}:
     // x rho^2, y rho^3, software-pipelined two quad steps per entry
-    fr rho{zrs[PTAB - 2][L]};
+    fr rho{zrs[NT - 2][L]};
     fr s2 = fr_sqr(rho);
 #pragma unroll 1
-    for (int i = PTAB - 2; i >= 0; --i) {
+    for (int i = NT - 2; i >= 0; --i) {
       const ger J = lds_pt(tab[i]);
       const fr zn{zrs[i > 0 ? i - 1 : 0][L]};
       fr ax, s3, rho_n;
@@ -198,7 +238,7 @@ DEV fr build_table_wave(const ger& P, TabT& tab, ColT& zrs) {
       rho = rho_n;
       s2 = s2_n;
     }
-    zeta = rho;  // rho_0 = Z_PTAB / Z_1 with Z_1 = 1
+    zeta = rho;  // rho_0 = Z_NT / Z_1 with Z_1 = 1
   }
   return zeta;
 }
@@ -210,9 +250,9 @@ DEV fr build_table_wave(const ger& P, TabT& tab, ColT& zrs) {
 // Windows [wlo, whi) of the GLV halves selected by jmask (bit 0: R digits against tab, bit 1:
 // lambda R digits against (btab, tab.y)), Horner from the top window: 5 doublings per window and
 // one addition per selected half. The narrow form runs [0, RWIN) with both halves.
-template <bool CHECKED>
-DEV void strauss_win(gejr& acc, bool& inf, const LatLds& S, const TabT& tab, const ColT& btab, int jmask, int wlo,
-                     int whi) {
+template <bool CHECKED, int BITS, int NT>
+DEV void strauss_win(gejr& acc, bool& inf, const TabT<NT>& tab, const ColT<NT>& btab, const int8_t* d0,
+                     const int8_t* d1, int jmask, int wlo, int whi) {
   inf = true;
   acc.x = fr_zero();
   acc.y = fr_zero();
@@ -221,12 +261,12 @@ DEV void strauss_win(gejr& acc, bool& inf, const LatLds& S, const TabT& tab, con
   for (int w = whi - 1; w >= wlo; --w) {
     if (w != whi - 1) {
 #pragma unroll 1
-      for (int k = 0; k < RBITS; ++k) acc = gejq_double(acc);
+      for (int k = 0; k < BITS; ++k) acc = gejq_double(acc);
     }
 #pragma unroll 1
     for (int j = 0; j < 2; ++j) {
       if (!((jmask >> j) & 1)) continue;
-      const int d = (int)S.rdig[j][w];
+      const int d = (int)(j ? d1 : d0)[w];
       const int a = d < 0 ? -d : d;
       const int e = a > 0 ? a - 1 : 0;
       ger p = lds_pt(tab[e]);
@@ -235,11 +275,11 @@ DEV void strauss_win(gejr& acc, bool& inf, const LatLds& S, const TabT& tab, con
     }
   }
 }
-template <bool UNUSED = false>
-DEV void strauss_win_exact(gejr& acc, bool& inf, const LatLds& S, const TabT& tab, const ColT& btab, int jmask,
-                           int wlo, int whi) {
-  strauss_win<false>(acc, inf, S, tab, btab, jmask, wlo, whi);
-  if (__any(!inf && fr_is_zero(acc.z))) strauss_win<true>(acc, inf, S, tab, btab, jmask, wlo, whi);
+template <int BITS, int NT>
+DEV void strauss_win_exact(gejr& acc, bool& inf, const TabT<NT>& tab, const ColT<NT>& btab, const int8_t* d0,
+                           const int8_t* d1, int jmask, int wlo, int whi) {
+  strauss_win<false, BITS, NT>(acc, inf, tab, btab, d0, d1, jmask, wlo, whi);
+  if (__any(!inf && fr_is_zero(acc.z))) strauss_win<true, BITS, NT>(acc, inf, tab, btab, d0, d1, jmask, wlo, whi);
 }
 // u_g G from the comb table: one addition per 16-bit digit, no doublings (true curve).
 template <bool CHECKED>
@@ -272,11 +312,12 @@ DEV gejr get_part(const LatLds& S, int k, bool& inf) {
   return a;
 }
 // beta x of the 16 table entries, four per quad step
-DEV void build_btab(const TabT& tab, ColT& btab) {
+template <int NT>
+DEV void build_btab(const TabT<NT>& tab, ColT<NT>& btab) {
   const fr beta = fe_to_fr(fe_const(FE_BETA));
   const uint32_t L = row_lane();
 #pragma unroll 1
-  for (int i = 0; i < PTAB; i += 4) {
+  for (int i = 0; i < NT; i += 4) {
     fr b0, b1, b2, b3;
     fr_mul4(b0, b1, b2, b3, lds_pt(tab[i]).x, beta, lds_pt(tab[i + 1]).x, beta, lds_pt(tab[i + 2]).x, beta,
             lds_pt(tab[i + 3]).x, beta);
@@ -343,13 +384,13 @@ DEV void high_wave(LatLds& S, const fr& x, const fr& c, int j) {
   ger Dp;
   Dp.x = D.x;
   Dp.y = D.y;
-  const fr zd = build_table_wave(Dp, S.dtab[j], S.dzr[j]);
-  if (j == 1) build_btab(S.dtab[1], S.dbtab);
+  const fr zd = build_table_wave<HTAB>(Dp, S.dtab[j], S.dzr[j]);
+  if (j == 1) build_btab<HTAB>(S.dtab[1], S.dbtab);
   const fr scale = fr_mul(zd, D.z);
   flag_wait(&S.flag[F_DIG]);
   gejr A;
   bool ainf;
-  strauss_win_exact(A, ainf, S, S.dtab[j], S.dbtab, 1 << j, SPLIT_W0, RWIN);
+  strauss_win_exact<HBITS, HTAB>(A, ainf, S.dtab[j], S.dbtab, S.hdig[0], S.hdig[1], 1 << j, 0, HWIN);
   flag_wait(&S.flag[F_Y]);
   A.z = fr_mul(A.z, fr_mul(scale, fr{S.ylift[row_lane()]}));
   if (j == 1) {
@@ -381,15 +422,15 @@ DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& 
                          const RootSrc* root = nullptr) {
   ger Rp;
   fr_mul2(Rp.x, Rp.y, c, x, c, c);  // (c x, c^2)
-  const fr zeta = build_table_wave(Rp, S.tab, S.zr);
-  build_btab(S.tab, S.btab);
+  const fr zeta = build_table_wave<PTAB>(Rp, S.tab, S.zr);
+  build_btab<PTAB>(S.tab, S.btab);
   st->mark(3);
   if (SPLIT) flag_wait(&S.flag[F_DIG]);
   else __syncthreads();  // digits ready
   st->mark(1);
   gejr A;
   bool ainf;
-  strauss_win_exact(A, ainf, S, S.tab, S.btab, 3, 0, SPLIT ? SPLIT_W0 : RWIN);
+  strauss_win_exact<RBITS, PTAB>(A, ainf, S.tab, S.btab, S.rdig[0], S.rdig[1], 3, 0, SPLIT ? SPLIT_W0 : RWIN);
   if (SPLIT) flag_wait(&S.flag[F_Y]);
   else __syncthreads();  // partial sums (and y) ready
   if (root) root_fetch(*root->prm, root->idx, c, root->odd, S);  // (this wave's own LDS words)
@@ -566,7 +607,7 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
     const uint64_t t1 = stamped ? __builtin_amdgcn_s_memtime() : 0;
     const sc u1 = sc_neg(sc_mul(rinv, Z));
     const sc u2 = sc_select(ok, sc_mul(rinv, Sv), sc_one());
-    recode_digits(u2, u1, S);
+    recode_digits<SPLIT>(u2, u1, S);
     if (stamped && lane_id() == 0) {
       S.w1t[0] = t1 - t0;
       S.w1t[1] = __builtin_amdgcn_s_memtime() - t1;
@@ -698,7 +739,7 @@ DEV void verify_lat_body(const VerifyParams& prm) {
     const sc sinv = sc_inv_row_var(sc_select(sig_ok, Sv, sc_one()));
     const sc u1 = sc_mul(sinv, Z);
     const sc u2 = sc_select(sig_ok, sc_mul(sinv, R), sc_one());
-    recode_digits(u2, u1, S);
+    recode_digits<SPLIT>(u2, u1, S);
     // the square root only for 33-byte keys; 65-byte keys give y
     if (SPLIT) {
       flag_set(&S.flag[F_DIG]);

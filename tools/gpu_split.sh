@@ -1,6 +1,6 @@
 # Latency-kernel check (via gpurun): latency / fr / concurrency / golden / block / raw parity
-# tests, the stamped phase breakdown at n = 16 and 1000, the native single-item bench (8 callers
-# with the gather window off and on, alternating; 16 callers), the C3 block.
+# tests, the stamped phase breakdown at n = 16 and 1000, the native single-item bench (8 and 16
+# callers), the C3 block.
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -13,10 +13,8 @@ timeout -k 10 120 python tools/phases.py 16 > gpurun_out/phases16.txt 2>&1
 timeout -k 10 120 python tools/phases.py 1000 > gpurun_out/phases1000.txt 2>&1
 tail -9 gpurun_out/phases16.txt; tail -9 gpurun_out/phases1000.txt
 for rep in 1 2; do
-  for g in 0 20; do
-    EGES_COALESCE_GATHER_US=$g timeout -k 10 120 tools/single_bench 8 2000 > gpurun_out/single_g${g}_$rep.json 2>> gpurun_out/single.err
-    echo "gather=$g rep=$rep $(cat gpurun_out/single_g${g}_$rep.json)"
-  done
+  timeout -k 10 120 tools/single_bench 8 2000 > gpurun_out/single8_$rep.json 2>> gpurun_out/single.err
+  cat gpurun_out/single8_$rep.json
 done
 timeout -k 10 120 tools/single_bench 16 2000 > gpurun_out/single16.json 2>> gpurun_out/single.err
 timeout -k 10 200 python bench.py --config c3 --no-cpu-baseline > gpurun_out/c3.json 2> gpurun_out/c3.err
