@@ -193,3 +193,39 @@ def test_lat_kernel_block_latency_record(engine):
             out[name] = float(np.median(ts[2:])) * 1e3
     print(f"\n1000-tx block via eges_sender_batch: latency kernel {out['latency']:.3f} ms, "
           f"lane-serial kernel {out['lane-serial']:.3f} ms")
+
+
+def test_split_boundaries_structured_scalars(engine, oracle):
+    """u2 = s / r chosen so that whole partial sums of the split form are empty or sit at its
+    boundaries: u2 = 1, 2, lambda (GLV halves (0, 1)), 2^k around the split point 2^75 and the
+    5-bit / 4-bit window edges, n - 1, n - lambda; each with u1 = -z / r for three z: 0 (no G
+    part), the golden item's message, and -s (u1 = u2: Q = u2 (R + G)). Every item through the
+    split (4-wave) and the narrow form must equal the oracle (pinned by the reference libsecp256k1)."""
+    from eges_amd.workloads import N
+    lam = 0x5363AD4CC05C30E0A5261C028812645A122E22EA20816678DF02967C1B23BD72
+    g = load_golden("recover.npz")
+    base = [i for i in range(len(g["kind"])) if g["status"][i] == 0][:3]
+    u2s = [1, 2, 3, lam, (N - lam) % N, N - 1, 1 << 74, 1 << 75, (1 << 75) - 1, (1 << 75) + 1, 1 << 76, 1 << 80,
+           1 << 128, (1 << 129) - 1, 1 << 200, 31 << 70, 15 << 75]
+    msgs, sigs = [], []
+    for i in base:
+        sig = g["sig"][i].tobytes()
+        r = int.from_bytes(sig[:32], "big")
+        for u2 in u2s:
+            s = u2 * r % N
+            for z in (0, int.from_bytes(g["msg"][i].tobytes(), "big") % N, (N - s) % N):
+                msgs.append(z.to_bytes(32, "big"))
+                sigs.append(sig[:32] + s.to_bytes(32, "big") + sig[64:])
+    m = np.frombuffer(b"".join(msgs), np.uint8).reshape(-1, 32)
+    sg = np.frombuffer(b"".join(sigs), np.uint8).reshape(-1, 65)
+    assert len(m) <= 256  # the split form
+    with lat_max(1 << 20):
+        pub, addr, st = engine.ecrecover_batch(m, sg)
+        with wide_max(0):
+            pub2, addr2, st2 = engine.ecrecover_batch(m, sg)
+    assert np.array_equal(pub, pub2) and np.array_equal(st, st2)
+    for k in range(len(m)):
+        ost, opub = oracle.recover_pubkey(m[k].tobytes(), sg[k].tobytes())
+        assert int(st[k]) == ost, (k, int(st[k]), ost)
+        if ost == 0:
+            assert pub[k].tobytes() == opub, k
