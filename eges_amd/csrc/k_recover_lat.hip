@@ -14,9 +14,15 @@
 //   table {1..16}R' on one global Z ...... co-Z dblu / zaddu + backward rescale (as core.cuh)
 //   Strauss over 26 windows (u2 R') ...... unchecked adds, exact redo if the accumulator was
 //                                            poisoned (Z == 0 and not infinity)
-//   y = sqrt(c), u1 G by a comb table .... the helper wave, beside the Strauss loop
+//   u1 G by a comb table ................. wave 1, beside the Strauss loop
+//   y = sqrt(c) .......................... narrow form: lane-serial root-helper workgroups at the
+//                                            head of the launch (root_helper / root_fetch);
+//                                            split form: wave 1
 //   back to E: (X, Y, Z) -> (X, Y, Z y); + u1 G; Z^-1 (limb-parallel safegcd), affine,
-//   serialize, Keccak address (scalar ALU); lane 0 stores.
+//   serialize, Keccak address across the wave's lanes (keccak_wave.cuh); lane 0 stores.
+// Forms: narrow (two waves per signature, batches above EGES_LAT_WIDE_MAX) and split (four
+// waves: the doubling chain cut at window SPLIT_W0, its high part on waves 2 / 3 against tables
+// of D = 2^75 R'; batches up to EGES_LAT_WIDE_MAX = 256). DESIGN.md §3.3.
 #include <atomic>
 #include <cstdlib>
 #include <type_traits>
