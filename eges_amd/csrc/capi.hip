@@ -952,6 +952,7 @@ struct Coalescer {
   std::atomic<size_t> qlen{0};   // queue.size(), for the gathering leader
   std::atomic<int> inflight{0};  // groups running or gathering (changed under mu)
   std::atomic<bool> gathering{false};  // a leader is gathering (changed under mu)
+  std::atomic<int> spinners{0};        // callers spinning on their completion flag
   size_t last_group = 1;         // guarded by mu
 
   static std::chrono::microseconds knob(const char* name, int dflt) {
@@ -1005,10 +1006,13 @@ struct Coalescer {
         lead(lk);
         continue;
       }
-      // served by another leader's group, or waiting for a free lane: spin, then block
+      // served by another leader's group, or waiting for a free lane: spin, then block. At most
+      // EGES_COALESCE_SPINNERS callers spin at once: with more spinning threads than the
+      // process's CPUs the leaders that launch and collect the groups get descheduled
+      static const int max_spinners = std::max(0, env_int("EGES_COALESCE_SPINNERS", 8));
       lk.unlock();
-      bool block = false;
-      while (!r->done.load(std::memory_order_acquire)) {
+      bool block = spinners.fetch_add(1, std::memory_order_relaxed) >= max_spinners;
+      while (!block && !r->done.load(std::memory_order_acquire)) {
         if (may_lead(r)) break;
         if (std::chrono::steady_clock::now() - t0 > spin) {
           block = true;
@@ -1016,6 +1020,7 @@ struct Coalescer {
         }
         cpu_relax();
       }
+      spinners.fetch_sub(1, std::memory_order_relaxed);
       lk.lock();
       if (block) cv.wait(lk, [&] { return r->done.load() || may_lead(r); });
     }
