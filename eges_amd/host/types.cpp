@@ -162,7 +162,6 @@ struct Stream {
     return true;
   }
   bool address_or_nil(std::optional<Address>& to) {
-    const size_t save = pos;
     int k;
     size_t size;
     uint8_t bv;
@@ -172,7 +171,6 @@ struct Stream {
       return true;
     }
     if (k == 0 || k == 2 || size != 20) return false;  // [20]byte: too short / long, not a string
-    (void)save;
     Address a;
     std::memcpy(a.data(), b + pos, 20);
     pos += 20;

@@ -107,3 +107,49 @@ def test_coalesced_single_item_callers(engine):
     print(f"\nsingle eges_ecdsa_recover p50 {np.median(ts[20:]) * 1e3:.3f} ms (one caller); "
           f"{nthreads} callers x {per_thread}: {nthreads * per_thread / dt:.0f} recoveries/s, "
           f"p50 {np.median(lat) * 1e3:.3f} ms per call")
+
+
+def test_coalesced_recover_and_verify_many_callers(engine):
+    """24 threads at once, 12 through eges_ecdsa_recover and 12 through eges_ecdsa_verify (the
+    reference's ext.h:30-47 / :58-75 per-call seams): both coalescers share the device's lanes,
+    more callers than the coalescer lets spin (capi.hip EGES_COALESCE_SPINNERS), so the blocking
+    path runs too. Every result against the golden fixtures (recover.npz, verify.npz)."""
+    from eges_amd._lib import lib
+    gr = load_golden("recover.npz")
+    gv = load_golden("verify.npz")
+    ridx = [i for i in range(gr["msg"].shape[0]) if gr["sig"][i, 64] < 4]
+    errors = []
+
+    def rec_worker(t):
+        out = (ctypes.c_ubyte * 65)()
+        try:
+            for k in range(300):
+                i = ridx[(t * 4099 + k * 37) % len(ridx)]
+                rc = lib.eges_ecdsa_recover(out, gr["sig"][i].tobytes(), gr["msg"][i].tobytes())
+                want = 1 if gr["status"][i] == 0 else 0
+                if rc != want or (rc == 1 and bytes(out) != gr["pub"][i].tobytes()):
+                    errors.append(("recover", t, k, i, rc))
+        except Exception as e:
+            errors.append(("recover-exc", t, repr(e)))
+
+    def ver_worker(t):
+        try:
+            n = gv["msg"].shape[0]
+            for k in range(300):
+                i = (t * 577 + k * 13) % n
+                plen = int(gv["publen"][i])
+                rc = lib.eges_ecdsa_verify(gv["sig"][i].tobytes(), gv["msg"][i].tobytes(), gv["pub"][i][:plen].tobytes(),
+                                           plen)
+                if rc != int(gv["ok"][i]):
+                    errors.append(("verify", t, k, i, rc, int(gv["ok"][i])))
+        except Exception as e:
+            errors.append(("verify-exc", t, repr(e)))
+
+    threads = [threading.Thread(target=rec_worker, args=(t,)) for t in range(12)]
+    threads += [threading.Thread(target=ver_worker, args=(t,)) for t in range(12)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=150)
+    assert not any(th.is_alive() for th in threads), "a caller thread did not return"
+    assert not errors, errors[:10]
