@@ -147,9 +147,18 @@ def test_mutation_fuzz(engine, oracle):
     assert (st == 0).all() and np.array_equal(addr, exp)
     mutated = [_mutate(raws[i], fields[i], sig[i], rng) for i in range(n)]
     seen = set()
+    # batches up to 8192 items decode one transaction per wave (k_txhash.hip), larger ones one per
+    # lane: the lane-serial form (forced by EGES_TXROWS_WAVE_MAX=0) must agree item by item
     for signer in SIGNERS:
-        _, st = _check(engine, oracle, mutated, signer, CHAIN)
+        addr, st = _check(engine, oracle, mutated, signer, CHAIN)
         seen |= set(np.unique(st).tolist())
+        _, _, sh = engine.sender_raw_batch(mutated, signer, CHAIN, want_sighash=True)
+        os.environ["EGES_TXROWS_WAVE_MAX"] = "0"
+        try:
+            addr1, st1, sh1 = engine.sender_raw_batch(mutated, signer, CHAIN, want_sighash=True)
+        finally:
+            del os.environ["EGES_TXROWS_WAVE_MAX"]
+        assert np.array_equal(st1, st) and np.array_equal(addr1, addr) and np.array_equal(sh1, sh)
     assert {0, 1, 2, T.DECODE_FAILED} <= seen, seen
 
 
