@@ -1,9 +1,10 @@
 // Wire-format transactions -> sender-batch rows on the GPU (SURVEY.md §8(f) N1 + N4).
 //
-// One thread per transaction. Input: the RLP encoding of one txdata (what rlp.DecodeBytes(raw, tx)
+// One wave per transaction up to 8192 items (tx_rows_wave_kernel), one thread per transaction
+// above (tx_rows_kernel). Input: the RLP encoding of one txdata (what rlp.DecodeBytes(raw, tx)
 // consumes, core/types/transaction.go:157-165); item first + i lies at
 // raw[offsets[first + i] - offsets[0], offsets[first + i + 1] - offsets[0]).
-// The thread
+// The wave (thread)
 //   1. decodes it with the reference decoder's acceptance rules for the 10-field Geec txdata
 //      struct (transaction.go:59-76; rlp/decode.go: readKind :937-984 and readUint :986-1008,
 //      Kind's bound checks :874-907, uint :707-737, Bool :742-756, decodeBigInt :254-269,

@@ -1,5 +1,5 @@
-# (Dropped experiment, kept for the record) two-step wave Keccak round vs the four-step one (eges_amd/libeges_diag_prev.so: the diagnostic
-# build with -DEGES_KECCAK_WAVE_STEPS=4, built by hand): parity tests of every path that ends in a
+# Wave Keccak A/B (eges_amd/libeges_diag_prev.so: the diagnostic build of the previous form, built
+# by hand, e.g. -DEGES_KECCAK_HALVES=0; earlier the dropped two-step round vs the four-step one): parity tests of every path that ends in a
 # wave Keccak, then stamped launches at n = 1 / 1000 alternating, C3 and C3 from wire bytes.
 set -e
 cd "$GRAFT_REPO_ROOT"
@@ -17,4 +17,4 @@ timeout -k 10 200 python bench.py --config c3 --no-cpu-baseline > gpurun_out/kw_
 timeout -k 10 200 python bench.py --config c3raw --no-cpu-baseline > gpurun_out/kw_c3raw.json 2> gpurun_out/kw_c3raw.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kw -o run --output-format csv -- python bench.py --config c3raw --no-cpu-baseline > gpurun_out/prof_kw.log 2>&1
 head -c 200 gpurun_out/kw_c3.json; echo; head -c 200 gpurun_out/kw_c3raw.json; echo
-grep -o '"eges::tx_rows_wave[^,]*,[0-9]*,[0-9]*,[0-9.]*' gpurun_out/prof_kw/run_kernel_stats.csv
+python -c "import csv; [print(r['Name'][:40], r['Calls'], r['AverageNs']) for r in csv.DictReader(open('gpurun_out/prof_kw/run_kernel_stats.csv'))]" 
