@@ -123,8 +123,10 @@ static int overlap_parts(size_t n) {
 // Batches (or pipeline chunks) of at most this many signatures run on the latency kernel
 // (k_recover_lat.hip: one signature per 16-lane row); larger ones on the lane-serial throughput
 // kernel. EGES_LAT_MAX overrides it (0 = never); read per call so tests can A/B both kernels.
+// Cut from C1-shaped whole calls (tools/gpu_latcut.sh): 3000 signatures 0.68 ms latency kernel vs
+// 0.84 lane-serial, 4096 0.87 vs 0.85, 6000 1.20 vs 0.89-0.94, 8192 1.56 vs 0.90.
 #ifndef EGES_LAT_MAX_DEFAULT
-#define EGES_LAT_MAX_DEFAULT 8192
+#define EGES_LAT_MAX_DEFAULT 3584
 #endif
 static size_t lat_max() {
   const char* e = std::getenv("EGES_LAT_MAX");
