@@ -26,12 +26,24 @@ Metric (BASELINE.json): "secp256k1 ecrecover+address/sec at 1/8 MI355X; % of INT
 --config c2host: configs[1]'s batch handed over as host (pageable) buffers through
   eges_ecrecover_batch — the PCIe-inclusive rate a Go caller sees (never `value` of the c2 line).
 
+The c2 line also carries a `secondary` object (N = 1, outside the timed region): C3's block
+latency (median / p99 over 50 blocks), C1's 10k transfers from wire bytes, and C5 over the same
+1M batch (ecrecover and sender statuses, mismatch counts).
+
+Multi-GPU: `--gpus N` without a launcher starts `torch.distributed.run --nproc-per-node N` on this
+script as a child process (no exec) and exits with its code; under a launcher WORLD_SIZE must
+equal N. Every line carries `ranks`: each rank's device index, PCI address and UUID, gathered
+through the process group. `--stub` rehearses the rank logic on the CPU (gloo, a timed sleep as
+the step, no GPU and no libeges): tests/test_shard.py runs it at world size 2.
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config c1|c2|c2host|c3|c3raw|c4|c5|verify]
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -66,7 +78,31 @@ def parse():
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2host", "c3", "c3raw", "c4", "c5", "verify"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="c2: skip the secondary C1 / C3 / C5 measurements")
+    ap.add_argument("--stub", action="store_true", help="CPU rehearsal of the rank logic (gloo, sleep as the step)")
     return ap.parse_args()
+
+
+def launch_ranks(args):
+    """--gpus N: one process per GPU. Without a torch.distributed launcher (WORLD_SIZE unset),
+    start `python -m torch.distributed.run --nproc-per-node N` on this script as a CHILD process
+    (nothing here has touched the GPU; no exec) and exit with its return code; its rank 0
+    prints the JSON line. Under a launcher, WORLD_SIZE must be N."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            print(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}", file=sys.stderr, flush=True)
+            sys.exit(2)
+        return
+    if args.gpus <= 1:
+        return
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
 
 
 def host_cpus():
@@ -172,6 +208,7 @@ class Ctx:
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.args = torch, dist, args
+        self.stub = args.stub
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -179,11 +216,15 @@ class Ctx:
         # gloo for the timing collectives. The driver's multi-GPU runs leave both unset.
         if "EGES_BENCH_DEVICE" in os.environ:
             self.local = int(os.environ["EGES_BENCH_DEVICE"])
-        # bind the rank's GPU before the process group exists, so RCCL's barrier uses it
-        torch.cuda.set_device(self.local)
+        if not self.stub:
+            # bind the rank's GPU before the process group exists, so RCCL's barrier uses it
+            torch.cuda.set_device(self.local)
         if self.world > 1:
-            backend = os.environ.get("EGES_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+            backend = "gloo" if self.stub else (os.environ.get("EGES_BENCH_BACKEND") or "nccl")
             dist.init_process_group(backend=backend)
+        self.ranks = self.gather_ranks()
+        if self.stub:
+            return
         import eges_amd
         self.eges = eges_amd
         eges_amd.init(1 << self.local)
@@ -191,6 +232,26 @@ class Ctx:
         # a dedicated stream: the engine's kernels and the timing events share it
         self.stream = torch.cuda.Stream(self.dev)
         self.sp = self.stream.cuda_stream
+
+    def gather_ranks(self):
+        """Each rank's device identity (index, PCI address, UUID), all-gathered through the process
+        group, so the line shows how many distinct GPUs the ranks ran on."""
+        me = {"rank": self.rank, "local_rank": self.local, "host": socket.gethostname()}
+        if self.stub:
+            me["device"] = "cpu (stub)"
+        else:
+            p = self.torch.cuda.get_device_properties(self.local)
+            me.update(device=self.local, name=p.name,
+                      pci=f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}", uuid=str(p.uuid))
+        if self.world == 1:
+            return [me]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, me)
+        return out
+
+    def sync(self):
+        if not self.stub:
+            self.torch.cuda.synchronize()
 
     def timed(self, step, reset=None):
         """W untimed steps, then K steps between barrier + synchronize on both sides; returns
@@ -200,34 +261,40 @@ class Ctx:
         torch, dist, a = self.torch, self.dist, self.args
         for _ in range(a.warmup):
             step()
-        torch.cuda.synchronize()
+        self.sync()
         if reset is not None:
             reset()
-            torch.cuda.synchronize()
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+            self.sync()
+        evs = [] if self.stub else [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                                    for _ in range(a.steps)]
         if self.world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        self.sync()
         t0 = time.perf_counter()
         for i in range(a.steps):
-            evs[i][0].record(self.stream)
+            if evs:
+                evs[i][0].record(self.stream)
             step()
-            evs[i][1].record(self.stream)
-        torch.cuda.synchronize()
+            if evs:
+                evs[i][1].record(self.stream)
+        self.sync()
         if self.world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
-        kern_ms = sum(x.elapsed_time(y) for x, y in evs) / a.steps
+        kern_ms = (sum(x.elapsed_time(y) for x, y in evs) / a.steps) if evs else elapsed * 1e3 / a.steps
         return elapsed, kern_ms
 
     def reduce_max(self, *vals):
         if self.world == 1:
             return vals
-        t = self.torch.tensor(list(vals), dtype=self.torch.float64, device=self.dev)
+        dev = "cpu" if self.stub else self.dev
+        t = self.torch.tensor(list(vals), dtype=self.torch.float64, device=dev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return tuple(t.tolist())
 
     def finish(self, line, ok):
+        line["ranks"] = self.ranks
+        line["distinct_devices"] = len({(r.get("host"), r.get("pci"), r.get("uuid"), r.get("device")) for r in self.ranks})
         if self.rank == 0:
             print(json.dumps(line), flush=True)
         if self.world > 1:
@@ -268,16 +335,31 @@ def roofline(per_gpu_rate, work, batch, kern_ms, kernel="eges::recover_kernel"):
 
 # ------------------------------------------------------------------ c2 / c4: throughput
 def run_throughput(c, strong):
-    torch, a = c.torch, c.args
+    a = c.args
     from eges_amd.shard import shard_range
     if strong:
         total = a.batch or C4_TOTAL
-        lo, hi = shard_range(total, c.rank, c.world)
+        shards = [shard_range(total, r, c.world) for r in range(c.world)]
     else:
         B0 = a.batch or (1 << 20)
-        lo, hi = c.rank * B0, (c.rank + 1) * B0
+        shards = [(r * B0, (r + 1) * B0) for r in range(c.world)]
         total = B0 * c.world
+    lo, hi = shards[c.rank]
     B = hi - lo
+    wl = ("configs[3]: 64M-signature batch sharded by index across the GPUs, batch ecrecover + Keccak address"
+          if strong else "configs[1]: 1M random-key secp256k1 signatures, batch ecrecover + Keccak address per "
+          "MI355X (inputs resident in HBM)")
+    if c.stub:
+        elapsed, kern_ms, ok = run_stub(c, B)
+        line = {"metric": METRIC, "value": round(total * a.steps / elapsed, 1), "unit": "sigs/s", "n_gpus": c.world,
+                "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 3),
+                "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
+                "dtype": "u32", "data": "stub: rank-logic rehearsal on the CPU (sleep as the step, no GPU)",
+                "config": {"workload": wl, "batch_per_gpu": B, "shards": shards, "total_batch": total,
+                           "parallelism": f"index-sharded x{c.world}", "correct": ok}}
+        c.finish(line, ok)
+        return
+    torch = c.torch
     # synthetic device-resident input: this rank's contiguous index shard
     msg, sig, exp_addr = c.eges.synth_sign_dev(lo, B, c.local)
     addr = torch.empty((B, 20), dtype=torch.uint8, device=c.dev)
@@ -307,26 +389,44 @@ def run_throughput(c, strong):
         cpu = cpu_baseline(msg.cpu().numpy(), sig.cpu().numpy(), a.cpu_seconds, gpu_addr=addr.cpu().numpy())
         if cpu and (cpu.get("reference_check") or {}).get("mismatches"):
             ok = False
-    wl = ("configs[3]: 64M-signature batch sharded by index across the GPUs, batch ecrecover + Keccak address"
-          if strong else "configs[1]: 1M random-key secp256k1 signatures, batch ecrecover + Keccak address per "
-          "MI355X (inputs resident in HBM)")
     line = {"metric": METRIC, "value": round(value, 1), "unit": "sigs/s", "n_gpus": c.world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 3), "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-            "config": {"workload": wl, "batch_per_gpu": B, "total_batch": total,
+            "config": {"workload": wl, "batch_per_gpu": B, "shards": shards, "total_batch": total,
                        "parallelism": f"index-sharded x{c.world}", "correct": ok},
             "roofline": roofline(per_gpu_rate, W_RECOVER, B, kern_ms), "cpu_baseline": cpu}
+    if c.world == 1 and not strong and not a.no_secondary:
+        # the other configs, after the timed region (about a second): C3 and C1 latency, C5 statuses
+        sec = {"note": "measured after the timed C2 region, same process; not part of value"}
+        sec["c3_block"] = measure_block(c, 1000, raw_mode=False, warmup=3, iters=50, cpu=False)
+        sec["c3_block_wire"] = measure_block(c, 1000, raw_mode=True, warmup=3, iters=50, cpu=False)
+        sec["c1_transfers"] = measure_c1(c, 10000, warmup=3, iters=20, cpu=False)
+        sec["c5_adversarial"] = measure_c5(c, B, msg, sig, exp_addr, steps=1, warmup=1)
+        line["secondary"] = sec
+        ok = ok and all(v.get("correct", True) for v in sec.values() if isinstance(v, dict))
+        line["config"]["correct"] = ok
     c.finish(line, ok)
 
 
+def run_stub(c, B):
+    """The rank logic of run_throughput on the CPU: timed steps between barriers, max over ranks,
+    the correctness reduce (EGES_BENCH_STUB_BAD_RANK makes one rank report a mismatch)."""
+    def step():
+        time.sleep(0.002)
+    elapsed, kern_ms = c.timed(step)
+    ok = str(c.rank) != os.environ.get("EGES_BENCH_STUB_BAD_RANK", "")
+    elapsed, kern_ms, bad = c.reduce_max(elapsed, kern_ms, 0.0 if ok else 1.0)
+    return elapsed, kern_ms, bad == 0.0
+
+
 # ------------------------------------------------------------------ c3: Geec block latency
-def run_block_latency(c):
+def measure_block(c, n, raw_mode, warmup, iters, cpu=True):
+    """A Geec block of n EIP-155 transactions (100-byte payload) through eges_sender_batch (host
+    buffers) or, raw_mode, as wire bytes through eges_sender_raw_batch: per-block latency."""
     import numpy as np
-    torch, a = c.torch, c.args
+    torch = c.torch
     from eges_amd import txs
     from eges_amd._lib import SIGNER_EIP155
-    n = a.batch or 1000
-    raw_mode = a.config == "c3raw"
     sighash = txs.geec_block(0, n, payload=100)
     sig_d, exp_d = c.eges.synth_sign_msg_dev(torch.from_numpy(sighash).to(c.dev), 0, stream=c.sp)
     torch.cuda.synchronize()
@@ -334,23 +434,26 @@ def run_block_latency(c):
     r, s, v = txs.sender_rows(sig_h, txs.GEEC_CHAIN_ID)
     if raw_mode:  # the block's transactions as the wire carries them (10-field Geec txdata RLP)
         packed = c.eges.pack_raw(txs.geec_block_raw(0, sig_h, payload=100))
-    iters = max(50, a.steps * 20)
     lat = []
     ok = True
-    for i in range(a.warmup + iters):
+    for i in range(warmup + iters):
         t0 = time.perf_counter()
         if raw_mode:
             addr, st, _ = c.eges.sender_raw_batch(packed, SIGNER_EIP155, txs.GEEC_CHAIN_ID)
         else:
             addr, st = c.eges.sender_batch(sighash, r, s, v, None, SIGNER_EIP155, txs.GEEC_CHAIN_ID)
         dt = time.perf_counter() - t0
-        if i >= a.warmup:
+        if i >= warmup:
             lat.append(dt)
-        if i == 0:
-            ok = bool((st == 0).all()) and np.array_equal(addr, exp_h)
+        ok = ok and bool((st == 0).all()) and np.array_equal(addr, exp_h)
     lat = np.array(lat) * 1e3
-    cpu = None
-    if not a.no_cpu_baseline:
+    out = {"median_ms": round(float(np.median(lat)), 3), "p99_ms": round(float(np.percentile(lat, 99)), 3),
+           "blocks": iters, "txs": n, "correct": ok,
+           "path": ("wire-format txdata RLP through eges_sender_raw_batch (H2D + decode + sighash RLP/Keccak + "
+                    "recovery kernels + D2H)" if raw_mode else "host buffers through eges_sender_batch (H2D + "
+                    "kernels + D2H)")}
+    if cpu:
+        out["cpu"] = None
         try:
             from oracle import RefLib, have_ref
             if have_ref():
@@ -358,32 +461,39 @@ def run_block_latency(c):
                 t0 = time.perf_counter()
                 ref.ecrecover_batch_mt(sighash, sig_h, 1)
                 dt = time.perf_counter() - t0
-                cpu = {"value": round(dt * 1e3, 3), "unit": "ms/block", "cores": 1, "kind": "reference",
-                       "sample": f"one {n}-tx block: the reference's serial per-tx ecrecover + Keccak address "
-                                 "(types.Sender inside StateProcessor.Process, state_processor.go:73-93), 1 core; "
-                                 + ("sighash RLP + Keccak excluded on the CPU side only (the GPU value includes "
-                                    "decode and sighash)" if raw_mode else "sighash RLP cost excluded on both sides")}
+                out["cpu"] = {"value": round(dt * 1e3, 3), "unit": "ms/block", "cores": 1, "kind": "reference",
+                              "sample": f"one {n}-tx block: the reference's serial per-tx ecrecover + Keccak address "
+                                        "(types.Sender inside StateProcessor.Process, state_processor.go:73-93), "
+                                        "1 core; " + ("sighash RLP + Keccak excluded on the CPU side only (the GPU "
+                                                      "value includes decode and sighash)" if raw_mode else
+                                                      "sighash RLP cost excluded on both sides")}
         except Exception:
-            cpu = None
-    path = ("wire-format txdata RLP through eges_sender_raw_batch (H2D + decode + sighash RLP/Keccak + recovery "
-            "kernels + D2H)" if raw_mode else "host buffers through eges_sender_batch (H2D + kernels + D2H)")
+            out["cpu"] = None
+    return out
+
+
+def run_block_latency(c):
+    a = c.args
+    n = a.batch or 1000
+    raw_mode = a.config == "c3raw"
+    iters = max(50, a.steps * 20)
+    m = measure_block(c, n, raw_mode, a.warmup, iters, cpu=not a.no_cpu_baseline)
     line = {"metric": "Geec block sender recovery latency (1000 EIP-155 txs, 100-byte payload)"
                       + (", from wire bytes" if raw_mode else ""),
-            "value": round(float(np.median(lat)), 3), "unit": "ms/block", "p99_ms": round(float(np.percentile(lat, 99)), 3),
-            "sigs_per_s": round(n / (np.median(lat) / 1e3), 1), "n_gpus": 1, "steps": iters, "warmup": a.warmup,
+            "value": m["median_ms"], "unit": "ms/block", "p99_ms": m["p99_ms"],
+            "sigs_per_s": round(n / (m["median_ms"] / 1e3), 1), "n_gpus": 1, "steps": iters, "warmup": a.warmup,
             "higher_is_better": False, "dtype": "u32", "data": "synthetic",
             "config": {"workload": "configs[2]: Geec block import, 1000 txns/block (txnSize 100), EIP155Signer(930412), "
-                                   + path, "correct": ok}, "cpu_baseline": cpu}
-    c.finish(line, ok)
+                                   + m["path"], "correct": m["correct"]}, "cpu_baseline": m.get("cpu")}
+    c.finish(line, m["correct"])
 
 
 # ------------------------------------------------------------------ c1: 10k EIP-155 transfers
-def run_c1(c):
+def measure_c1(c, n, warmup, iters, cpu=True):
     import numpy as np
-    torch, a = c.torch, c.args
+    torch = c.torch
     from eges_amd import txs
     from eges_amd._lib import SIGNER_EIP155
-    n = a.batch or 10000
     sighash = txs.c1_sighashes(0, n)
     # the GPU synthetic signer uses C1's keys (tests/test_c1.py pins them against the reference's
     # pubkey_create); its nonces are not RFC6979, which does not change what recovery computes
@@ -391,20 +501,21 @@ def run_c1(c):
     torch.cuda.synchronize()
     sig_h, exp_h = sig_d.cpu().numpy(), exp_d.cpu().numpy()
     packed = c.eges.pack_raw(txs.c1_raw(0, sig_h))
-    iters = max(20, a.steps * 4)
     lat = []
     ok = True
-    for i in range(a.warmup + iters):
+    for i in range(warmup + iters):
         t0 = time.perf_counter()
         addr, st, _ = c.eges.sender_raw_batch(packed, SIGNER_EIP155, txs.GEEC_CHAIN_ID)
         dt = time.perf_counter() - t0
-        if i >= a.warmup:
+        if i >= warmup:
             lat.append(dt)
-        if i == 0:
-            ok = bool((st == 0).all()) and np.array_equal(addr, exp_h)
+        ok = ok and bool((st == 0).all()) and np.array_equal(addr, exp_h)
     med = float(np.median(lat))
-    cpu = None
-    if not a.no_cpu_baseline:
+    out = {"txs_per_s": round(n / med, 1), "median_ms": round(med * 1e3, 3),
+           "p99_ms": round(float(np.percentile(np.array(lat) * 1e3, 99)), 3), "txs": n, "batches": iters,
+           "correct": ok}
+    if cpu:
+        out["cpu"] = None
         try:
             from oracle import RefLib, have_ref
             if have_ref():
@@ -417,32 +528,45 @@ def run_c1(c):
                 _, _, ret = ref.ecrecover_batch_mt(sighash, sig_h, threads)
                 dtn = time.perf_counter() - t0
                 assert (ret == 1).all()
-                cpu = {"value": round(n / dtn, 1), "unit": "txs/s", "cores": threads, "kind": "reference",
-                       "single_core_txs_per_s": round(n / dt1, 1),
-                       "sample": f"the same {n} transfers: reference libsecp256k1 ecrecover (cgo build flags) + Keccak "
-                                 f"address, {threads} pthreads ({dtn:.2f} s; 1 core {dt1:.2f} s); sighash RLP + Keccak "
-                                 "excluded on the CPU side only (the GPU value includes decode and sighash)"}
+                out["cpu"] = {"value": round(n / dtn, 1), "unit": "txs/s", "cores": threads, "kind": "reference",
+                              "single_core_txs_per_s": round(n / dt1, 1),
+                              "sample": f"the same {n} transfers: reference libsecp256k1 ecrecover (cgo build flags) + "
+                                        f"Keccak address, {threads} pthreads ({dtn:.2f} s; 1 core {dt1:.2f} s); sighash "
+                                        "RLP + Keccak excluded on the CPU side only (the GPU value includes decode and "
+                                        "sighash)"}
         except Exception:
-            cpu = None
+            out["cpu"] = None
+    return out
+
+
+def run_c1(c):
+    a = c.args
+    n = a.batch or 10000
+    iters = max(20, a.steps * 4)
+    m = measure_c1(c, n, a.warmup, iters, cpu=not a.no_cpu_baseline)
     line = {"metric": "types.Sender over 10k synthetic EIP-155-signed transfers (configs[0]), from wire bytes",
-            "value": round(n / med, 1), "unit": "txs/s", "ms_per_batch": round(med * 1e3, 3), "n_gpus": 1,
-            "steps": iters, "warmup": a.warmup, "higher_is_better": True, "dtype": "u32", "data": "synthetic",
+            "value": m["txs_per_s"], "unit": "txs/s", "ms_per_batch": m["median_ms"], "p99_ms": m["p99_ms"],
+            "n_gpus": 1, "steps": iters, "warmup": a.warmup, "higher_is_better": True, "dtype": "u32",
+            "data": "synthetic",
             "config": {"workload": f"configs[0]: {n} EIP-155 transfers (nonce i, gasPrice 1, gas 21000, value 1, "
                                    "empty data, chainId 930412) as 10-field txdata RLP through eges_sender_raw_batch "
                                    "(pageable host buffers: H2D + GPU decode + sighash RLP/Keccak + recovery + D2H)",
-                       "correct": ok}, "cpu_baseline": cpu}
-    c.finish(line, ok)
+                       "correct": m["correct"]}, "cpu_baseline": m.get("cpu")}
+    if m.get("cpu"):
+        line["vs_cpu"] = round(m["txs_per_s"] / m["cpu"]["value"], 1)
+    c.finish(line, m["correct"])
 
 
 # ------------------------------------------------------------------ c5: adversarial mix
-def run_adversarial(c):
+def measure_c5(c, B, msg, sig, exp_addr, steps, warmup):
+    """configs[4] over a device-resident batch (msg, sig valid low-s signatures, exp_addr their
+    addresses): 10 % mutated over 7 reject classes, through crypto.Ecrecover and types.Sender
+    (EIP155Signer) semantics; every status against its by-construction expectation, every
+    accepted item's address against the signer's."""
     import numpy as np
-    torch, a = c.torch, c.args
+    torch = c.torch
     from eges_amd import txs, workloads
     from eges_amd._lib import SIGNER_EIP155
-    B = a.batch or (1 << 20)
-    msg, sig, exp_addr = c.eges.synth_sign_dev(0, B, c.local, stream=c.sp)
-    torch.cuda.synchronize()
     sig_h = sig.cpu().numpy()
     kind = workloads.adversarial_mix(sig_h, frac=0.10)
     exp_e = workloads.expected_status(kind, "ecrecover")
@@ -471,23 +595,38 @@ def run_adversarial(c):
         addr2.fill_(0xAB)
         st2.fill_(0xFF)
 
-    el_e, k_e = c.timed(step_e, reset_e)
-    el_s, k_s = c.timed(step_s, reset_s)
+    saved = (c.args.steps, c.args.warmup)
+    c.args.steps, c.args.warmup = steps, warmup
+    try:
+        el_e, _ = c.timed(step_e, reset_e)
+        el_s, _ = c.timed(step_s, reset_s)
+    finally:
+        c.args.steps, c.args.warmup = saved
     got_e, got_s = st.cpu().numpy(), st2.cpu().numpy()
     a_e, a_s, ex = addr.cpu().numpy(), addr2.cpu().numpy(), exp_addr.cpu().numpy()
     okm_e = got_e == 0
     okm_s = got_s == 0
-    ok = (np.array_equal(got_e, exp_e) and np.array_equal(got_s, exp_s) and np.array_equal(a_e[okm_e], ex[okm_e])
-          and np.array_equal(a_s[okm_s], ex[okm_s]) and not a_e[~okm_e].any() and not a_s[~okm_s].any())
-    counts = {workloads.KIND_NAMES[k]: int((kind == k).sum()) for k in range(len(workloads.KIND_NAMES))}
-    line = {"metric": "adversarial-mix sender recovery, bit-exact statuses", "value": round(B * a.steps / el_s, 1),
-            "unit": "sigs/s", "ecrecover_sigs_per_s": round(B * a.steps / el_e, 1), "n_gpus": 1, "steps": a.steps,
+    mism = {"ecrecover_status": int((got_e != exp_e).sum()), "sender_status": int((got_s != exp_s).sum()),
+            "ecrecover_addr": int((a_e[okm_e] != ex[okm_e]).any(axis=1).sum()) + int(a_e[~okm_e].any(axis=1).sum()),
+            "sender_addr": int((a_s[okm_s] != ex[okm_s]).any(axis=1).sum()) + int(a_s[~okm_s].any(axis=1).sum())}
+    return {"batch": B, "sender_sigs_per_s": round(B * steps / el_s, 1), "ecrecover_sigs_per_s": round(B * steps / el_e, 1),
+            "kinds": {workloads.KIND_NAMES[k]: int((kind == k).sum()) for k in range(len(workloads.KIND_NAMES))},
+            "mismatches": mism, "correct": not any(mism.values())}
+
+
+def run_adversarial(c):
+    a = c.args
+    B = a.batch or (1 << 20)
+    msg, sig, exp_addr = c.eges.synth_sign_dev(0, B, c.local, stream=c.sp)
+    c.torch.cuda.synchronize()
+    m = measure_c5(c, B, msg, sig, exp_addr, a.steps, a.warmup)
+    line = {"metric": "adversarial-mix sender recovery, bit-exact statuses", "value": m["sender_sigs_per_s"],
+            "unit": "sigs/s", "ecrecover_sigs_per_s": m["ecrecover_sigs_per_s"], "n_gpus": 1, "steps": a.steps,
             "warmup": a.warmup, "higher_is_better": True, "dtype": "u32", "data": "synthetic",
             "config": {"workload": "configs[4]: 10% invalid (high-s, bad recid / chain id, r>=n, s>=n, non-residue R, "
                                    "zero r/s); types.Sender (EIP155Signer 930412) and crypto.Ecrecover semantics",
-                       "batch": B, "kinds": counts, "correct": ok,
-                       "mismatches": {"ecrecover": int((got_e != exp_e).sum()), "sender": int((got_s != exp_s).sum())}}}
-    c.finish(line, ok)
+                       "batch": B, "kinds": m["kinds"], "correct": m["correct"], "mismatches": m["mismatches"]}}
+    c.finish(line, m["correct"])
 
 
 # ------------------------------------------------------------------ verify mode
@@ -578,7 +717,10 @@ def run_host_throughput(c):
 
 def main():
     args = parse()
+    launch_ranks(args)  # --gpus N: one process per GPU (before anything touches the GPU)
     c = Ctx(args)
+    if args.stub and args.config not in ("c2", "c4"):
+        sys.exit("bench.py: --stub rehearses the c2 / c4 rank logic only")
     if args.config == "c1":
         run_c1(c)
     elif args.config == "c2":

@@ -67,7 +67,15 @@ SIGNATURES = {
     "eges_keccak256": (None, [_P, _SZ, _P]),
     "eges_synth_sign_dev": (_I, [_I, _U64, _SZ, _P, _P, _P, _P]),
     "eges_synth_sign_msg_dev": (_I, [_I, _U64, _SZ, _P, _P, _P, _P]),
+    "eges_diag_counters": (_I, [_I, _P, _SZ, _I]),
+    "eges_test_set_knob": (_I, [ctypes.c_char_p, ctypes.c_longlong]),
+    "eges_test_get_knob": (_I, [ctypes.c_char_p, _P]),
 }
+
+# EGES_DIAG_* (include/eges.h): rare exact branches the kernels count
+DIAG_NAMES = ["ls_redo", "ls_exc", "lat_redo", "lat_exc", "comb_redo", "join_dbl", "join_inf", "mid_redo",
+              "mid_exc", "mid_join"]
+DIAG_COUNT = 16
 
 
 class EgesError(RuntimeError):

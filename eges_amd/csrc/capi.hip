@@ -91,6 +91,7 @@ struct Dev {
   hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_k[2] = {nullptr, nullptr};  // per pipeline region
   uint32_t* gtab = nullptr;
   uint32_t* ws = nullptr;
+  uint32_t* diag = nullptr;  // DIAG_WORDS counters (eges_diag_counters)
   int mb_recover = 0, mb_verify = 0, mb_synth = 0;
   int ws_blocks = 0;  // blocks ws (and ws2) hold: every launch's grid is checked against it
   uint8_t* buf = nullptr;  // per-call device scratch, grown on demand
@@ -106,32 +107,65 @@ struct Dev {
 };
 using DevPtr = std::shared_ptr<Dev>;
 
-// Overlapped launches: a device-resident recover batch runs as launches alternating between
-// two streams with their own workspaces, so each launch's tail (its slowest waves) overlaps the
-// next launch's start. Default: on when the batch spans more than one CHUNK (64M signatures:
-// +3.9 % on one box), off for a single-chunk batch, whose launch then stays one kernel.
-// EGES_OVERLAP=S forces S parts (S >= 2); EGES_OVERLAP=0 turns it off.
-static int overlap_parts(size_t n) {
-  static const int v = [] {
-    const char* e = std::getenv("EGES_OVERLAP");
-    return e ? std::max(0, std::atoi(e)) : -1;
-  }();
-  if (v >= 0) return v;
-  return n > CHUNK ? 2 : 0;
-}
-
-// Batches (or pipeline chunks) of at most this many signatures run on the latency kernel
-// (k_recover_lat.hip: one signature per 16-lane row); larger ones on the lane-serial throughput
-// kernel. EGES_LAT_MAX overrides it (0 = never); read per call so tests can A/B both kernels.
-// Cut from C1-shaped whole calls (tools/gpu_latcut.sh): 3000 signatures 0.68 ms latency kernel vs
-// 0.84 lane-serial, 4096 0.87 vs 0.85, 6000 1.20 vs 0.89-0.94, 8192 1.56 vs 0.90.
+// ------------------------------------------------------------------ knobs (knobs.h)
+// Name (the environment variable read once at the first eges_init) and product default.
+struct KnobDef {
+  const char* name;
+  long long dflt;
+};
+// Batches (or pipeline chunks) of at most LAT_MAX signatures run on the latency kernels
+// (k_recover_lat.hip: one signature per wave), up to MID_MAX on the mid-size kernel
+// (k_recover_mid.hip), larger ones on the lane-serial throughput kernel. Cuts from C1-shaped
+// whole calls (tools/gpu_latcut.sh).
+// Overlapped launches (OVERLAP): a device-resident recover batch runs as launches alternating
+// between two streams with their own workspaces, so each launch's tail (its slowest waves)
+// overlaps the next launch's start. Auto (-1): on when the batch spans more than one CHUNK (64M
+// signatures: +3.9 % on one box), off for a single-chunk batch, whose launch then stays one
+// kernel. S >= 2 forces S parts; 0 turns it off.
 #ifndef EGES_LAT_MAX_DEFAULT
 #define EGES_LAT_MAX_DEFAULT 3584
 #endif
-static size_t lat_max() {
-  const char* e = std::getenv("EGES_LAT_MAX");
-  return e && *e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)EGES_LAT_MAX_DEFAULT;
+#ifndef EGES_MID_MAX_DEFAULT
+#define EGES_MID_MAX_DEFAULT 0
+#endif
+const KnobDef KNOB_DEFS[KNOB_COUNT] = {
+    {"EGES_LAT_MAX", EGES_LAT_MAX_DEFAULT},
+    {"EGES_LAT_WIDE_MAX", 256},
+    {"EGES_MID_MAX", EGES_MID_MAX_DEFAULT},
+    {"EGES_TXROWS_WAVE_MAX", 8192},
+    {"EGES_TEST_ROOT_HELPERS", 1},
+    {"EGES_OVERLAP", -1},
+    {"EGES_TEST_FORCE_REDO", 0},
+    {"EGES_COALESCE_GATHER_US", 20},
+    {"EGES_COALESCE_SPIN_US", 2000},
+    {"EGES_COALESCE_SPINNERS", 8},
+};
+std::atomic<long long> g_knob[KNOB_COUNT];
+std::once_flag g_knob_once;
+
+void knobs_load_env() {  // once per process, from eges_init (the only getenv of these names)
+  std::call_once(g_knob_once, [] {
+    for (int k = 0; k < KNOB_COUNT; ++k) {
+      const char* e = std::getenv(KNOB_DEFS[k].name);
+      g_knob[k].store(e && *e ? std::strtoll(e, nullptr, 10) : KNOB_DEFS[k].dflt, std::memory_order_relaxed);
+    }
+  });
 }
+int knob_index(const char* name) {
+  if (!name) return -1;
+  for (int k = 0; k < KNOB_COUNT; ++k)
+    if (std::strcmp(name, KNOB_DEFS[k].name) == 0) return k;
+  return -1;
+}
+
+static int overlap_parts(size_t n) {
+  const long long v = knob(KNOB_OVERLAP);
+  if (v >= 0) return (int)std::min<long long>(v, 64);
+  return n > CHUNK ? 2 : 0;
+}
+static size_t lat_max() { return (size_t)std::max<long long>(0, knob(KNOB_LAT_MAX)); }
+static size_t mid_max() { return (size_t)std::max<long long>(0, knob(KNOB_MID_MAX)); }
+static uint32_t wide_max() { return (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_LAT_WIDE_MAX), 1u << 30)); }
 
 std::mutex g_mu;
 std::vector<DevPtr> g_devs;
@@ -212,6 +246,8 @@ int init_device(int id, DevPtr* out) {
                                        lane_serial_grid((uint32_t)CHUNK, d->mb_verify)));
   HIPCHK(hipMalloc(&d->gtab, gtab_bytes()));
   HIPCHK(hipMalloc(&d->ws, ws_bytes_per_block() * (size_t)d->ws_blocks));
+  HIPCHK(hipMalloc(&d->diag, DIAG_WORDS * sizeof(uint32_t)));
+  HIPCHK(hipMemsetAsync(d->diag, 0, DIAG_WORDS * sizeof(uint32_t), d->stream));
   HIPCHK(launch_init_gtab(d->gtab, d->stream));
   HIPCHK(hipEventRecord(d->last, d->stream));
   HIPCHK(hipStreamSynchronize(d->stream));
@@ -227,6 +263,7 @@ Dev::~Dev() {
   if (last) (void)hipEventSynchronize(last);  // the last engine work, on whichever stream the caller gave
   if (gtab) (void)hipFree(gtab);
   if (ws) (void)hipFree(ws);
+  if (diag) (void)hipFree(diag);
   if (buf) (void)hipFree(buf);
   if (pin) (void)hipHostFree(pin);
   if (last) (void)hipEventDestroy(last);
@@ -278,6 +315,14 @@ struct Serial {
   ~Serial() { (void)hipEventRecord(d.last, st); }
 };
 
+// The device's diagnostic counters and the test-only redo knob, on every launch's parameters.
+template <class P>
+P with_diag(const Dev& d, P p) {
+  p.diag = d.diag;
+  p.force_redo = knob(KNOB_FORCE_REDO) != 0 ? 1u : 0u;
+  return p;
+}
+
 // One recover pass over prepared records: the latency kernel for small passes, else the
 // resident-grid lane-serial kernel (its workspace bound checked by the launcher).
 #ifdef EGES_PHASE_STAMPS
@@ -298,9 +343,9 @@ static hipError_t stamp_buf(size_t waves, hipStream_t st) {
 #endif
 
 hipError_t launch_recover_pass(Dev& d, const RecoverParams& p0, hipStream_t st) {
-  RecoverParams p = p0;
+  RecoverParams p = with_diag(d, p0);
   // the split form (four waves per signature) while the batch leaves SIMDs idle
-  p.wide = p.n <= (uint32_t)env_int("EGES_LAT_WIDE_MAX", 256) ? 1u : 0u;
+  p.wide = p.n <= wide_max() ? 1u : 0u;
 #ifdef EGES_PHASE_STAMPS
   if (p.n <= lat_max() || p.raw_sig) {
     hipError_t e = stamp_buf(lat_waves(p.n), st);
@@ -349,7 +394,7 @@ int run_recover_dev_overlap(Dev& d, const uint8_t* msg, const uint8_t* sig, size
     HIPCHK(launch_prep_ecrecover(msg + off * 32, sig + off * 65, m, (uint32_t)n_pad, rec, sj));
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr ? addr + off * 20 : nullptr, pub ? pub + off * 65 : nullptr,
                     d.gtab, (j & 1) ? d.ws2 : d.ws};
-    HIPCHK(launch_recover(p, d.mb_recover, d.ws_blocks, sj));
+    HIPCHK(launch_recover(with_diag(d, p), d.mb_recover, d.ws_blocks, sj));
   }
   HIPCHK(hipEventRecord(d.ev_join, d.aux));
   HIPCHK(hipStreamWaitEvent(st, d.ev_join, 0));
@@ -380,7 +425,7 @@ int run_recover_dev(Dev& d, const uint8_t* msg, const uint8_t* sig, size_t n, ui
 #ifdef EGES_PHASE_STAMPS
     if (p.n > lat_max()) {
       HIPCHK(stamp_buf((size_t)d.ws_blocks * 4 /* waves per block */, st));
-      HIPCHK(launch_recover_stamped(p, d.mb_recover, d.ws_blocks, st, g_stamps));
+      HIPCHK(launch_recover_stamped(with_diag(d, p), d.mb_recover, d.ws_blocks, st, g_stamps));
       continue;
     }
 #endif
@@ -467,7 +512,8 @@ int run_verify_dev(Dev& d, const uint8_t* pub, const uint8_t* publen, const uint
     const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
     VerifyParams p{pub + off * 65, publen + off, msg + off * 32, sig + off * 64, m, ok + off, d.gtab, d.ws};
     verify_scratch_bind(p, d.buf, n_pad);
-    if (m <= lat_max()) HIPCHK(launch_verify_lat(p, p.n <= (uint32_t)env_int("EGES_LAT_WIDE_MAX", 256), st));
+    p = with_diag(d, p);
+    if (m <= lat_max()) HIPCHK(launch_verify_lat(p, p.n <= wide_max(), st));
     else HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
   }
   return EGES_SUCCESS;
@@ -480,6 +526,7 @@ struct HostJob {
   const uint32_t* inlen = nullptr;  // PRECOMPILE: optional input lengths
   const uint64_t* offsets = nullptr;  // SENDER_RAW: n + 1 entries
   uint8_t* sighash = nullptr;         // SENDER_RAW: optional output
+  bool decode_only = false;           // SENDER_RAW: decode only; status receives the vflags
   // inputs
   const uint8_t *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr, *e = nullptr;
   int signer = 0;
@@ -557,6 +604,18 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
   if (rc) return rc;
   // a single chunk has nothing to overlap: one stream, no cross-stream waits (C3 latency)
   hipStream_t st = small ? lane->stream : d.stream, sx = nreg > 1 ? d.copy : st;
+  // Every return after this point (errors included) first drains both streams, so the lane /
+  // device mutex is never released while kernels or copies of this call still touch its
+  // pinned staging or scratch (the next caller writes its inputs there).
+  struct Drain {
+    hipStream_t a, b;
+    bool armed;
+    ~Drain() {
+      if (!armed) return;
+      (void)hipStreamSynchronize(a);
+      if (b != a) (void)hipStreamSynchronize(b);
+    }
+  } drain{st, sx, true};
   if (pinned && !pin && hipHostMalloc(&pin, PIN_BYTES, hipHostMallocDefault) != hipSuccess) {
     pin = nullptr;
     return set_err(EGES_E_NOMEM, "hipHostMalloc(%zu) failed", PIN_BYTES);
@@ -704,10 +763,14 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       H2D(B, reinterpret_cast<uint8_t*>(doff), j.offsets + base, 8 * (m + 1));
       FLUSH_IN(B);
       JOIN_IN(r);
-      HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, vf, st));
-      HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, st));
-      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
-      HIPCHK(launch_recover_pass(d, p, st));
+      if (j.decode_only) {  // the decoder's flags straight into the status bytes
+        HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, o_st, st));
+      } else {
+        HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, vf, st));
+        HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, st));
+        RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
+        HIPCHK(launch_recover_pass(d, p, st));
+      }
     } else {
       uint8_t* dp = I;
       uint8_t* dl = dp + m * 65;
@@ -721,8 +784,9 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       JOIN_IN(r);
       VerifyParams p{dp, dl, dm, ds, (uint32_t)m, o_st, d.gtab, d.ws};
       verify_scratch_bind(p, B + rg.o_rec, m_pad);
+      p = with_diag(d, p);
       // small (lane) calls must not touch the device's shared workspace: latency kernel
-      if (small || m <= lat_max()) HIPCHK(launch_verify_lat(p, p.n <= (uint32_t)env_int("EGES_LAT_WIDE_MAX", 256), st));
+      if (small || m <= lat_max()) HIPCHK(launch_verify_lat(p, p.n <= wide_max(), st));
       else HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
     }
     if (sx != st) HIPCHK(hipEventRecord(ev_k[r], st));
@@ -740,6 +804,8 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
   }
   if (!small) HIPCHK(hipEventRecord(d.last, sx));
   HIPCHK(hipStreamSynchronize(sx));
+  if (sx != st) HIPCHK(hipStreamSynchronize(st));  // (st's last work is already behind sx's events)
+  drain.armed = false;
   if (pinned && have_prev) unpack(prev);
   return EGES_SUCCESS;
 #undef H2D
@@ -776,6 +842,27 @@ int run_host(const HostJob& j, size_t n) {
   for (auto& t : th) t.join();
   for (size_t i = 0; i < ndev; ++i)
     if (rcs[i]) return set_err(rcs[i], "device %d: %s", devs[i]->id, errs[i].c_str());
+  return EGES_SUCCESS;
+}
+
+// Decode-only pass over wire-format transactions (the same GPU decoder as eges_sender_raw_batch,
+// no recovery): *bad = some item fails rlp.DecodeBytes.
+int decode_check_raw(const uint8_t* raw, const uint64_t* offsets, size_t n, int signer, uint64_t chain_id, bool* bad) {
+  *bad = false;
+  if (n == 0) return EGES_SUCCESS;
+  std::vector<uint8_t> vf(n);
+  HostJob j;
+  j.kind = HostJob::SENDER_RAW;
+  j.decode_only = true;
+  j.a = raw;
+  j.offsets = offsets;
+  j.signer = signer;
+  j.chain_id = chain_id;
+  j.status = vf.data();
+  const int rc = run_host(j, n);
+  if (rc) return rc;
+  for (uint8_t f : vf)
+    if (f & VF_DECODE_ERR) *bad = true;
   return EGES_SUCCESS;
 }
 
@@ -897,6 +984,8 @@ struct RecoverReq {
   const uint8_t* sig;
   uint8_t* pub;
   int result = 0;
+  int rc = EGES_SUCCESS;  // the group's engine call; nonzero: result 0 is an engine failure
+  std::string err;        //   and its error text, for the caller's eges_last_error
   std::atomic<bool> done{false};
   std::atomic<bool> queued{false};
 };
@@ -906,6 +995,8 @@ struct VerifyReq {
   const uint8_t* pub;
   uint8_t publen;
   int result = 0;
+  int rc = EGES_SUCCESS;
+  std::string err;
   std::atomic<bool> done{false};
   std::atomic<bool> queued{false};
 };
@@ -922,6 +1013,8 @@ void run_group(std::vector<RecoverReq*>& g) {
     const bool ok = rc == EGES_SUCCESS && st[i] == EGES_OK;
     if (ok) std::memcpy(g[i]->pub, &pub[i * 65], 65);
     g[i]->result = ok ? 1 : 0;
+    g[i]->rc = rc;
+    if (rc) g[i]->err = t_err;
   }
 }
 void run_group(std::vector<VerifyReq*>& g) {
@@ -934,7 +1027,11 @@ void run_group(std::vector<VerifyReq*>& g) {
     std::memcpy(&sig[i * 64], g[i]->sig, 64);
   }
   const int rc = eges_verify_batch(pub.data(), publen.data(), msg.data(), sig.data(), n, ok.data());
-  for (size_t i = 0; i < n; ++i) g[i]->result = (rc == EGES_SUCCESS && ok[i]) ? 1 : 0;
+  for (size_t i = 0; i < n; ++i) {
+    g[i]->result = (rc == EGES_SUCCESS && ok[i]) ? 1 : 0;
+    g[i]->rc = rc;
+    if (rc) g[i]->err = t_err;
+  }
 }
 
 // Up to NLANES groups are in flight at once (one per small-call lane of the device), so a
@@ -957,8 +1054,8 @@ struct Coalescer {
   std::atomic<int> spinners{0};        // callers spinning on their completion flag
   size_t last_group = 1;         // guarded by mu
 
-  static std::chrono::microseconds knob(const char* name, int dflt) {
-    return std::chrono::microseconds(std::max(0, env_int(name, dflt)));
+  static std::chrono::microseconds us_knob(KnobId k) {
+    return std::chrono::microseconds(std::max<long long>(0, knob(k)));
   }
   bool may_lead(const Req* r) const {
     return r->queued.load(std::memory_order_relaxed) && inflight.load(std::memory_order_relaxed) < NLANES &&
@@ -967,7 +1064,7 @@ struct Coalescer {
 
   // mu held on entry and exit; the caller has counted this group in `inflight` and set `gathering`
   void lead(std::unique_lock<std::mutex>& lk) {
-    static const auto gather = knob("EGES_COALESCE_GATHER_US", 20);
+    const auto gather = us_knob(KNOB_COALESCE_GATHER_US);
     const size_t want = std::min(last_group, MAX_GROUP);
     if (queue.size() < want && gather.count() > 0) {
       lk.unlock();
@@ -994,7 +1091,7 @@ struct Coalescer {
   }
 
   void submit(Req* r) {
-    static const auto spin = knob("EGES_COALESCE_SPIN_US", 2000);
+    const auto spin = us_knob(KNOB_COALESCE_SPIN_US);
     const auto t0 = std::chrono::steady_clock::now();
     std::unique_lock<std::mutex> lk(mu);
     r->queued.store(true, std::memory_order_relaxed);
@@ -1011,7 +1108,7 @@ struct Coalescer {
       // served by another leader's group, or waiting for a free lane: spin, then block. At most
       // EGES_COALESCE_SPINNERS callers spin at once: with more spinning threads than the
       // process's CPUs the leaders that launch and collect the groups get descheduled
-      static const int max_spinners = std::max(0, env_int("EGES_COALESCE_SPINNERS", 8));
+      const int max_spinners = (int)std::max<long long>(0, knob(KNOB_COALESCE_SPINNERS));
       lk.unlock();
       bool block = spinners.fetch_add(1, std::memory_order_relaxed) >= max_spinners;
       while (!block && !r->done.load(std::memory_order_acquire)) {
@@ -1033,6 +1130,10 @@ Coalescer<VerifyReq> g_verify_co;
 
 }  // namespace
 
+namespace eges {
+long long knob(KnobId k) { return g_knob[k].load(std::memory_order_relaxed); }
+}  // namespace eges
+
 // ====================================================================== C ABI
 extern "C" {
 
@@ -1042,6 +1143,7 @@ const char* eges_last_error(void) { return t_err.c_str(); }
 
 int eges_init(uint32_t device_mask, uint32_t flags) {
   (void)flags;
+  knobs_load_env();
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_inited && !g_devs.empty()) return EGES_SUCCESS;
   int count = 0;
@@ -1152,6 +1254,9 @@ int eges_block_senders_raw(const uint8_t* block, size_t len, uint32_t lists, int
     *block_status = EGES_DECODE_FAILED;
     return EGES_SUCCESS;
   }
+  // the structure decodes: *block_status and counts are valid from here on, also when the
+  // selected lists exceed cap (the caller's sizing call)
+  *block_status = EGES_OK;
   size_t total = 0;
   for (int k = 0; k < 3; ++k) {
     counts[k] = (uint32_t)(offs[k].size() - 1);
@@ -1159,11 +1264,19 @@ int eges_block_senders_raw(const uint8_t* block, size_t len, uint32_t lists, int
   }
   if (total > cap) return set_err(EGES_E_INVALID_ARG, "block has %zu selected transactions, cap %zu", total, cap);
   if (total && (!addr_out || !status)) return set_err(EGES_E_NULLPTR, "NULL output");
-  *block_status = EGES_OK;
   size_t base = 0;
   for (int k = 0; k < 3; ++k) {
-    if (!(lists & (1u << k)) || counts[k] == 0) continue;
+    if (counts[k] == 0) continue;
     const std::vector<uint64_t>& o = offs[k];
+    if (!(lists & (1u << k))) {
+      // rlp.DecodeBytes(block) decodes every list: an undecodable transaction of an unselected
+      // list fails the block too. Decode-only pass (the GPU decoder, no recovery).
+      bool bad = false;
+      const int rc = decode_check_raw(block + o[0], o.data(), counts[k], signer, chain_id, &bad);
+      if (rc) return rc;
+      if (bad) *block_status = EGES_DECODE_FAILED;
+      continue;
+    }
     const int rc = eges_sender_raw_batch(block + o[0], o.data(), counts[k], signer, chain_id, addr_out + base * 20,
                                          status + base, nullptr);
     if (rc) return rc;
@@ -1206,6 +1319,9 @@ int eges_ecdsa_recover(unsigned char* pubkey_out65, const unsigned char* sigdata
   if (!pubkey_out65 || !sigdata65 || !msgdata32) return 0;
   RecoverReq r{msgdata32, sigdata65, pubkey_out65};
   g_recover_co.submit(&r);
+  // the reference returns 0 for every failure; an engine failure (no device, HIP error) also
+  // leaves its text for eges_last_error on this caller's thread, and "" on success
+  t_err = r.rc ? r.err : std::string();
   return r.result;
 }
 
@@ -1215,6 +1331,7 @@ int eges_ecdsa_verify(const unsigned char* sigdata64, const unsigned char* msgda
   if (pubkeylen != 33 && pubkeylen != 65) return 0;  // eckey_pubkey_parse accepts only these sizes
   VerifyReq r{sigdata64, msgdata32, pubkeydata, (uint8_t)pubkeylen};
   g_verify_co.submit(&r);
+  t_err = r.rc ? r.err : std::string();
   return r.result;
 }
 
@@ -1320,6 +1437,46 @@ int eges_synth_sign_msg_dev(int device, uint64_t first_index, size_t n, const ui
   if (n == 0) return EGES_SUCCESS;
   if (!msg_in || !sig || !addr_expected) return set_err(EGES_E_NULLPTR, "NULL argument");
   return synth_common(device, first_index, n, msg_in, nullptr, sig, addr_expected, stream);
+}
+
+int eges_diag_counters(int device, uint64_t* out, size_t n, int reset) {
+  if (!out && n) return set_err(EGES_E_NULLPTR, "out is NULL");
+  std::vector<DevPtr> devs;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (const DevPtr& d : g_devs)
+      if (d->id == device) devs.push_back(d);
+  }
+  if (devs.empty()) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
+  uint64_t sum[DIAG_WORDS] = {0};
+  for (const DevPtr& d : devs) {  // every logical instance of the device
+    std::lock_guard<std::mutex> dl(d->mu);
+    DevGuard g(d->id);
+    uint32_t w[DIAG_WORDS];
+    HIPCHK(hipDeviceSynchronize());  // the lanes' and the callers' streams too
+    HIPCHK(hipMemcpy(w, d->diag, sizeof w, hipMemcpyDeviceToHost));
+    for (int k = 0; k < DIAG_WORDS; ++k) sum[k] += w[k];
+    if (reset) HIPCHK(hipMemset(d->diag, 0, sizeof w));
+  }
+  for (size_t k = 0; k < n && k < (size_t)DIAG_WORDS; ++k) out[k] = sum[k];
+  return EGES_SUCCESS;
+}
+
+int eges_test_set_knob(const char* name, long long value) {
+  knobs_load_env();  // a value set before the first eges_init is not overwritten by it
+  const int k = knob_index(name);
+  if (k < 0) return set_err(EGES_E_INVALID_ARG, "unknown knob %s", name ? name : "(null)");
+  g_knob[k].store(value, std::memory_order_relaxed);
+  return EGES_SUCCESS;
+}
+
+int eges_test_get_knob(const char* name, long long* value) {
+  knobs_load_env();
+  const int k = knob_index(name);
+  if (k < 0) return set_err(EGES_E_INVALID_ARG, "unknown knob %s", name ? name : "(null)");
+  if (!value) return set_err(EGES_E_NULLPTR, "value is NULL");
+  *value = g_knob[k].load(std::memory_order_relaxed);
+  return EGES_SUCCESS;
 }
 
 void eges_keccak256(const uint8_t* data, size_t len, uint8_t* out32) {

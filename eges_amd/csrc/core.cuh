@@ -25,6 +25,7 @@
 #include "ge.cuh"
 #include "keccak.cuh"
 #include "launch.h"
+#include "eges.h"  // EGES_DIAG_* counter indices
 
 namespace eges {
 
@@ -86,6 +87,28 @@ DEV ge gen_point() {
   g.x = fe_const(GEN_X);
   g.y = fe_const(GEN_Y);
   return g;
+}
+
+// ------------------------------------------------------------------ diagnostics
+// Where a kernel's rare exact branches report (EGES_DIAG_*, eges_diag_counters) and whether a
+// test forces every exact-redo pass (KNOB_FORCE_REDO). Both wave-uniform.
+struct Diag {
+  uint32_t* ctr = nullptr;
+  bool force = false;
+};
+// one increment per wave: the first active lane adds (a vector-memory atomic)
+DEV void diag_bump(const Diag& d, int k) {
+  if (!d.ctr) return;
+  const uint64_t act = __ballot(1);
+  if ((uint32_t)__lane_id() == (uint32_t)__builtin_ctzll(act))
+    __hip_atomic_fetch_add(d.ctr + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class P>
+DEV Diag diag_of(const P& prm) {
+  Diag d;
+  d.ctr = prm.diag;
+  d.force = prm.force_redo != 0;
+  return d;
 }
 
 // ------------------------------------------------------------------ cross-lane helpers
@@ -245,11 +268,12 @@ DEV ge load_pt(const uint32_t* src) {
 // ------------------------------------------------------------------ Strauss step
 // acc += p when `use`; acc_inf tracks the point at infinity. Exceptional sums (acc == +-p)
 // are resolved exactly on a wave-uniform slow path.
-DEV void add_step(gej& acc, bool& inf, const ge& p, bool use) {
+DEV void add_step(gej& acc, bool& inf, const ge& p, bool use, const Diag& dg) {
   bool hz, rz;
   gej s = gej_add_ge(acc, p, hz, rz);
   const bool exc = use && !inf && hz;
   if (__any(exc)) {
+    diag_bump(dg, EGES_DIAG_LS_EXC);
     gej d = gej_double(acc);
     s = gej_select(exc && rz, d, s);
   }
@@ -261,11 +285,12 @@ DEV void add_step(gej& acc, bool& inf, const ge& p, bool use) {
 }
 
 // acc (on the table's isomorphic curve, global Z = zeta) += p (affine on the true curve).
-DEV void add_step_zinv(gej& acc, bool& inf, const ge& p, bool use, const fe& zeta) {
+DEV void add_step_zinv(gej& acc, bool& inf, const ge& p, bool use, const fe& zeta, const Diag& dg) {
   bool hz, rz;
   gej s = gej_add_ge_zinv(acc, p, zeta, hz, rz);
   const bool exc = use && !inf && hz;
   if (__any(exc)) {
+    diag_bump(dg, EGES_DIAG_LS_EXC);
     gej d = gej_double(acc);
     s = gej_select(exc && rz, d, s);
   }
@@ -436,7 +461,7 @@ DEV int rdig_entry(const CoreLds& L, int j, int w) {
 // Strauss-Shamir over the digits in L and the tables (per-lane R table at `base`, G / lambda G
 // in gtab): acc = sum of the window contributions on the R table's isomorphic curve.
 template <bool CHECKED>
-DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab, CoreLds& L) {
+DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab, CoreLds& L, const Diag& dg) {
   const int tid = threadIdx.x;
 #if EGES_PF
 #pragma unroll
@@ -474,12 +499,12 @@ DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab
       else p = load_pt(gtab + ((size_t)(j - 2) * GTAB + e) * PT_WORDS);
       if (j == 1) p.x = fe_mul(p.x, fe_const(FE_BETA));
       if (j < 2) {
-        if (CHECKED) add_step(acc, inf, neg_if(p, d < 0), d != 0);
+        if (CHECKED) add_step(acc, inf, neg_if(p, d < 0), d != 0, dg);
         else add_step_fast(acc, inf, neg_if(p, d < 0), d != 0);
       } else {
         fe z;
         lds_get<FE_LIMBS>(L.zeta, z.v);
-        if (CHECKED) add_step_zinv(acc, inf, neg_if(p, d < 0), d != 0, z);
+        if (CHECKED) add_step_zinv(acc, inf, neg_if(p, d < 0), d != 0, z, dg);
         else add_step_zinv_fast(acc, inf, neg_if(p, d < 0), d != 0, z);
       }
     }
@@ -497,7 +522,7 @@ DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab
 // possibly a dummy for failed lanes). Returns Jacobian Q and its infinity flag.
 template <class ST = NoStamp>
 DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& u_g, const uint32_t* gtab,
-                     uint32_t* ws, CoreLds& L, ST* st = nullptr) {
+                     uint32_t* ws, CoreLds& L, ST* st = nullptr, const Diag& dg = Diag()) {
   const int tid = threadIdx.x;
   uint32_t* const base = ws + (size_t)blockIdx.x * WS_WORDS;
   // --- digits
@@ -560,8 +585,11 @@ DEV void ecmult_core(gej& acc, bool& inf, const ge& P, const sc& u_r, const sc& 
   }
   if (st) st->mark(3);
   // --- Strauss-Shamir, unchecked; exact redo of the whole wave if any lane was poisoned
-  strauss<false>(acc, inf, base, gtab, L);
-  if (__any(!inf && fe_is_zero(acc.z))) strauss<true>(acc, inf, base, gtab, L);
+  strauss<false>(acc, inf, base, gtab, L, dg);
+  if (dg.force || __any(!inf && fe_is_zero(acc.z))) {
+    diag_bump(dg, EGES_DIAG_LS_REDO);
+    strauss<true>(acc, inf, base, gtab, L, dg);
+  }
   // true Jacobian Z of the accumulator
   {
     fe z;

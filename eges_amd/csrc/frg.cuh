@@ -106,8 +106,9 @@ DEV fr gejq_zaddu(ger& t, ger& b) {
 // General Jacobian addition a + b (add-2007-bl, 11M + 5S in 5 quad levels), both points in the
 // same coordinates, with infinity flags in and out; wave-uniform exceptional cases resolved
 // exactly (a == b doubles, a == -b is infinity). Used once per signature to join the partial
-// sums of the wide latency kernel. In: X m1, Y <= 2, Z <= 2. Out: X, Y m1, Z m2.
-DEV gejr gejq_add(const gejr& a, bool ainf, const gejr& b, bool binf, bool& rinf) {
+// sums of the wide latency kernel. In: X m1, Y <= 2, Z <= 2. Out: X, Y m1, Z m2. *exc (nullable)
+// reports which exact branch ran: 0 none, 1 a == b, 2 a == -b.
+DEV gejr gejq_add(const gejr& a, bool ainf, const gejr& b, bool binf, bool& rinf, int* exc = nullptr) {
   fr Z1Z1, Z2Z2, Y1Z2, Y2Z1;
   fr_mul4(Z1Z1, Z2Z2, Y1Z2, Y2Z1, a.z, a.z, b.z, b.z, a.y, b.z, b.y, a.z);
   fr U1, U2, S1, S2;
@@ -126,13 +127,16 @@ DEV gejr gejq_add(const gejr& a, bool ainf, const gejr& b, bool binf, bool& rinf
   r.y = fr_normalize_weak(fr_sub<2>(W, fr_add(SJ, SJ)));             // r (V - X3) - 2 S1 J
   r.z = fr_add(ZH, ZH);                                               // 2 Z1 Z2 H
   rinf = false;
+  if (exc) *exc = 0;
   if (ainf) {
     rinf = binf;
     return b;
   }
   if (binf) return a;
   if (fr_is_zero(H)) {  // same x: a == b or a == -b
-    if (fr_is_zero(Rd)) return gejq_double(a);
+    const bool dbl = fr_is_zero(Rd);
+    if (exc) *exc = dbl ? 1 : 2;
+    if (dbl) return gejq_double(a);
     rinf = true;
   }
   return r;

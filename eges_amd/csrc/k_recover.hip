@@ -104,7 +104,7 @@ DEV void recover_body(const RecoverParams& prm, uint64_t* stamps) {
     park_put<FE_LIMBS>(prm.ws, 8, zpre.v);
     gej Q;
     bool qinf;
-    ecmult_core(Q, qinf, Rp, u2, u1, prm.gtab, prm.ws, L, st);
+    ecmult_core(Q, qinf, Rp, u2, u1, prm.gtab, prm.ws, L, st, diag_of(prm));
     park_get<8>(prm.ws, 0, rinv_acc.v);
     park_get<FE_LIMBS>(prm.ws, 8, zpre.v);
     ok = ok && !qinf;  // main_impl.h:120

@@ -133,14 +133,17 @@ DEV ger ger_neg_if(const ger& p, bool neg) {
 
 // acc += p (core.cuh add_step / add_step_fast, quad form; inf is wave-uniform)
 template <bool CHECKED>
-DEV void add_r(gejr& acc, bool& inf, const ger& p, bool use) {
+DEV void add_r(gejr& acc, bool& inf, const ger& p, bool use, const Diag& dg) {
   gejr s;
   bool to_inf = false;
   if (CHECKED) {
     bool hz, rz;
     s = gejq_add_ge_t<ADD_PLAIN, true>(acc, p, nullptr, hz, rz);
     const bool exc = use && !inf && hz;
-    if (__any(exc)) s = gejr_select(exc && rz, gejq_double(acc), s);
+    if (__any(exc)) {
+      diag_bump(dg, EGES_DIAG_LAT_EXC);
+      s = gejr_select(exc && rz, gejq_double(acc), s);
+    }
     to_inf = exc && !rz;
   } else {
     bool h, r;
@@ -258,7 +261,7 @@ DEV fr build_table_wave(const ger& P, TabT<NT>& tab, ColT<NT>& zrs) {
 // one addition per selected half. The narrow form runs [0, RWIN) with both halves.
 template <bool CHECKED, int BITS, int NT>
 DEV void strauss_win(gejr& acc, bool& inf, const TabT<NT>& tab, const ColT<NT>& btab, const int8_t* d0,
-                     const int8_t* d1, int jmask, int wlo, int whi) {
+                     const int8_t* d1, int jmask, int wlo, int whi, const Diag& dg) {
   inf = true;
   acc.x = fr_zero();
   acc.y = fr_zero();
@@ -277,19 +280,22 @@ DEV void strauss_win(gejr& acc, bool& inf, const TabT<NT>& tab, const ColT<NT>& 
       const int e = a > 0 ? a - 1 : 0;
       ger p = lds_pt(tab[e]);
       if (j == 1) p.x.v = btab[e][row_lane()];  // lambda (x, y) = (beta x, y)
-      add_r<CHECKED>(acc, inf, ger_neg_if(p, d < 0), d != 0);
+      add_r<CHECKED>(acc, inf, ger_neg_if(p, d < 0), d != 0, dg);
     }
   }
 }
 template <int BITS, int NT>
 DEV void strauss_win_exact(gejr& acc, bool& inf, const TabT<NT>& tab, const ColT<NT>& btab, const int8_t* d0,
-                           const int8_t* d1, int jmask, int wlo, int whi) {
-  strauss_win<false, BITS, NT>(acc, inf, tab, btab, d0, d1, jmask, wlo, whi);
-  if (__any(!inf && fr_is_zero(acc.z))) strauss_win<true, BITS, NT>(acc, inf, tab, btab, d0, d1, jmask, wlo, whi);
+                           const int8_t* d1, int jmask, int wlo, int whi, const Diag& dg) {
+  strauss_win<false, BITS, NT>(acc, inf, tab, btab, d0, d1, jmask, wlo, whi, dg);
+  if (dg.force || __any(!inf && fr_is_zero(acc.z))) {
+    diag_bump(dg, EGES_DIAG_LAT_REDO);
+    strauss_win<true, BITS, NT>(acc, inf, tab, btab, d0, d1, jmask, wlo, whi, dg);
+  }
 }
 // u_g G from the comb table: one addition per 16-bit digit, no doublings (true curve).
 template <bool CHECKED>
-DEV void strauss_gcomb(gejr& acc, bool& inf, const LatLds& S, const uint32_t* gcomb) {
+DEV void strauss_gcomb(gejr& acc, bool& inf, const LatLds& S, const uint32_t* gcomb, const Diag& dg) {
   inf = true;
   acc.x = fr_zero();
   acc.y = fr_zero();
@@ -298,8 +304,24 @@ DEV void strauss_gcomb(gejr& acc, bool& inf, const LatLds& S, const uint32_t* gc
   for (int k = 0; k < CWIN; ++k) {
     const int d = (int)S.cdig[k];
     const ger p = gtab_pt(gcomb + ((size_t)k * CTAB + (d > 0 ? d - 1 : 0)) * PT_WORDS);
-    add_r<CHECKED>(acc, inf, p, d != 0);
+    add_r<CHECKED>(acc, inf, p, d != 0, dg);
   }
+}
+// u_g G, unchecked, with the exact redo (every digit is nonzero-checked, so a poisoned sum
+// shows as Z == 0 and not infinity)
+DEV void gcomb_exact(gejr& A, bool& ainf, const LatLds& S, const uint32_t* gcomb, const Diag& dg) {
+  strauss_gcomb<false>(A, ainf, S, gcomb, dg);
+  if (dg.force || __any(!ainf && fr_is_zero(A.z))) {
+    diag_bump(dg, EGES_DIAG_COMB_REDO);
+    strauss_gcomb<true>(A, ainf, S, gcomb, dg);
+  }
+}
+// exact join of two partial sums, the exceptional branch counted
+DEV gejr join_parts(const gejr& a, bool ainf, const gejr& b, bool binf, bool& rinf, const Diag& dg) {
+  int exc;
+  const gejr r = gejq_add(a, ainf, b, binf, rinf, &exc);
+  if (exc) diag_bump(dg, exc == 1 ? EGES_DIAG_JOIN_DBL : EGES_DIAG_JOIN_INF);
+  return r;
 }
 DEV void put_part(LatLds& S, int k, const gejr& a, bool inf) {
   const uint32_t L = row_lane();
@@ -347,7 +369,8 @@ DEV bool lift_y(fr& y, const fr& c, bool odd) {
 
 // Narrow form, wave 1 after the barrier: the square root (when the point came compressed) and
 // the u_g G comb part into LDS, then the second barrier. Both run beside wave 0's Strauss loop.
-DEV void helper_wave(LatLds& S, const uint32_t* gcomb, bool need_y, const fr& c, bool odd, const fr& y_given) {
+DEV void helper_wave(LatLds& S, const uint32_t* gcomb, bool need_y, const fr& c, bool odd, const fr& y_given,
+                     const Diag& dg) {
   fr y = y_given;
   bool ok = true;
 #ifndef EGES_PROBE_NO_SQRT  // diagnostic probe only: the narrow form's time without the root
@@ -357,13 +380,13 @@ DEV void helper_wave(LatLds& S, const uint32_t* gcomb, bool need_y, const fr& c,
   if (lane_id() == 0) S.yok = ok ? 1u : 0u;
   gejr A;
   bool ainf;
-  strauss_gcomb<false>(A, ainf, S, gcomb);
-  if (__any(!ainf && fr_is_zero(A.z))) strauss_gcomb<true>(A, ainf, S, gcomb);
+  gcomb_exact(A, ainf, S, gcomb, dg);
   put_part(S, 2, A, ainf);
   __syncthreads();  // partial sums and y ready
 }
 // Split form, wave 1 after its scalar work: y (the square root, or the given y), then u_g G.
-DEV void helper_split(LatLds& S, const uint32_t* gcomb, bool need_y, const fr& c, bool odd, const fr& y_given) {
+DEV void helper_split(LatLds& S, const uint32_t* gcomb, bool need_y, const fr& c, bool odd, const fr& y_given,
+                      const Diag& dg) {
   fr y = y_given;
   bool ok = true;
   if (need_y) ok = lift_y(y, c, odd);
@@ -372,8 +395,7 @@ DEV void helper_split(LatLds& S, const uint32_t* gcomb, bool need_y, const fr& c
   flag_set(&S.flag[F_Y]);
   gejr A;
   bool ainf;
-  strauss_gcomb<false>(A, ainf, S, gcomb);
-  if (__any(!ainf && fr_is_zero(A.z))) strauss_gcomb<true>(A, ainf, S, gcomb);
+  gcomb_exact(A, ainf, S, gcomb, dg);
   put_part(S, 2, A, ainf);
   flag_set(&S.flag[F_G]);
 }
@@ -381,7 +403,7 @@ DEV void helper_split(LatLds& S, const uint32_t* gcomb, bool need_y, const fr& c
 // (each wave its own copy, no hand-off), the table of D's (X, Y) on the curve where it is affine,
 // the high windows of one GLV half, then back to the true curve: a sum (X, Y, Z) there is the E'
 // point (X, Y, Z zeta_D Z_D) and the E point (X, Y, Z zeta_D Z_D y). Wave 2 joins wave 3's part.
-DEV void high_wave(LatLds& S, const fr& x, const fr& c, int j) {
+DEV void high_wave(LatLds& S, const fr& x, const fr& c, int j, const Diag& dg) {
   gejr D;
   fr_mul2(D.x, D.y, c, x, c, c);  // R' = (c x, c^2)
   D.z = fr_one();
@@ -396,7 +418,7 @@ DEV void high_wave(LatLds& S, const fr& x, const fr& c, int j) {
   flag_wait(&S.flag[F_DIG]);
   gejr A;
   bool ainf;
-  strauss_win_exact<HBITS, HTAB>(A, ainf, S.dtab[j], S.dbtab, S.hdig[0], S.hdig[1], 1 << j, 0, HWIN);
+  strauss_win_exact<HBITS, HTAB>(A, ainf, S.dtab[j], S.dbtab, S.hdig[0], S.hdig[1], 1 << j, 0, HWIN, dg);
   flag_wait(&S.flag[F_Y]);
   A.z = fr_mul(A.z, fr_mul(scale, fr{S.ylift[row_lane()]}));
   if (j == 1) {
@@ -407,7 +429,7 @@ DEV void high_wave(LatLds& S, const fr& x, const fr& c, int j) {
   flag_wait(&S.flag[F_LHI]);
   bool linf;
   const gejr Lp = get_part(S, 4, linf);
-  A = gejq_add(A, ainf, Lp, linf, ainf);
+  A = join_parts(A, ainf, Lp, linf, ainf, dg);
   put_part(S, 3, A, ainf);
   flag_set(&S.flag[F_HI]);
 }
@@ -424,7 +446,7 @@ struct RootSrc {  // narrow recover form: where wave 0 finds R's y (root_fetch)
   bool odd;
 };
 template <class ST, bool SPLIT>
-DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& S, ST* st,
+DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& S, ST* st, const Diag& dg,
                          const RootSrc* root = nullptr) {
   ger Rp;
   fr_mul2(Rp.x, Rp.y, c, x, c, c);  // (c x, c^2)
@@ -436,7 +458,7 @@ DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& 
   st->mark(1);
   gejr A;
   bool ainf;
-  strauss_win_exact<RBITS, PTAB>(A, ainf, S.tab, S.btab, S.rdig[0], S.rdig[1], 3, 0, SPLIT ? SPLIT_W0 : RWIN);
+  strauss_win_exact<RBITS, PTAB>(A, ainf, S.tab, S.btab, S.rdig[0], S.rdig[1], 3, 0, SPLIT ? SPLIT_W0 : RWIN, dg);
   if (SPLIT) flag_wait(&S.flag[F_Y]);
   else __syncthreads();  // partial sums (and y) ready
   if (root) root_fetch(*root->prm, root->idx, c, root->odd, S);  // (this wave's own LDS words)
@@ -444,12 +466,12 @@ DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& 
   bool ginf;
   if (SPLIT) flag_wait(&S.flag[F_G]);
   const gejr Gp = get_part(S, 2, ginf);
-  Q = gejq_add(A, ainf, Gp, ginf, qinf);
+  Q = join_parts(A, ainf, Gp, ginf, qinf, dg);
   if (SPLIT) {
     flag_wait(&S.flag[F_HI]);
     bool hinf;
     const gejr Hp = get_part(S, 3, hinf);
-    Q = gejq_add(Q, qinf, Hp, hinf, qinf);
+    Q = join_parts(Q, qinf, Hp, hinf, qinf, dg);
   }
   st->mark(4);
 }
@@ -464,6 +486,7 @@ DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& 
 // computes the root itself, so the result never depends on the helpers being scheduled.
 constexpr uint32_t ROOT_TAG = 0x9E3779B9u, ROOT_TAG2 = 0x7F4A7C15u;
 constexpr int ROOT_WORDS = 11;
+static_assert(ROOT_WORDS <= SLOT_ROWS * 4, "the root words live in the slot rows");
 constexpr int ROOT_WG = LAT_WG;  // helper lanes per workgroup (same block size as the kernel)
 DEV uint32_t* root_area(const RecoverParams& prm) {
   return const_cast<uint32_t*>(prm.rec) + (size_t)REC_ROWS * prm.n_pad;
@@ -575,6 +598,7 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   __shared__ LatLds S;
   ST st_;
   ST* st = &st_;
+  const Diag dg = diag_of(prm);
   if (!SPLIT && blockIdx.x < prm.n_helpers) {  // narrow form: the lane-serial roots
     root_helper(prm);
     return;
@@ -620,15 +644,15 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
     }
     if (SPLIT) {
       flag_set(&S.flag[F_DIG]);
-      helper_split(S, gcomb, true, c, odd, fr_zero());
+      helper_split(S, gcomb, true, c, odd, fr_zero(), dg);
     } else {
       __syncthreads();  // digits ready (and the table)
-      helper_wave(S, gcomb, false, c, odd, fr_zero());  // y: the helper workgroups (root_fetch)
+      helper_wave(S, gcomb, false, c, odd, fr_zero(), dg);  // y: the helper workgroups (root_fetch)
     }
     return;
   }
   if (SPLIT && (wv == 2 || wv == 3)) {
-    high_wave(S, x, c, (int)wv - 2);
+    high_wave(S, x, c, (int)wv - 2, dg);
     return;
   }
   st->mark(0);
@@ -636,7 +660,7 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   gejr Q;
   bool qinf;
   const RootSrc root{&prm, idx, odd};
-  ecmult_deferred<ST, SPLIT>(Q, qinf, x, c, S, st, SPLIT ? nullptr : &root);
+  ecmult_deferred<ST, SPLIT>(Q, qinf, x, c, S, st, dg, SPLIT ? nullptr : &root);
   ok = ok && S.yok != 0 && !qinf;  // ge_set_xo_var failure, main_impl.h:120
   // --- affine, serialize, address
   const fr zq = fr_select(ok, Q.z, fr_one());
@@ -702,6 +726,7 @@ template <bool SPLIT>
 DEV void verify_lat_body(const VerifyParams& prm) {
   __shared__ LatLds S;
   NoStamp st_;
+  const Diag dg = diag_of(prm);
   const uint32_t idx = blockIdx.x;  // grid = n
   if (SPLIT) {
     if (threadIdx.x < NFLAGS) S.flag[threadIdx.x] = 0u;
@@ -749,21 +774,21 @@ DEV void verify_lat_body(const VerifyParams& prm) {
     // the square root only for 33-byte keys; 65-byte keys give y
     if (SPLIT) {
       flag_set(&S.flag[F_DIG]);
-      helper_split(S, gcomb, c33, c, pfx == 3, Y);
+      helper_split(S, gcomb, c33, c, pfx == 3, Y, dg);
     } else {
       __syncthreads();  // digits ready (and the table)
-      helper_wave(S, gcomb, c33, c, pfx == 3, Y);
+      helper_wave(S, gcomb, c33, c, pfx == 3, Y, dg);
     }
     return;
   }
   if (SPLIT && (wv == 2 || wv == 3)) {
-    high_wave(S, x, c, (int)wv - 2);
+    high_wave(S, x, c, (int)wv - 2, dg);
     return;
   }
   const bool on = fr_equal(c, fr_sqr(Y));  // 65-byte keys: on the curve
   gejr Q;
   bool qinf;
-  ecmult_deferred<NoStamp, SPLIT>(Q, qinf, x, c, S, &st_);
+  ecmult_deferred<NoStamp, SPLIT>(Q, qinf, x, c, S, &st_, dg);
   const bool pk_ok = c33 ? (x_ok && S.yok != 0) : (c65 && x_ok && y_ok && !hybrid_bad && on);
   bool ok = sig_ok && pk_ok && !qinf;
   // x(Q) mod n == r  <=>  r Z^2 == X  or  (r < p - n and (r + n) Z^2 == X)  (ecdsa_impl.h:246-270)
@@ -809,7 +834,7 @@ static RecoverParams with_helpers(const RecoverParams& p0) {
   RecoverParams p = p0;
   p.n_helpers = p.wide ? 0u : (p.n + ROOT_WG - 1) / ROOT_WG;
   // tests only: no helper workgroups, so every signature wave takes root_fetch's own-root path
-  if (const char* e = std::getenv("EGES_TEST_ROOT_HELPERS"); e && *e == '0') p.n_helpers = 0;
+  if (knob(KNOB_ROOT_HELPERS) == 0) p.n_helpers = 0;
   p.epoch = g_root_epoch.fetch_add(1) + 1u;
   return p;
 }

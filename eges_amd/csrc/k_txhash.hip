@@ -292,7 +292,6 @@ constexpr int TXW_WAVES = 4;      // waves per workgroup
 constexpr int TXW_STAGE = 1024;   // staged bytes per wave; longer encodings decode from global memory
 // Up to block-sized batches the wave form wins (C3 from wire bytes: 0.325 -> 0.261 ms/block);
 // at 10k transfers the two tie, and beyond the lane-serial form does (100k: 1.91 vs 2.26 ms).
-constexpr uint32_t TXW_DEFAULT_MAX = 8192;
 
 // Big-endian integer content -> byte `lane` of the 32-byte row (lanes 0..31).
 DEV uint32_t rlp_be32_byte(const uint8_t* __restrict__ p, const RlpHead& h, uint32_t lane) {
@@ -370,9 +369,8 @@ __global__ void __launch_bounds__(64 * TXW_WAVES) tx_rows_wave_kernel(
 hipError_t launch_tx_rows(const uint8_t* raw, const uint64_t* offsets, uint64_t first, uint32_t n, int signer,
                           uint64_t chain_id, uint8_t* sighash, uint8_t* r, uint8_t* s, uint8_t* v, uint8_t* vflags,
                           hipStream_t st) {
-  // EGES_TXROWS_WAVE_MAX overrides the cut (0: never the wave form); read per call so tests can A/B
-  const char* e = std::getenv("EGES_TXROWS_WAVE_MAX");
-  const uint32_t wave_max = e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : TXW_DEFAULT_MAX;
+  // KNOB_TXROWS_WAVE_MAX (default 8192, capi.hip) sets the cut (0: never the wave form)
+  const uint32_t wave_max = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TXROWS_WAVE_MAX), 1u << 30));
   if (n <= wave_max)
     hipLaunchKernelGGL(tx_rows_wave_kernel, dim3((n + TXW_WAVES - 1) / TXW_WAVES), dim3(64 * TXW_WAVES), 0, st, raw,
                        offsets, first, n, signer, chain_id, sighash, r, s, v, vflags);

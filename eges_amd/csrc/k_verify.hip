@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(WG, 2) verify_kernel(VerifyParams prm) {
     park_put<8>(prm.ws, 0, sinv_acc.v);
     gej Q;
     bool qinf;
-    ecmult_core(Q, qinf, P, u2, u1, prm.gtab, prm.ws, L);
+    ecmult_core<NoStamp>(Q, qinf, P, u2, u1, prm.gtab, prm.ws, L, nullptr, diag_of(prm));
     park_get<8>(prm.ws, 0, sinv_acc.v);
     ok = ok && !qinf;
     // x(Q) mod n == r  <=>  r*Z^2 == X  or  (r < p - n and (r + n)*Z^2 == X)  (ecdsa_impl.h:246-270)

@@ -1,0 +1,32 @@
+// Engine knobs and diagnostic counters (host side of libeges.so).
+//
+// Knobs are read from the environment ONCE, at the first eges_init, and are otherwise changed
+// only through eges_test_set_knob (include/eges.h): no call path after init reads the
+// environment (getenv racing a host application's setenv is undefined behaviour in glibc).
+// The values are atomics, so a test may flip one between calls while other threads run.
+#pragma once
+#include <stdint.h>
+
+namespace eges {
+
+enum KnobId : int {
+  KNOB_LAT_MAX = 0,       // batches of at most this many signatures take the latency kernels
+  KNOB_LAT_WIDE_MAX,      // latency batches of at most this many take the split (4-wave) form
+  KNOB_MID_MAX,           // batches above LAT_MAX and at most this many take the mid-size kernel
+  KNOB_TXROWS_WAVE_MAX,   // wire-format batches of at most this many decode one tx per wave
+  KNOB_ROOT_HELPERS,      // 0: the narrow form launches no root-helper workgroups (tests)
+  KNOB_OVERLAP,           // device-resident recover batches as S overlapped launches (-1 = auto)
+  KNOB_FORCE_REDO,        // tests: run every exact-redo pass as if an accumulator was poisoned
+  KNOB_COALESCE_GATHER_US,  // single-item coalescer: a leader's gather window
+  KNOB_COALESCE_SPIN_US,    //   a waiting caller spins this long before it blocks
+  KNOB_COALESCE_SPINNERS,   //   at most this many callers spin at once
+  KNOB_COUNT
+};
+
+long long knob(KnobId k);
+
+// Diagnostic counters (per device, device memory, incremented by the kernels' rare branches;
+// read by eges_diag_counters). Indices are the EGES_DIAG_* values of include/eges.h.
+constexpr int DIAG_WORDS = 16;
+
+}  // namespace eges

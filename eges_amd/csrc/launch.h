@@ -4,6 +4,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "knobs.h"
+
 namespace eges {
 
 // Record layout produced by the prep kernels: 25 SoA rows of n_pad words
@@ -41,6 +43,10 @@ struct RecoverParams {
   // latency kernel, narrow form: leading workgroups that compute R's y lane-serially (one lane
   // per signature) into the slot rows, tagged with this launch's epoch (set by the launcher)
   uint32_t n_helpers = 0, epoch = 0;
+  // diagnostic counters of the device (EGES_DIAG_*, bumped by the rare exact branches; nullable)
+  uint32_t* diag = nullptr;
+  // tests only (KNOB_FORCE_REDO): run every exact-redo pass as if an accumulator was poisoned
+  uint32_t force_redo = 0;
 };
 
 struct VerifyParams {
@@ -56,6 +62,8 @@ struct VerifyParams {
   uint4* slot;        // VERIFY_SLOT_ROWS rows of n_pad
   uint32_t* order;    // n_pad: processing order (compressed keys first)
   uint32_t* counts;   // 2 counters for the order kernel
+  uint32_t* diag = nullptr;   // as RecoverParams
+  uint32_t force_redo = 0;
 };
 // Verify scratch: slot rows (P affine, prefix product of s), the order, the two counters.
 constexpr int VERIFY_SLOT_ROWS = 7;

@@ -30,6 +30,39 @@ def device_count():
     return lib.eges_device_count()
 
 
+def set_knob(name, value):
+    """eges_test_set_knob: change an engine knob (its environment name) while the engine runs."""
+    check(lib.eges_test_set_knob(name.encode(), int(value)))
+
+
+def get_knob(name):
+    v = ctypes.c_longlong()
+    check(lib.eges_test_get_knob(name.encode(), ctypes.byref(v)))
+    return v.value
+
+
+class knob:
+    """with knob("EGES_LAT_MAX", 0): ... sets a knob for the block and restores it after."""
+
+    def __init__(self, name, value):
+        self.name, self.value = name, value
+
+    def __enter__(self):
+        self.old = get_knob(self.name)
+        set_knob(self.name, self.value)
+        return self
+
+    def __exit__(self, *a):
+        set_knob(self.name, self.old)
+
+
+def diag_counters(device=0, reset=False):
+    """eges_diag_counters: {name: count} of the rare exact branches the kernels ran (DIAG_NAMES)."""
+    out = (ctypes.c_uint64 * _lib.DIAG_COUNT)()
+    check(lib.eges_diag_counters(device, out, _lib.DIAG_COUNT, 1 if reset else 0))
+    return {n: int(out[i]) for i, n in enumerate(_lib.DIAG_NAMES)}
+
+
 def ecrecover_batch(msg, sig, want_pub=True, want_addr=True):
     """crypto.Ecrecover over n items: msg (n,32), sig (n,65) -> (pub (n,65)|None, addr (n,20)|None, status (n,))."""
     msg = _u8(msg, (32,), "msg")

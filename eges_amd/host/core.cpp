@@ -16,8 +16,11 @@ using types::Signer;
 using types::TxPtr;
 
 // ---------------------------------------------------------------- TxPool
-TxPool::TxPool(const types::ChainConfig& cfg, uint64_t head_number)
-    : signer_(Signer::Make(cfg, head_number)) {}  // pool.signer = types.NewEIP155Signer(chainconfig.ChainId)
+// pool.signer = types.NewEIP155Signer(chainconfig.ChainId) (tx_pool.go:227), whatever the fork
+// schedule and the head: the pool accepts EIP-155-protected transactions before the fork block
+TxPool::TxPool(const types::ChainConfig& cfg, uint64_t head_number) : signer_(Signer::EIP155(cfg.chain_id)) {
+  (void)head_number;
+}
 
 std::vector<PoolErr> TxPool::AddRemotes(const std::vector<TxPtr>& txs) { return AddTxsLocked(txs, false); }
 std::vector<PoolErr> TxPool::AddLocals(const std::vector<TxPtr>& txs) { return AddTxsLocked(txs, true); }

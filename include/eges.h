@@ -85,12 +85,13 @@ int eges_abi_version(void);
 /* Replaces secp256k1_ext_ecdsa_recover (crypto/secp256k1/ext.h:30-47).
  * sig65 = R || S || recid, msg32 = hash. Returns 1 and writes the 65-byte uncompressed
  * public key on success, 0 on failure (including recid >= 4, which the reference's
- * parse_compact ARG_CHECK would reject). */
+ * parse_compact ARG_CHECK would reject). An engine failure (no device, HIP error) also returns 0
+ * and leaves its text for eges_last_error on the calling thread ("" after a call that ran). */
 int eges_ecdsa_recover(unsigned char *pubkey_out65, const unsigned char *sigdata65,
                        const unsigned char *msgdata32);
 
 /* Replaces secp256k1_ext_ecdsa_verify (crypto/secp256k1/ext.h:58-75).
- * sig64 = R || S. Returns 1 if valid, 0 otherwise (low-s enforced). */
+ * sig64 = R || S. Returns 1 if valid, 0 otherwise (low-s enforced); engine failures as above. */
 int eges_ecdsa_verify(const unsigned char *sigdata64, const unsigned char *msgdata32,
                       const unsigned char *pubkeydata, size_t pubkeylen);
 
@@ -134,8 +135,10 @@ int eges_sender_raw_batch(const uint8_t *raw, const uint64_t *offsets, size_t n,
  * item count of each list; addr_out / status (cap entries) receive the selected lists' results
  * concatenated in list order. *block_status = EGES_OK, or EGES_DECODE_FAILED when the block
  * structure (or a selected transaction) would make rlp.DecodeBytes fail; header, uncle and
- * confirm-message field contents are not decoded. Returns EGES_E_INVALID_ARG when more than
- * cap transactions are selected. */
+ * confirm-message field contents are not decoded; the transactions of unselected lists are
+ * decoded (not recovered) on the GPU, as rlp.DecodeBytes decodes them too. Returns
+ * EGES_E_INVALID_ARG when more than cap transactions are selected; *block_status and counts are
+ * then still valid (a sizing call). */
 #define EGES_LIST_FAKE 0x1u
 #define EGES_LIST_GEEC 0x2u
 #define EGES_LIST_TXS 0x4u
@@ -195,6 +198,35 @@ int eges_synth_sign_dev(int device, uint64_t first_index, size_t n, uint8_t *msg
  * EIP-155 sighashes). */
 int eges_synth_sign_msg_dev(int device, uint64_t first_index, size_t n, const uint8_t *msg_in, uint8_t *sig,
                             uint8_t *addr_expected, void *stream);
+
+/* ---------------------------------------------------------------- diagnostics and tests */
+
+/* Counters the kernels bump (once per wave) when a rare exact branch runs. The reference takes
+ * these branches inline (group_impl.h:414-461 gej_add_ge_var's a == b doubling and a == -b
+ * infinity); this engine adds without the check and redoes a poisoned accumulator exactly
+ * (DESIGN.md §3.1), or joins partial sums with an exact addition (§3.3). */
+#define EGES_DIAG_LS_REDO 0   /* lane-serial kernels: exact redo of a wave's Strauss loop */
+#define EGES_DIAG_LS_EXC 1    /* lane-serial checked addition met P == +-Q (doubling / infinity) */
+#define EGES_DIAG_LAT_REDO 2  /* latency kernels: exact redo of an R' Strauss part */
+#define EGES_DIAG_LAT_EXC 3   /* latency kernels: checked addition met P == +-Q */
+#define EGES_DIAG_COMB_REDO 4 /* latency kernels: exact redo of the u1*G comb */
+#define EGES_DIAG_JOIN_DBL 5  /* latency kernels: partial sums joined with a == b (doubling) */
+#define EGES_DIAG_JOIN_INF 6  /* latency kernels: partial sums joined with a == -b (infinity) */
+#define EGES_DIAG_MID_REDO 7  /* mid-size kernel: exact redo of an R' Strauss part */
+#define EGES_DIAG_MID_EXC 8   /* mid-size kernel: checked addition met P == +-Q */
+#define EGES_DIAG_MID_JOIN 9  /* mid-size kernel: partial sums joined with a == +-b */
+#define EGES_DIAG_COUNT 16
+/* Copies min(n, EGES_DIAG_COUNT) counters of `device` (summed over the engine's instances of
+ * it) into out; reset != 0 zeroes them afterwards. Synchronises the device. */
+int eges_diag_counters(int device, uint64_t *out, size_t n, int reset);
+
+/* Engine knobs. Read from the environment once, at the first eges_init (EGES_LAT_MAX,
+ * EGES_LAT_WIDE_MAX, EGES_MID_MAX, EGES_TXROWS_WAVE_MAX, EGES_TEST_ROOT_HELPERS, EGES_OVERLAP,
+ * EGES_TEST_FORCE_REDO); no call path reads the environment after that. These two entries
+ * change / read one by its environment name while the engine runs (tests and A/B tools; the
+ * product defaults need neither). Return EGES_E_INVALID_ARG for an unknown name. */
+int eges_test_set_knob(const char *name, long long value);
+int eges_test_get_knob(const char *name, long long *value);
 
 #ifdef __cplusplus
 }

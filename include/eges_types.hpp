@@ -147,6 +147,7 @@ enum class PoolErr : int {
 // types.Sender now hits the cache). Accepted transactions are kept per sender by nonce.
 class TxPool {
  public:
+  // head_number does not pick the signer: the pool always uses EIP155(cfg.chain_id) (tx_pool.go:227)
   explicit TxPool(const types::ChainConfig& cfg, uint64_t head_number = 0);
   std::vector<PoolErr> AddRemotes(const std::vector<types::TxPtr>& txs);  // AddRemotes -> addTxs(false)
   std::vector<PoolErr> AddLocals(const std::vector<types::TxPtr>& txs);   // AddLocals -> addTxs(true)

@@ -312,13 +312,23 @@ def block_senders(oracle, raw, lists_mask, signer, chain_id):
     except DecodeError:
         return [], [], [0, 0, 0], DECODE_FAILED
     sts, addrs = [], []
+    bst = 0
     for k in range(3):
         if lists_mask & (1 << k):
             for item in lists[k]:
                 st, addr, _ = sender_raw(oracle, item, signer, chain_id)
                 sts.append(st)
                 addrs.append(addr)
-    bst = DECODE_FAILED if DECODE_FAILED in sts else 0
+        else:
+            # rlp.DecodeBytes decodes every transaction list of the block (extblock :188-195),
+            # so an undecodable item of an unselected list fails the block too
+            for item in lists[k]:
+                try:
+                    decode_txdata(item)
+                except DecodeError:
+                    bst = DECODE_FAILED
+    if DECODE_FAILED in sts:
+        bst = DECODE_FAILED
     return sts, addrs, [len(x) for x in lists], bst
 
 

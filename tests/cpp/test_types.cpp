@@ -93,6 +93,12 @@ static void cpu_unit() {
         "MakeSigner: Frontier / Homestead / EIP155 by block number");
   c2.eip155_block.reset();
   check(Signer::Make(c2, 1000).Equal(H), "MakeSigner: no EIP-155 fork -> Homestead");
+  // the pool's signer is types.NewEIP155Signer(chainconfig.ChainId) (tx_pool.go:227) whatever
+  // the fork schedule and head: protected transactions stay acceptable before the fork block
+  check(core::TxPool(c2, 1000).signer().Equal(Signer::EIP155(7)) && core::TxPool(c2, 0).signer().Equal(Signer::EIP155(7)),
+        "TxPool signer: EIP155(chain id) with the EIP-155 fork unset");
+  c2.eip155_block = 10;
+  check(core::TxPool(c2, 4).signer().Equal(Signer::EIP155(7)), "TxPool signer: EIP155(chain id) below the fork block");
   // isProtectedV (transaction.go:142-149)
   check(!sample_tx(0, 27)->Protected() && !sample_tx(0, 28)->Protected() && sample_tx(0, 37)->Protected() &&
             sample_tx(0, 0)->Protected(),

@@ -66,11 +66,21 @@ def test_malformed_blocks(name, raw):
 
 
 def test_counts_without_selection():
-    from eges_amd._lib import lib
+    """A sizing call (cap 0) returns EGES_E_INVALID_ARG with counts and block_status valid, on the
+    host. With nothing selected, every list still goes through the GPU decoder (rlp.DecodeBytes
+    decodes all of them): no fallback without a device."""
+    import torch
+    from eges_amd._lib import EGES_E_INVALID_ARG, EGES_E_NODEVICE, lib
     raw, _ = block(4, 3, 11)
     counts = np.zeros(3, np.uint32)
     bst = ctypes.c_int(-1)
     buf = np.frombuffer(raw, np.uint8)
+    rc = lib.eges_block_senders_raw(ctypes.c_void_p(buf.ctypes.data), len(raw), 7, 2, txs.GEEC_CHAIN_ID, 0, None, None,
+                                    ctypes.c_void_p(counts.ctypes.data), ctypes.byref(bst))
+    assert rc == EGES_E_INVALID_ARG and bst.value == 0 and counts.tolist() == [4, 3, 11]
+    if torch.cuda.is_available():
+        return
+    counts[:] = 0
     rc = lib.eges_block_senders_raw(ctypes.c_void_p(buf.ctypes.data), len(raw), 0, 2, txs.GEEC_CHAIN_ID, 0, None, None,
                                     ctypes.c_void_p(counts.ctypes.data), ctypes.byref(bst))
-    assert rc == 0 and bst.value == 0 and counts.tolist() == [4, 3, 11]
+    assert rc == EGES_E_NODEVICE and counts.tolist() == [4, 3, 11]

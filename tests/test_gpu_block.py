@@ -54,6 +54,21 @@ def test_geec_block_with_undecodable_tx(engine, oracle):
     assert np.array_equal(addr[ok], exp[ok])
 
 
+def test_undecodable_tx_in_an_unselected_list(engine, oracle):
+    """rlp.DecodeBytes(block) decodes FakeTxs and GeecTxs too: a Txs-only call (the Geec
+    validator's selection) still fails a block whose FakeTx does not decode."""
+    tx_raws, exp = signed_block(engine, 991_000, 32)
+    fake = [txs.fake_tx(data_len=100) for _ in range(5)]
+    fake[3] = T.enc_list([fake[3][2:-7]])  # not a txdata
+    geec = [txs.fake_tx(data_len=23, is_geec=True, data=b"geec udp txn %03d......." % i) for i in range(3)]
+    for f, g, bad in ((fake, geec, True), (geec, fake, True), (geec, geec, False)):
+        raw = txs.geec_extblock(f, g, tx_raws)
+        addr, st, counts, bst = engine.block_senders_raw(raw, lists=txs_mask("txs"))
+        _, _, _, obst = T.block_senders(oracle, raw, txs_mask("txs"), 2, txs.GEEC_CHAIN_ID)
+        assert bst == obst == (T.DECODE_FAILED if bad else 0)
+        assert (st == 0).all() and np.array_equal(addr, exp)  # the selected list is still recovered
+
+
 def txs_mask(name):
     from eges_amd import _lib
     return {"fake": _lib.LIST_FAKE, "geec": _lib.LIST_GEEC, "txs": _lib.LIST_TXS}[name]

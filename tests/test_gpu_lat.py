@@ -1,8 +1,7 @@
 """The latency kernels (k_recover_lat.hip: one signature per wave, recover and verify) against the
 throughput kernels and the golden fixtures. Batches up to EGES_LAT_MAX signatures take the latency kernel;
-EGES_LAT_MAX=0 forces the lane-serial kernel (capi.hip lat_max is read per call), so every
+EGES_LAT_MAX=0 (eges_test_set_knob) forces the lane-serial kernel, so every
 case runs both ways and must agree byte for byte, and with the reference-generated fixtures."""
-import os
 import time
 
 import numpy as np
@@ -14,21 +13,21 @@ pytestmark = pytest.mark.gpu
 
 
 class env_knob:
-    """Sets an engine knob (read per call by capi.hip) for the duration of a with-block."""
+    """Sets an engine knob (eges_test_set_knob; the engine reads no environment after init) for
+    the duration of a with-block."""
     name = None
 
     def __init__(self, v):
         self.v = v
 
     def __enter__(self):
-        self.old = os.environ.get(self.name)
-        os.environ[self.name] = str(self.v)
+        import eges_amd
+        self.old = eges_amd.get_knob(self.name)
+        eges_amd.set_knob(self.name, self.v)
 
     def __exit__(self, *a):
-        if self.old is None:
-            os.environ.pop(self.name, None)
-        else:
-            os.environ[self.name] = self.old
+        import eges_amd
+        eges_amd.set_knob(self.name, self.old)
 
 
 class lat_max(env_knob):  # batches up to this size take the latency kernels

@@ -153,11 +153,8 @@ def test_mutation_fuzz(engine, oracle):
         addr, st = _check(engine, oracle, mutated, signer, CHAIN)
         seen |= set(np.unique(st).tolist())
         _, _, sh = engine.sender_raw_batch(mutated, signer, CHAIN, want_sighash=True)
-        os.environ["EGES_TXROWS_WAVE_MAX"] = "0"
-        try:
+        with engine.knob("EGES_TXROWS_WAVE_MAX", 0):
             addr1, st1, sh1 = engine.sender_raw_batch(mutated, signer, CHAIN, want_sighash=True)
-        finally:
-            del os.environ["EGES_TXROWS_WAVE_MAX"]
         assert np.array_equal(st1, st) and np.array_equal(addr1, addr) and np.array_equal(sh1, sh)
     assert {0, 1, 2, T.DECODE_FAILED} <= seen, seen
 

@@ -74,3 +74,53 @@ def test_gloo_two_ranks_gather_equals_single(n):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert np.array_equal(got, _item_work(range(n)))
+
+
+def _bench(args, env_extra=None, timeout=240):
+    """bench.py as the driver runs it (no launcher: --gpus N starts torch.distributed.run itself)."""
+    import json
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.pop("WORLD_SIZE", None)
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=ROOT)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+@pytest.mark.parametrize("config", ["c2", "c4"])
+def test_bench_rank_logic_two_ranks(config):
+    """bench.py's own rank logic at world size 2 on the CPU (--stub: gloo, a timed sleep as the
+    step): --gpus 2 launches two ranks, each takes its shard (weak: its own batch; strong:
+    shard_range of the fixed total), times between barriers, the max over ranks and the
+    correctness reduce come back to rank 0, whose line names both ranks."""
+    rc, line, err = _bench(["--stub", "--gpus", "2", "--steps", "3", "--warmup", "1", "--config", config,
+                            "--batch", "1001"])
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == 2 and len(line["ranks"]) == 2
+    assert sorted(r["rank"] for r in line["ranks"]) == [0, 1]
+    sh = line["config"]["shards"]
+    if config == "c4":
+        assert sh == [list(shard_range(1001, r, 2)) for r in range(2)] and line["scaling"] == "strong"
+        assert line["config"]["total_batch"] == 1001
+    else:
+        assert sh == [[0, 1001], [1001, 2002]] and line["scaling"] == "weak"
+        assert line["config"]["total_batch"] == 2002
+    # value = all ranks' items / the max elapsed over ranks (3 steps of >= 2 ms each)
+    assert line["ms_per_step"] >= 2.0
+    assert abs(line["value"] - line["config"]["total_batch"] * 3 / (line["ms_per_step"] * 3 / 1e3)) \
+        <= 1e-3 * line["value"] + 1.0
+    assert line["config"]["correct"] is True
+
+
+def test_bench_correctness_reduce_and_world_check():
+    """one rank's mismatch fails the whole line (rc != 0, correct false on rank 0); a launcher
+    whose WORLD_SIZE differs from --gpus is refused"""
+    rc, line, _ = _bench(["--stub", "--gpus", "2", "--steps", "2", "--warmup", "0"], {"EGES_BENCH_STUB_BAD_RANK": "1"})
+    assert rc != 0 and line["config"]["correct"] is False
+    rc, line, err = _bench(["--stub", "--gpus", "2"], {"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc == 2 and line is None and "WORLD_SIZE=3" in err
