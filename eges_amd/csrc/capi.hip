@@ -123,10 +123,10 @@ struct KnobDef {
 // signatures: +3.9 % on one box), off for a single-chunk batch, whose launch then stays one
 // kernel. S >= 2 forces S parts; 0 turns it off.
 #ifndef EGES_LAT_MAX_DEFAULT
-#define EGES_LAT_MAX_DEFAULT 3584
+#define EGES_LAT_MAX_DEFAULT 1536
 #endif
 #ifndef EGES_MID_MAX_DEFAULT
-#define EGES_MID_MAX_DEFAULT 0
+#define EGES_MID_MAX_DEFAULT 40000
 #endif
 const KnobDef KNOB_DEFS[KNOB_COUNT] = {
     {"EGES_LAT_MAX", EGES_LAT_MAX_DEFAULT},
@@ -342,16 +342,32 @@ static hipError_t stamp_buf(size_t waves, hipStream_t st) {
 }
 #endif
 
+size_t dev_ws_bytes(const Dev& d) { return ws_bytes_per_block() * (size_t)d.ws_blocks; }
+// batches (or chunks) the mid-size kernel takes: above LAT_MAX, up to MID_MAX and what the
+// device workspace holds
+bool use_mid(const Dev& d, size_t n) {
+  if (n <= lat_max() || n > mid_max()) return false;
+  return (n + 63) / 64 * mid_ws_bytes_per_block() <= dev_ws_bytes(d);
+}
+// the recover kernels that parse msg / sig bytes themselves (no prep launch)
+bool fused_parse(const Dev& d, size_t n) { return n <= lat_max() || use_mid(d, n); }
+
 hipError_t launch_recover_pass(Dev& d, const RecoverParams& p0, hipStream_t st) {
   RecoverParams p = with_diag(d, p0);
   // the split form (four waves per signature) while the batch leaves SIMDs idle
   p.wide = p.n <= wide_max() ? 1u : 0u;
+  const bool mid = use_mid(d, p.n);
 #ifdef EGES_PHASE_STAMPS
+  if (mid) {
+    hipError_t e = stamp_buf((p.n + 63) / 64 * 4, st);  // one row per wave
+    return e != hipSuccess ? e : launch_recover_mid_stamped(p, dev_ws_bytes(d), st, g_stamps);
+  }
   if (p.n <= lat_max() || p.raw_sig) {
     hipError_t e = stamp_buf(lat_waves(p.n), st);
     return e != hipSuccess ? e : launch_recover_lat_stamped(p, st, g_stamps);
   }
 #endif
+  if (mid) return launch_recover_mid(p, dev_ws_bytes(d), st);
   if (p.n <= lat_max() || p.raw_sig) return launch_recover_lat(p, st);
   return launch_recover(p, d.mb_recover, d.ws_blocks, st);
 }
@@ -416,14 +432,14 @@ int run_recover_dev(Dev& d, const uint8_t* msg, const uint8_t* sig, size_t n, ui
     const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr ? addr + off * 20 : nullptr, pub ? pub + off * 65 : nullptr,
                     d.gtab, d.ws};
-    if (m <= lat_max()) {  // the latency kernel parses the bytes itself
+    if (fused_parse(d, m)) {  // the latency / mid-size kernels parse the bytes themselves
       p.raw_msg = msg + off * 32;
       p.raw_sig = sig + off * 65;
     } else {
       HIPCHK(launch_prep_ecrecover(msg + off * 32, sig + off * 65, m, (uint32_t)n_pad, rec, st));
     }
 #ifdef EGES_PHASE_STAMPS
-    if (p.n > lat_max()) {
+    if (!fused_parse(d, p.n)) {
       HIPCHK(stamp_buf((size_t)d.ws_blocks * 4 /* waves per block */, st));
       HIPCHK(launch_recover_stamped(with_diag(d, p), d.mb_recover, d.ws_blocks, st, g_stamps));
       continue;
@@ -715,7 +731,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       JOIN_IN(r);
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, j.addr ? o_addr : nullptr, j.pub ? o_pub : nullptr,
                       d.gtab, d.ws};
-      if (m <= lat_max()) {  // the latency kernel parses the bytes itself
+      if (fused_parse(d, m)) {  // the latency / mid-size kernels parse the bytes themselves
         p.raw_msg = dm;
         p.raw_sig = ds;
       } else {

@@ -268,12 +268,12 @@ DEV ge load_pt(const uint32_t* src) {
 // ------------------------------------------------------------------ Strauss step
 // acc += p when `use`; acc_inf tracks the point at infinity. Exceptional sums (acc == +-p)
 // are resolved exactly on a wave-uniform slow path.
-DEV void add_step(gej& acc, bool& inf, const ge& p, bool use, const Diag& dg) {
+DEV void add_step(gej& acc, bool& inf, const ge& p, bool use, const Diag& dg, int slot = EGES_DIAG_LS_EXC) {
   bool hz, rz;
   gej s = gej_add_ge(acc, p, hz, rz);
   const bool exc = use && !inf && hz;
   if (__any(exc)) {
-    diag_bump(dg, EGES_DIAG_LS_EXC);
+    diag_bump(dg, slot);
     gej d = gej_double(acc);
     s = gej_select(exc && rz, d, s);
   }
@@ -707,6 +707,55 @@ DEV void pub_address(uint32_t a[5], const uint32_t X[8], const uint32_t Y[8]) {
   a[2] = (uint32_t)(h[2] >> 32);
   a[3] = (uint32_t)h[3];
   a[4] = (uint32_t)(h[3] >> 32);
+}
+
+struct LatParse {
+  sc R, Sv, Z;
+  uint32_t xr[8];
+  uint32_t meta, recid;
+  bool ok;
+};
+// ------------------------------------------------------------------ record parse
+// The signature's scalars, R's x and the pre-check status (main_impl.h:38-121) from the prep
+// kernels' record rows, or (raw_sig set) from the caller's msg / sig bytes (the fused prep of
+// prep_ecrecover_kernel, k_prep.hip). Wave-uniform in the latency kernels' row-form waves, per
+// lane in the lane-serial ones (root helpers, the mid-size kernel).
+DEV LatParse lat_parse(const RecoverParams& prm, uint32_t idx) {
+  LatParse q;
+  uint32_t rl[8], sl[8], zl[8];
+  if (prm.raw_sig) {  // fused prep: prep_ecrecover_kernel's parse (k_prep.hip), same record
+    const uint8_t* sg = prm.raw_sig + (size_t)idx * 65;
+    limbs_from_be32(zl, prm.raw_msg + (size_t)idx * 32);
+    limbs_from_be32(rl, sg);
+    limbs_from_be32(sl, sg + 32);
+    const uint32_t v = sg[64];
+    q.meta = v >= 4 ? (ST_INVALID_RECOVERY_ID << 8) : v;  // checkSignature, secp256.go:171-179
+  } else {
+    rec_get(prm, 8, idx, rl);
+    rec_get(prm, 16, idx, sl);
+    rec_get(prm, 0, idx, zl);
+    q.meta = prm.rec[(size_t)24 * prm.n_pad + idx];
+  }
+  q.recid = q.meta & 3u;
+  q.ok = ((q.meta >> 8) & 0xffu) == ST_OK;
+  bool ovr, ovs, ovz;
+  q.R = sc_from_limbs(rl, ovr);
+  q.Sv = sc_from_limbs(sl, ovs);
+  q.Z = sc_from_limbs(zl, ovz);  // msg mod n (main_impl.h:183)
+  q.ok = q.ok && !ovr && !ovs && !sc_is_zero(q.R) && !sc_is_zero(q.Sv);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q.xr[i] = q.R.v[i];
+  if (q.recid & 2u) {  // x = r + n, only when r < p - n (main_impl.h:101-109)
+    q.ok = q.ok && !u256_ge(q.R.v, P_MINUS_N);
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      c += (uint64_t)q.xr[i] + SC_N[i];
+      q.xr[i] = (uint32_t)c;
+      c >>= 32;
+    }
+  }
+  return q;
 }
 
 }  // namespace eges

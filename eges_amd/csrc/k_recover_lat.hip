@@ -492,52 +492,6 @@ DEV uint32_t* root_area(const RecoverParams& prm) {
   return const_cast<uint32_t*>(prm.rec) + (size_t)REC_ROWS * prm.n_pad;
 }
 
-struct LatParse {
-  sc R, Sv, Z;
-  uint32_t xr[8];
-  uint32_t meta, recid;
-  bool ok;
-};
-// the signature's scalars, R's x and the pre-check status (main_impl.h:38-121); wave-uniform in
-// the row-form waves, per lane in the helpers
-DEV LatParse lat_parse(const RecoverParams& prm, uint32_t idx) {
-  LatParse q;
-  uint32_t rl[8], sl[8], zl[8];
-  if (prm.raw_sig) {  // fused prep: prep_ecrecover_kernel's parse (k_prep.hip), same record
-    const uint8_t* sg = prm.raw_sig + (size_t)idx * 65;
-    limbs_from_be32(zl, prm.raw_msg + (size_t)idx * 32);
-    limbs_from_be32(rl, sg);
-    limbs_from_be32(sl, sg + 32);
-    const uint32_t v = sg[64];
-    q.meta = v >= 4 ? (ST_INVALID_RECOVERY_ID << 8) : v;  // checkSignature, secp256.go:171-179
-  } else {
-    rec_get(prm, 8, idx, rl);
-    rec_get(prm, 16, idx, sl);
-    rec_get(prm, 0, idx, zl);
-    q.meta = prm.rec[(size_t)24 * prm.n_pad + idx];
-  }
-  q.recid = q.meta & 3u;
-  q.ok = ((q.meta >> 8) & 0xffu) == ST_OK;
-  bool ovr, ovs, ovz;
-  q.R = sc_from_limbs(rl, ovr);
-  q.Sv = sc_from_limbs(sl, ovs);
-  q.Z = sc_from_limbs(zl, ovz);  // msg mod n (main_impl.h:183)
-  q.ok = q.ok && !ovr && !ovs && !sc_is_zero(q.R) && !sc_is_zero(q.Sv);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) q.xr[i] = q.R.v[i];
-  if (q.recid & 2u) {  // x = r + n, only when r < p - n (main_impl.h:101-109)
-    q.ok = q.ok && !u256_ge(q.R.v, P_MINUS_N);
-    uint64_t c = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      c += (uint64_t)q.xr[i] + SC_N[i];
-      q.xr[i] = (uint32_t)c;
-      c >>= 32;
-    }
-  }
-  return q;
-}
-
 DEV void root_helper(const RecoverParams& prm) {
   const uint32_t j = blockIdx.x * ROOT_WG + threadIdx.x;
   if (j >= prm.n) return;

@@ -100,6 +100,7 @@ hipError_t launch_tx_rows(const uint8_t* raw, const uint64_t* offsets, uint64_t 
 #ifdef EGES_PHASE_STAMPS
 hipError_t launch_recover_stamped(const RecoverParams& p, int max_blocks, int ws_blocks, hipStream_t st, uint64_t* stamps);
 hipError_t launch_recover_lat_stamped(const RecoverParams& p, hipStream_t st, uint64_t* stamps);
+hipError_t launch_recover_mid_stamped(const RecoverParams& p, size_t ws_bytes, hipStream_t st, uint64_t* stamps);
 size_t lat_waves(uint32_t n);
 #endif
 // max_blocks: the resident grid; ws_blocks: blocks the workspace p.ws was allocated for. A
@@ -108,6 +109,10 @@ hipError_t launch_recover(const RecoverParams& p, int max_blocks, int ws_blocks,
 // Small batches: one signature per 16-lane row, limb-parallel field arithmetic (k_recover_lat.hip).
 // Same inputs (prep records) and outputs as launch_recover; no workspace.
 hipError_t launch_recover_lat(const RecoverParams& p, hipStream_t st);
+// Mid-size batches: 64 signatures per 4-wave workgroup, one role per wave (k_recover_mid.hip).
+// Uses p.ws (ceil(n / 64) blocks of mid_ws_bytes_per_block(), refused beyond ws_bytes).
+hipError_t launch_recover_mid(const RecoverParams& p, size_t ws_bytes, hipStream_t st);
+size_t mid_ws_bytes_per_block();
 hipError_t launch_verify(const VerifyParams& p, int max_blocks, int ws_blocks, hipStream_t st);
 // one item per 128-thread workgroup (k_recover_lat.hip; wide: 192 threads, three partial sums);
 // uses pub/publen/msg/sig/n/ok/gtab only

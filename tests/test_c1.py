@@ -66,13 +66,25 @@ def test_c1_senders_gpu(engine):
     from eges_amd._lib import SIGNER_EIP155
     ref = _ref()
     h, sig, addr = _c1_signed(ref, N_GPU)
-    a1, st1, sh = engine.sender_raw_batch(txs.c1_raw(0, sig), SIGNER_EIP155, txs.GEEC_CHAIN_ID, want_sighash=True)
-    assert (st1 == 0).all(), np.nonzero(st1)[0][:10]
-    assert np.array_equal(sh, h)
-    assert np.array_equal(a1, addr)
     r, s, v = txs.sender_rows(sig)
-    a2, st2 = engine.sender_batch(h, r, s, v, None, SIGNER_EIP155, txs.GEEC_CHAIN_ID)
-    assert (st2 == 0).all() and np.array_equal(a2, addr)
+    # every recover form that can take the batch: the engine's default dispatch, the mid-size
+    # kernel, the lane-serial kernel (knobs, eges_test_set_knob)
+    forms = [{}, {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20}, {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 0}]
+    for kv in forms:
+        old = {k: engine.get_knob(k) for k in kv}
+        try:
+            for k, x in kv.items():
+                engine.set_knob(k, x)
+            a1, st1, sh = engine.sender_raw_batch(txs.c1_raw(0, sig), SIGNER_EIP155, txs.GEEC_CHAIN_ID,
+                                                  want_sighash=True)
+            assert (st1 == 0).all(), (kv, np.nonzero(st1)[0][:10])
+            assert np.array_equal(sh, h)
+            assert np.array_equal(a1, addr), kv
+            a2, st2 = engine.sender_batch(h, r, s, v, None, SIGNER_EIP155, txs.GEEC_CHAIN_ID)
+            assert (st2 == 0).all() and np.array_equal(a2, addr), kv
+        finally:
+            for k, x in old.items():
+                engine.set_knob(k, x)
     # the GPU synthetic signer (bench.py --config c1) uses the same keys
     sig_d, exp_d = engine.synth_sign_msg_dev(torch.from_numpy(h[:512]).cuda(), 0)
     torch.cuda.synchronize()

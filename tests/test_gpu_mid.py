@@ -1,0 +1,134 @@
+"""The mid-size recover kernel (k_recover_mid.hip: 64 signatures per 4-wave workgroup, one role
+per wave) against the fixtures, the oracle and the other two recover forms.
+
+Forms are selected with engine knobs (eges_test_set_knob): EGES_LAT_MAX = 0 and EGES_MID_MAX
+large send every batch through the mid-size kernel; EGES_MID_MAX = 0 through the lane-serial
+kernel. Every output byte must agree across forms and with the reference-generated fixtures."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+MID = {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20}
+LANE = {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 0}
+
+
+class knobs:
+    def __init__(self, engine, kv):
+        self.engine, self.kv = engine, kv
+
+    def __enter__(self):
+        self.old = {k: self.engine.get_knob(k) for k in self.kv}
+        for k, v in self.kv.items():
+            self.engine.set_knob(k, v)
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            self.engine.set_knob(k, v)
+
+
+def test_mid_golden_recover_and_sender(engine):
+    """every golden recovery item (all reject classes) and every golden sender item through the
+    mid-size kernel: byte for byte the fixtures (reference libsecp256k1, oracle/_ref)"""
+    g = load_golden("recover.npz")
+    with knobs(engine, MID):
+        pub, addr, st = engine.ecrecover_batch(g["msg"], g["sig"])
+    names = list(g["kind_names"])
+    bad = np.nonzero(st != g["status"])[0]
+    assert bad.size == 0, [(int(i), names[g["kind"][i]], int(st[i]), int(g["status"][i])) for i in bad[:20]]
+    assert np.array_equal(pub, g["pub"])
+    with knobs(engine, LANE):
+        pub2, addr2, st2 = engine.ecrecover_batch(g["msg"], g["sig"])
+    assert np.array_equal(addr, addr2) and np.array_equal(st, st2)
+    g2 = load_golden("sender.npz")
+    for signer, cid in sorted(set(zip(g2["signer"].tolist(), g2["chain_id"].tolist()))):
+        sel = np.nonzero((g2["signer"] == signer) & (g2["chain_id"] == cid))[0]
+        with knobs(engine, MID):
+            a, s_ = engine.sender_batch(g2["sighash"][sel], g2["r"][sel], g2["s"][sel], g2["v"][sel],
+                                        g2["vflags"][sel], int(signer), int(cid))
+        assert np.array_equal(s_, g2["status"][sel]), (signer, cid)
+        assert np.array_equal(a, g2["addr"][sel]), (signer, cid)
+
+
+def test_mid_golden_tiled_ragged(engine):
+    """the golden recovery set tiled to 10,007 items (ragged last workgroup), device-resident
+    entry, mid-size kernel vs the fixtures item for item"""
+    import torch
+    g = load_golden("recover.npz")
+    n = 10007
+    rep = -(-n // len(g["msg"]))
+    msg = np.tile(g["msg"], (rep, 1))[:n]
+    sig = np.tile(g["sig"], (rep, 1))[:n]
+    with knobs(engine, MID):
+        pub, addr, st = engine.ecrecover_batch_dev(torch.from_numpy(msg).cuda(), torch.from_numpy(sig).cuda(),
+                                                   pub=torch.empty((n, 65), dtype=torch.uint8, device="cuda"))
+        torch.cuda.synchronize()
+    st, pub = st.cpu().numpy(), pub.cpu().numpy()
+    assert np.array_equal(st, np.tile(g["status"], rep)[:n])
+    assert np.array_equal(pub, np.tile(g["pub"], (rep, 1))[:n])
+
+
+@pytest.mark.parametrize("n", [10000, 50000])
+def test_mid_adversarial_mix(engine, oracle, n):
+    """configs[4]'s mix at 10k and 50k through the mid-size kernel: statuses bit-exact against
+    their expectation and equal to the lane-serial kernel's, addresses of accepted items the
+    signers', a sample of every class against the oracle"""
+    import torch
+    from eges_amd import txs, workloads
+    from eges_amd._lib import SIGNER_EIP155
+    msg, sig, exp = engine.synth_sign_dev(300_000 + n, n, 0)
+    torch.cuda.synchronize()
+    sig_h, msg_h, exp_h = sig.cpu().numpy(), msg.cpu().numpy(), exp.cpu().numpy()
+    kind = workloads.adversarial_mix(sig_h, frac=0.10, seed=n)
+    r, s, v = workloads.sender_rows_mixed(sig_h, kind, txs.GEEC_CHAIN_ID)
+    sig_m = torch.from_numpy(sig_h).cuda()
+    rows = [torch.from_numpy(x).cuda() for x in (r, s, v)]
+    vf = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    out = {}
+    for name, kv in (("mid", MID), ("lane", LANE)):
+        with knobs(engine, kv):
+            pub, addr, st = engine.ecrecover_batch_dev(msg, sig_m, pub=torch.empty((n, 65), dtype=torch.uint8,
+                                                                                    device="cuda"))
+            a2, st2 = engine.sender_batch_dev(msg, *rows, vf, SIGNER_EIP155, txs.GEEC_CHAIN_ID)
+            torch.cuda.synchronize()
+        out[name] = [x.cpu().numpy() for x in (pub, addr, st, a2, st2)]
+    pub, addr, st, a2, st2 = out["mid"]
+    for x, y in zip(out["mid"], out["lane"]):
+        assert np.array_equal(x, y)
+    assert np.array_equal(st, workloads.expected_status(kind, "ecrecover"))
+    assert np.array_equal(st2, workloads.expected_status(kind, "sender"))
+    assert np.array_equal(addr[st == 0], exp_h[st == 0]) and not addr[st != 0].any()
+    assert np.array_equal(a2[st2 == 0], exp_h[st2 == 0]) and not a2[st2 != 0].any()
+    for k in range(len(workloads.KIND_NAMES)):
+        for i in np.nonzero(kind == k)[0][:6]:
+            ost, opub = oracle.recover_pubkey(msg_h[i].tobytes(), sig_h[i].tobytes())
+            assert ost == st[i] and (ost != 0 or opub == pub[i].tobytes())
+
+
+def test_mid_exceptional_joins(engine, oracle):
+    """the split-form constructions (tests/ecmodel.py) meet the mid-size kernel's joins: both the
+    doubling and the infinity branch run, results equal the oracle's; forced redo of its loops
+    and comb leaves the golden outputs unchanged"""
+    import random
+
+    import ecmodel as M
+    cases = [c for c in M.recover_cases(random.Random(21), 8) if c[0] in ("split1", "split2")]
+    msg = np.frombuffer(b"".join(M.recover_input(c[2], c[3], c[4], c[5])[0] for c in cases), np.uint8).reshape(-1, 32)
+    sig = np.frombuffer(b"".join(M.recover_input(c[2], c[3], c[4], c[5])[1] for c in cases), np.uint8).reshape(-1, 65)
+    engine.diag_counters(reset=True)
+    with knobs(engine, MID):
+        pub, addr, st = engine.ecrecover_batch(msg, sig)
+    d = engine.diag_counters(reset=True)
+    assert d["mid_join"] > 0 and d["mid_redo"] == 0 and d["mid_exc"] == 0, d
+    for i in range(len(msg)):
+        ost, opub = oracle.recover_pubkey(msg[i].tobytes(), sig[i].tobytes())
+        assert ost == st[i] and (ost != 0 or opub == pub[i].tobytes()), i
+    assert (st == 6).any() and (st == 0).any()
+    g = load_golden("recover.npz")
+    with knobs(engine, dict(MID, EGES_TEST_FORCE_REDO=1)):
+        pub, addr, st = engine.ecrecover_batch(g["msg"], g["sig"])
+    d = engine.diag_counters(reset=True)
+    assert np.array_equal(st, g["status"]) and np.array_equal(pub, g["pub"])
+    assert d["mid_redo"] > 0, d
