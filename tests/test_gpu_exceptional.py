@@ -26,9 +26,10 @@ pytestmark = pytest.mark.gpu
 
 LAT_ALL = 1 << 20
 FORMS = {  # knob settings per form (recovery / verification)
-    "lane_serial": {"EGES_LAT_MAX": 0},
+    "lane_serial": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 0},
     "narrow": {"EGES_LAT_MAX": LAT_ALL, "EGES_LAT_WIDE_MAX": 0},
     "split": {"EGES_LAT_MAX": LAT_ALL, "EGES_LAT_WIDE_MAX": LAT_ALL},
+    "mid": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": LAT_ALL},
 }
 
 
@@ -97,6 +98,9 @@ def test_recover_exceptional_sums_every_form(engine, oracle):
         if form == "lane_serial":
             # window 0: the u1 G addition meets u2 R == +-u1 G, the wave redoes its loop exactly
             assert d["ls_redo"] > 0 and d["ls_exc"] > 0, d
+        elif form == "mid":
+            # the split constructions meet the mid-size kernel's joins ((A + u1 G) + H, as split)
+            assert d["mid_join"] > 0 and d["mid_redo"] == 0 and d["mid_exc"] == 0, d
         else:
             assert d["join_dbl"] > 0 and d["join_inf"] > 0, (form, d)
             assert d["lat_redo"] == 0 and d["comb_redo"] == 0 and d["lat_exc"] == 0, (form, d)
@@ -120,18 +124,22 @@ def test_recover_exceptional_sums_reference_lib(engine):
 
 
 def test_precompile_and_single_item_exceptional(engine, oracle):
-    """The attacker-facing entries: the EVM ECRECOVER precompile (both latency forms) and the
+    """The attacker-facing entries: the EVM ECRECOVER precompile (both latency forms and the
+    mid-size kernel) and the
     coalesced single-item secp256k1_ext_ecdsa_recover replacement."""
     from eges_amd._lib import lib
     cases, msg, sig = _recover_inputs(seed=12)
     est, epub = _expected_recover(oracle, msg, sig)
     inputs = [msg[i].tobytes() + bytes(31) + bytes([27 + sig[i, 64]]) + sig[i, :64].tobytes() for i in range(len(msg))]
-    for form in ("narrow", "split"):
+    for form in ("narrow", "split", "mid"):
         engine.diag_counters(reset=True)
         with knobs(engine, FORMS[form]):
             out, st = engine.ecrecover_precompile_batch(inputs)
         d = engine.diag_counters(reset=True)
-        assert d["join_dbl"] > 0 and d["join_inf"] > 0, (form, d)
+        if form == "mid":
+            assert d["mid_join"] > 0, d
+        else:
+            assert d["join_dbl"] > 0 and d["join_inf"] > 0, (form, d)
         for i in range(len(msg)):
             if est[i] == 0:
                 assert st[i] == 0 and out[i].tobytes() == bytes(12) + oracle.pub_to_addr(epub[i].tobytes()), (form, i)
@@ -170,6 +178,8 @@ def test_verify_exceptional_sums_every_form(engine, oracle):
         assert np.array_equal(ok, exp), (form, np.nonzero(ok != exp)[0])
         if form == "lane_serial":
             assert d["ls_redo"] > 0 and d["ls_exc"] > 0, d
+        elif form == "mid":  # (verification has no mid-size form: the lane-serial kernel runs)
+            assert d["ls_redo"] > 0 and d["ls_exc"] > 0, d
         else:
             assert d["join_dbl"] > 0 and d["join_inf"] > 0, (form, d)
     for i in range(n):
@@ -192,5 +202,7 @@ def test_forced_redo_every_form_golden(engine):
         assert np.array_equal(ok, gv["ok"]), form
         if form == "lane_serial":
             assert d["ls_redo"] > 0, d
+        elif form == "mid":
+            assert d["mid_redo"] > 0 and d["ls_redo"] > 0, d  # recovery: mid-size; verification: lane-serial
         else:
             assert d["lat_redo"] > 0 and d["comb_redo"] > 0, (form, d)

@@ -13,29 +13,43 @@ pytestmark = pytest.mark.gpu
 
 
 class env_knob:
-    """Sets an engine knob (eges_test_set_knob; the engine reads no environment after init) for
+    """Sets engine knobs (eges_test_set_knob; the engine reads no environment after init) for
     the duration of a with-block."""
-    name = None
 
     def __init__(self, v):
-        self.v = v
+        self.kv = self.knobs(v)
 
     def __enter__(self):
         import eges_amd
-        self.old = eges_amd.get_knob(self.name)
-        eges_amd.set_knob(self.name, self.v)
+        self.old = {k: eges_amd.get_knob(k) for k in self.kv}
+        for k, v in self.kv.items():
+            eges_amd.set_knob(k, v)
 
     def __exit__(self, *a):
         import eges_amd
-        eges_amd.set_knob(self.name, self.old)
+        for k, v in self.old.items():
+            eges_amd.set_knob(k, v)
 
 
-class lat_max(env_knob):  # batches up to this size take the latency kernels
-    name = "EGES_LAT_MAX"
+class lat_max(env_knob):
+    """batches up to v take the latency kernels; lat_max(0) forces the lane-serial kernel (the
+    mid-size kernel, k_recover_mid.hip, is switched off too; tests/test_gpu_mid.py covers it)"""
+
+    @staticmethod
+    def knobs(v):
+        return {"EGES_LAT_MAX": v} if v else {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 0}
 
 
 class wide_max(env_knob):  # latency batches up to this size use the split (4-wave) form
-    name = "EGES_LAT_WIDE_MAX"
+    @staticmethod
+    def knobs(v):
+        return {"EGES_LAT_WIDE_MAX": v}
+
+
+class root_helpers(env_knob):  # 0: the narrow form launches no root-helper workgroups
+    @staticmethod
+    def knobs(v):
+        return {"EGES_TEST_ROOT_HELPERS": v}
 
 
 def test_wide_kernel_golden_recover(engine):
@@ -74,8 +88,6 @@ def test_lat_kernel_golden_recover(engine):
     assert np.array_equal(addr, addr2) and np.array_equal(st, st2)
 
 
-class root_helpers(env_knob):  # 0: the narrow form launches no root-helper workgroups
-    name = "EGES_TEST_ROOT_HELPERS"
 
 
 def test_narrow_root_fetch_fallback_golden(engine):
