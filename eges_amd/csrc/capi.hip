@@ -132,6 +132,8 @@ const KnobDef KNOB_DEFS[KNOB_COUNT] = {
     {"EGES_LAT_MAX", EGES_LAT_MAX_DEFAULT},
     {"EGES_LAT_WIDE_MAX", 256},
     {"EGES_MID_MAX", EGES_MID_MAX_DEFAULT},
+    {"EGES_MID_FORM", 1},
+    {"EGES_WIRE_FUSED", 1},
     {"EGES_TXROWS_WAVE_MAX", 8192},
     {"EGES_TEST_ROOT_HELPERS", 1},
     {"EGES_OVERLAP", -1},
@@ -345,9 +347,18 @@ static hipError_t stamp_buf(size_t waves, hipStream_t st) {
 size_t dev_ws_bytes(const Dev& d) { return ws_bytes_per_block() * (size_t)d.ws_blocks; }
 // batches (or chunks) the mid-size kernel takes: above LAT_MAX, up to MID_MAX and what the
 // device workspace holds
+// The bucket form (k_recover_mid.hip) holds 138 KB of LDS: one workgroup per CU. It is the
+// faster form while the grid fits one generation (n <= 64 x CUs); beyond that the windowed form
+// (two workgroups per CU) is (tools/formcurve.py).
+bool mid_bucket(const Dev& d, size_t n) {
+  const long long f = knob(KNOB_MID_FORM);
+  if (f == 0) return false;
+  if (f >= 2) return true;
+  return (n + MID_SIGS_PER_BLOCK - 1) / MID_SIGS_PER_BLOCK <= (size_t)d.cus;
+}
 bool use_mid(const Dev& d, size_t n) {
   if (n <= lat_max() || n > mid_max()) return false;
-  return (n + 63) / 64 * mid_ws_bytes_per_block() <= dev_ws_bytes(d);
+  return mid_bucket(d, n) || (n + 63) / 64 * mid_ws_bytes_per_block() <= dev_ws_bytes(d);
 }
 // the recover kernels that parse msg / sig bytes themselves (no prep launch)
 bool fused_parse(const Dev& d, size_t n) { return n <= lat_max() || use_mid(d, n); }
@@ -357,17 +368,18 @@ hipError_t launch_recover_pass(Dev& d, const RecoverParams& p0, hipStream_t st) 
   // the split form (four waves per signature) while the batch leaves SIMDs idle
   p.wide = p.n <= wide_max() ? 1u : 0u;
   const bool mid = use_mid(d, p.n);
+  if (p.wire_raw && !(mid && mid_bucket(d, p.n))) return hipErrorInvalidValue;  // wire_fused() decides
 #ifdef EGES_PHASE_STAMPS
   if (mid) {
     hipError_t e = stamp_buf((p.n + 63) / 64 * 4, st);  // one row per wave
-    return e != hipSuccess ? e : launch_recover_mid_stamped(p, dev_ws_bytes(d), st, g_stamps);
+    return e != hipSuccess ? e : launch_recover_mid_stamped(p, mid_bucket(d, p.n), dev_ws_bytes(d), st, g_stamps);
   }
   if (p.n <= lat_max() || p.raw_sig) {
     hipError_t e = stamp_buf(lat_waves(p.n), st);
     return e != hipSuccess ? e : launch_recover_lat_stamped(p, st, g_stamps);
   }
 #endif
-  if (mid) return launch_recover_mid(p, dev_ws_bytes(d), st);
+  if (mid) return launch_recover_mid(p, mid_bucket(d, p.n), dev_ws_bytes(d), st);
   if (p.n <= lat_max() || p.raw_sig) return launch_recover_lat(p, st);
   return launch_recover(p, d.mb_recover, d.ws_blocks, st);
 }
@@ -472,6 +484,12 @@ int run_sender_dev(Dev& d, const uint8_t* sighash, const uint8_t* r, const uint8
 // Wire-format transactions: tx_rows_kernel (decode + sighash) writes the sender rows into device
 // scratch after the recovery records; then the sender pipeline runs unchanged.
 inline size_t tx_rows_bytes(size_t m) { return align_up(m * (4 * 32 + 1), 256); }
+// Batches the bucket form takes run their wire-format decode, sighash and Sender checks inside
+// the recovery kernel (RecoverParams::wire_*): no tx_rows / prep_sender launches and no rows in
+// between (EGES_WIRE_FUSED = 0 turns it off for A/B).
+bool wire_fused(const Dev& d, size_t m, const uint8_t* raw) {
+  return knob(KNOB_WIRE_FUSED) != 0 && use_mid(d, m) && mid_bucket(d, m) && ((uintptr_t)raw & 3u) == 0;
+}
 
 int run_sender_raw_dev(Dev& d, const uint8_t* raw, const uint64_t* offsets, size_t n, int signer, uint64_t chain_id,
                        uint8_t* addr, uint8_t* status, uint8_t* sighash_out, hipStream_t st) {
@@ -490,9 +508,18 @@ int run_sender_raw_dev(Dev& d, const uint8_t* raw, const uint64_t* offsets, size
     uint8_t* sr = rr + (size_t)m * 32;
     uint8_t* vr = sr + (size_t)m * 32;
     uint8_t* vf = vr + (size_t)m * 32;
-    HIPCHK(launch_tx_rows(raw, offsets, off, m, signer, chain_id, hs, rr, sr, vr, vf, st));
-    HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, m, (uint32_t)n_pad, signer, chain_id, rec, st));
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr + off * 20, nullptr, d.gtab, d.ws};
+    if (wire_fused(d, m, raw)) {
+      p.wire_raw = raw;
+      p.wire_off = offsets;
+      p.wire_first = off;
+      p.wire_signer = signer;
+      p.wire_chain_id = chain_id;
+      p.wire_sighash = sighash_out ? hs : nullptr;
+    } else {
+      HIPCHK(launch_tx_rows(raw, offsets, off, m, signer, chain_id, hs, rr, sr, vr, vf, st));
+      HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, m, (uint32_t)n_pad, signer, chain_id, rec, st));
+    }
     HIPCHK(launch_recover_pass(d, p, st));
   }
   return EGES_SUCCESS;
@@ -782,9 +809,17 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       if (j.decode_only) {  // the decoder's flags straight into the status bytes
         HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, o_st, st));
       } else {
-        HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, vf, st));
-        HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, st));
         RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
+        if (wire_fused(d, m, draw)) {
+          p.wire_raw = draw;
+          p.wire_off = doff;
+          p.wire_signer = j.signer;
+          p.wire_chain_id = j.chain_id;
+          p.wire_sighash = j.sighash ? hs : nullptr;
+        } else {
+          HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, vf, st));
+          HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, st));
+        }
         HIPCHK(launch_recover_pass(d, p, st));
       }
     } else {

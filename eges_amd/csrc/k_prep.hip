@@ -1,5 +1,6 @@
 // Table-initialisation and record-preparation kernels (gfx950).
 #include "core.cuh"
+#include "sender.cuh"
 
 namespace eges {
 
@@ -82,17 +83,7 @@ __global__ void __launch_bounds__(256) prep_ecrecover_kernel(const uint8_t* __re
   rec[(size_t)24 * n_pad + i] = meta;
 }
 
-DEV int bitlen_limbs(const uint32_t x[8]) {
-  int bl = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-    if (x[i]) bl = 32 * i + (32 - __clz(x[i]));
-  return bl;
-}
-
-// types.Sender classification (transaction_signing.go:127-137,182-184,218-247, crypto.go:181-192,
-// transaction.go:142-149, deriveChainId :250-260). Items that fail before the C call get their
-// Go error as status; the rest become ecrecover records with recid = v.
+// types.Sender classification (sender.cuh sender_meta) of the sender rows.
 __global__ void __launch_bounds__(256) prep_sender_kernel(const uint8_t* __restrict__ sighash,
                                                           const uint8_t* __restrict__ rb,
                                                           const uint8_t* __restrict__ sb,
@@ -107,89 +98,14 @@ __global__ void __launch_bounds__(256) prep_sender_kernel(const uint8_t* __restr
   limbs_from_be32(r, rb + (size_t)i * 32);
   limbs_from_be32(s, sb + (size_t)i * 32);
   limbs_from_be32(v, vb + (size_t)i * 32);
-  const uint32_t f = vflags ? vflags[i] : 0u;
-  const bool v_wide = f & 1u, r_wide = f & 2u, s_wide = f & 4u;
-  // wire-format batches (k_txhash.hip): rlp.DecodeBytes failed, the tx never reaches Sender
-  uint32_t status = (f & VF_DECODE_ERR) ? ST_DECODE_FAILED : ST_OK;
-  bool homestead = signer != 0;
-  // Vb: the V handed to recoverPlain
-  uint32_t vb8[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) vb8[k] = v[k];
-  bool vb_wide = v_wide;
-  if (signer == 2 && status == ST_OK) {
-    const int bl = v_wide ? 1000 : bitlen_limbs(v);
-    const bool prot = bl <= 8 ? !(v[0] == 27u || v[0] == 28u) : true;
-    if (prot) {
-      bool match;
-      if (bl <= 64) {
-        const uint64_t vv = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
-        const uint64_t cid = (vv == 27 || vv == 28) ? 0 : (vv - 35) / 2;  // uint64 wrap as Go
-        match = cid == chain_id;
-      } else if (v_wide) {
-        match = false;
-      } else {
-        // (V - 35) >> 1 == chain_id, V >= 2^64 so no underflow
-        uint32_t t[8];
-        uint64_t br = 35;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint64_t d = (uint64_t)v[k] - br;
-          t[k] = (uint32_t)d;
-          br = (d >> 63) & 1;
-        }
-        bool hi0 = (t[2] >> 1) == 0;
-#pragma unroll
-        for (int k = 3; k < 8; ++k) hi0 = hi0 && t[k] == 0;
-        const uint64_t sh = ((uint64_t)t[0] >> 1) | ((uint64_t)t[1] << 31) | ((uint64_t)(t[2] & 1u) << 63);
-        match = hi0 && sh == chain_id;
-      }
-      if (!match) {
-        status = ST_INVALID_CHAIN_ID;
-      } else {
-        // V' = V - 2*chainId - 8 (big.Int, no wrap)
-        const uint64_t lo = chain_id * 2 + 8;
-        const uint32_t hi = (uint32_t)((chain_id >> 63) & 1u) + (uint32_t)(chain_id * 2 + 8 < 8 ? 1 : 0);
-        uint32_t sub[8] = {(uint32_t)lo, (uint32_t)(lo >> 32), hi, 0, 0, 0, 0, 0};
-        uint64_t br = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint64_t d = (uint64_t)v[k] - sub[k] - br;
-          vb8[k] = (uint32_t)d;
-          br = (d >> 63) & 1;
-        }
-        vb_wide = false;
-      }
-    }
-    homestead = true;
-  }
-  uint32_t recid = 0;
-  if (status == ST_OK) {
-    // recoverPlain :223-229
-    if (vb_wide || bitlen_limbs(vb8) > 8) {
-      status = ST_INVALID_SIG;
-    } else {
-      const uint32_t vv = (vb8[0] - 27u) & 0xffu;
-      // ValidateSignatureValues (crypto.go:181-192)
-      bool r_zero = true, s_zero = true;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) { r_zero = r_zero && r[k] == 0; s_zero = s_zero && s[k] == 0; }
-      const bool r_lt_1 = !r_wide && r_zero, s_lt_1 = !s_wide && s_zero;
-      const bool s_high = s_wide || !u256_ge(SC_HALF, s);
-      const bool r_ge_n = r_wide || u256_ge(r, SC_N), s_ge_n = s_wide || u256_ge(s, SC_N);
-      if (r_lt_1 || s_lt_1 || (homestead && s_high) || r_ge_n || s_ge_n || !(vv == 0 || vv == 1))
-        status = ST_INVALID_SIG;
-      else
-        recid = vv;
-    }
-  }
+  const uint32_t meta = sender_meta(r, s, v, vflags ? vflags[i] : 0u, signer, chain_id);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     rec[(size_t)k * n_pad + i] = z[k];
     rec[(size_t)(8 + k) * n_pad + i] = r[k];
     rec[(size_t)(16 + k) * n_pad + i] = s[k];
   }
-  rec[(size_t)24 * n_pad + i] = recid | (status << 8);
+  rec[(size_t)24 * n_pad + i] = meta;
 }
 
 // EVM ECRECOVER precompile (core/vm/contracts.go:77-101): input (hash, v, r, s), each 32 bytes,

@@ -26,6 +26,8 @@
 #include <type_traits>
 
 #include "core.cuh"
+#include "rlp.cuh"
+#include "sender.cuh"
 
 namespace eges {
 
@@ -437,6 +439,445 @@ DEV void recover_mid_body(const RecoverParams& prm, uint64_t* stamps) {
   stamp_out();
 }
 
+// ================================================================== bucket form
+// The same 64 signatures per 4-wave workgroup, with u2 R computed bottom-up so the doubling
+// chain carries no additions and needs no table:
+//
+//   wave 0 "X"   P_0 = R' (affine on E'), P_{3k} = 2^(3k) R' by 126 doublings; publishes
+//                every third point into an LDS ring (BK_RING slots, flow-controlled by the
+//                consumers' counters)
+//   wave 2 "Y1"  for every published P_{3k}: bucket[|d1_k|] += sign(d1_k) P_{3k}, d1 the signed
+//                3-bit digits of the R half; then Q1 = sum_v v bucket[v] (running sums, exact
+//                joins), Q = Q1 + Q2 (E'), Q *= y (E), Q += u1 G, Z^-1, affine, address, stores
+//   wave 3 "Y2"  the same for the lambda R half: buckets of d2_k P_{3k}, then Q2 = lambda (sum)
+//                by (X, Y, Z) -> (beta X, Y, Z) once, and hands Q2 to Y1
+//   wave 1 "S"   r^-1, u1, u2, GLV split, the digits; R's y; u1 G by the comb
+//
+// The critical path is X's 126 doublings plus Y1's tail (bucket sums, two joins, Z^-1, Keccak);
+// the windowed form's chain (D = 2^75 R', its table, 14 windows with their additions, then the
+// same tail) was ~20 % longer.
+//
+// Exceptional sums. A bucket of half h collects +-2^(3j) R'_h over distinct j in increasing
+// order: before window k its value is m R'_h with 0 < |m| <= sum_{j<k} 2^(3j) < 2^(3k), so
+// m == +-2^(3k) (mod n) is impossible (|m|, 2^(3k) < n / 2) and the unchecked general
+// additions never meet a == +-b (tests/ecmodel.py `bucket`, tests/test_exceptional_model.py).
+// The bucket sum Q_h = (B1 + B3) + 2 ((B2 + B3) + 2 B4) cannot meet them either: every join
+// adds signed-binary integers whose +-1 digits sit at distinct bit positions (3j, 3j + 1,
+// 3j + 2 for the windows j of each bucket), so a == +-b only when both are empty. Q_1 + Q_2
+// would need k1 == lambda k2 for the split's own output (never, test_exceptional_model.py);
+// the final join with u1 G is reachable (u1 chosen against u2 R). All joins are exact
+// additions (join_mid) anyway. A lane that ends with Z == 0 although it is valid would
+// contradict the argument: it is counted (EGES_DIAG_MID_EXC; the tests require 0).
+constexpr int BK_BITS = 3;
+// |k1|, |k2| < 0.64 * 2^128 for the Babai-rounded split (sc.cuh glv_split; the bound is
+// (|a1| + |a2|) / 2 and (|b1| + a1) / 2 over the lattice basis, tests/test_exceptional_model.py):
+// 128 bits + the recoding carry, 43 windows, 126 doublings
+constexpr int BK_WIN = (129 + BK_BITS - 1) / BK_BITS;
+constexpr int BK_NB = 1 << (BK_BITS - 1);             // buckets for |digit| = 1..4
+#ifndef EGES_BK_RING
+#define EGES_BK_RING 10
+#endif
+#ifndef EGES_BK_VARINV
+#define EGES_BK_VARINV 0  // variable-time safegcd for r^-1 and Z^-1: slower here (lanes diverge)
+#endif
+constexpr int BK_RING = EGES_BK_RING;
+constexpr int GJ_WORDS = 3 * FE_LIMBS;
+
+enum { BF_DIG = 0, BF_Y, BF_G, BF_Q2, BF_PUB, BF_CON0, BF_CON1, BF_PARSED, BF_STAGE_FREE, BF_N };
+
+constexpr int BK_STAGE_WORDS = 2 * GJ_WORDS * MID_L;  // wire form: staged encodings (13.5 KB)
+struct BktLds {
+  uint32_t ring[BK_RING][GJ_WORDS][MID_L];           // published P_{3k}, slot k % BK_RING
+  uint32_t bucket[2][BK_NB][GJ_WORDS][MID_L];        // per half; lanes index their own bucket
+  union {
+    uint32_t part[2][GJ_WORDS][MID_L];               // 0: u1 G (E), 1: Q2 (E')
+    uint32_t stage[BK_STAGE_WORDS];                  // wire form: the workgroup's encodings, until
+  } u;                                               //   wave S has hashed them (BF_STAGE_FREE)
+  uint32_t xr[8][MID_L];                             // wire form: R's x, the pre-check meta, ok
+  uint32_t meta[MID_L];
+  uint8_t pok[MID_L];
+  uint32_t y[FE_LIMBS][MID_L];
+  uint8_t binf[2][BK_NB][MID_L];
+  uint8_t pinf[2][MID_L];
+  uint8_t yok[MID_L];
+  int8_t dig[2][BK_WIN][MID_L];
+  uint32_t flag[BF_N];
+};
+static_assert(sizeof(BktLds) <= 160 * 1024, "bucket form LDS");
+
+DEV void lds_put_gej(uint32_t (*a)[MID_L], const gej& p, uint32_t l) {
+  lds_put_fe<FE_LIMBS>(a, p.x.v, l);
+  lds_put_fe<FE_LIMBS>(a + FE_LIMBS, p.y.v, l);
+  lds_put_fe<FE_LIMBS>(a + 2 * FE_LIMBS, p.z.v, l);
+}
+DEV gej lds_get_gej(const uint32_t (*a)[MID_L], uint32_t l) {
+  gej p;
+  lds_get_fe<FE_LIMBS>(a, p.x.v, l);
+  lds_get_fe<FE_LIMBS>(a + FE_LIMBS, p.y.v, l);
+  lds_get_fe<FE_LIMBS>(a + 2 * FE_LIMBS, p.z.v, l);
+  return p;
+}
+
+// LDS counters: the producer publishes a count (release), consumers wait until it reaches k.
+DEV void cnt_set(uint32_t* f, uint32_t v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+DEV uint32_t cnt_get(const uint32_t* f) {
+  return __hip_atomic_load(const_cast<uint32_t*>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// The bound (~1 s) only keeps a logic error from hanging the device (results would be wrong).
+DEV void cnt_wait(const uint32_t* f, uint32_t k) {
+#pragma unroll 1
+  for (uint32_t it = 0; it < (1u << 24); ++it) {
+    if (cnt_get(f) >= k) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// a + b, both Jacobian, neither at infinity, a != +-b (add-2007-bl, join_mid without the checks).
+// In: X m1, Y <= 2, Z <= 2. Out: X, Y m1, Z m2.
+DEV gej gej_add_fast(const gej& a, const gej& b) {
+  const fe Z1Z1 = fe_sqr(a.z), Z2Z2 = fe_sqr(b.z);
+  const fe U1 = fe_mul(a.x, Z2Z2);
+  const fe S1 = fe_mul(fe_mul(a.y, b.z), Z2Z2);
+  const fe H = fe_mul_sub<1>(b.x, Z1Z1, U1);                   // U2 - U1
+  const fe Rd = fe_mul_sub<1>(fe_mul(b.y, a.z), Z1Z1, S1);     // S2 - S1
+  const fe H2 = fe_add(H, H), R2 = fe_add(Rd, Rd);
+  const fe I = fe_sqr(H2);
+  const fe J = fe_mul(H, I);
+  const fe V = fe_mul(U1, I);
+  gej r;
+  r.x = fe_sqr_sub<2>(R2, fe_add(J, fe_add(V, V)));
+  r.y = fe_mul_sub<1, 1>(R2, fe_sub<1>(V, r.x), fe_mul(S1, J));
+  const fe zh = fe_mul(fe_mul(a.z, b.z), H);
+  r.z = fe_add(zh, zh);
+  return r;
+}
+
+// signed BK_BITS-bit windows of a GLV half into this lane's column (core.cuh recode)
+DEV void recode_bk(const glv_half& h, int8_t (*out)[MID_L], uint32_t l) {
+  uint32_t m[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) m[i] = h.mag[i];
+  int carry = 0;
+#pragma unroll 1
+  for (int w = 0; w < BK_WIN; ++w) {
+    constexpr uint32_t mask = (1u << BK_BITS) - 1;
+    int v = (int)(m[0] & mask) + carry;
+    carry = v > (1 << (BK_BITS - 1)) ? 1 : 0;
+    v -= carry << BK_BITS;
+    out[w][l] = (int8_t)(h.neg ? -v : v);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m[i] = (m[i] >> BK_BITS) | (m[i + 1] << (32 - BK_BITS));
+    m[4] >>= BK_BITS;
+  }
+}
+
+// Wire form: the workgroup's encodings [lo, hi) (relative to wire_raw, which is 4-byte aligned)
+// copied into S.u.stage by all 256 threads with coalesced dword loads (from pinned host memory
+// these are long PCIe reads instead of one dependent byte load per RLP header); bytes past the
+// stage's capacity stay in global memory. Returns the staged window [a0, end).
+DEV void wire_stage(BktLds& S, const RecoverParams& prm, uint64_t& a0, uint64_t& end) {
+  const uint32_t i0 = blockIdx.x * MID_L;
+  const uint32_t cnt = prm.n - i0 < (uint32_t)MID_L ? prm.n - i0 : (uint32_t)MID_L;
+  const uint64_t* off = prm.wire_off + prm.wire_first;
+  const uint64_t base = prm.wire_off[0], lo = off[i0] - base, hi = off[i0 + cnt] - base;
+  a0 = lo & ~(uint64_t)3;
+  end = a0;
+  if (hi <= lo || off[i0] < base) return;  // malformed offsets: every item reads global memory
+  const uint64_t full = (hi - a0) / 4;  // whole dwords inside [a0, hi): no read past the batch
+  const uint32_t nw = full < (uint64_t)BK_STAGE_WORDS ? (uint32_t)full : (uint32_t)BK_STAGE_WORDS;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(prm.wire_raw + a0);
+#pragma unroll 4
+  for (uint32_t w = threadIdx.x; w < nw; w += MID_WG) S.u.stage[w] = src[w];
+  end = a0 + 4 * (uint64_t)nw;
+  if (nw == full && nw < (uint32_t)BK_STAGE_WORDS) {  // the tail bytes of the last dword
+    const uint32_t tb = (uint32_t)(hi - end);
+    if (threadIdx.x < tb) reinterpret_cast<uint8_t*>(S.u.stage)[4 * nw + threadIdx.x] = prm.wire_raw[end + threadIdx.x];
+    end = hi;
+  }
+}
+
+// Wire form, wave S, one lane per transaction: tx_rows_kernel's decode (k_txhash.hip, rlp.cuh)
+// and prep_sender_kernel's classification (sender.cuh) of item idx. Fills q as lat_parse would
+// (except q.Z: the signing hash comes later, from m).
+DEV void wire_parse(const BktLds& S, const RecoverParams& prm, uint32_t idx, uint64_t a0, uint64_t end, LatParse& q,
+                    Payload& m) {
+  const uint64_t base = prm.wire_off[0], a = prm.wire_off[prm.wire_first + idx], e = prm.wire_off[prm.wire_first + idx + 1];
+  const bool span_ok = e >= a && a >= base;
+  const uint64_t ra = span_ok ? a - base : 0, len = span_ok ? e - a : 0;
+  const uint8_t* p = (ra >= a0 && ra + len <= end) ? reinterpret_cast<const uint8_t*>(S.u.stage) + (ra - a0)
+                                                   : prm.wire_raw + ra;
+  RlpHead f[10]{};
+  const bool ok = span_ok && tx_parse(p, len, prm.wire_signer, prm.wire_chain_id, f, m);
+  uint32_t r[8], s[8], v[8];
+  uint32_t fl = VF_DECODE_ERR;
+  if (ok) {
+    uint8_t b[32];
+    fl = 0;
+    fl |= rlp_to_be32(p, f[7], b) ? 0u : 1u;  // EGES_VF_V_WIDE
+    limbs_from_be32(v, b);
+    fl |= rlp_to_be32(p, f[8], b) ? 0u : 2u;  // EGES_VF_R_WIDE
+    limbs_from_be32(r, b);
+    fl |= rlp_to_be32(p, f[9], b) ? 0u : 4u;  // EGES_VF_S_WIDE
+    limbs_from_be32(s, b);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] = s[k] = v[k] = 0;
+    m.p = p;  // an empty payload: the sponge absorbs one block
+    m.hlen = 0;
+    m.mid_len = 0;
+    m.tlen = 0;
+    m.to_patch = false;
+  }
+  q.meta = sender_meta(r, s, v, fl, prm.wire_signer, prm.wire_chain_id);
+  q.recid = q.meta & 3u;
+  q.ok = ((q.meta >> 8) & 0xffu) == ST_OK;
+  bool ovr, ovs;
+  q.R = sc_from_limbs(r, ovr);
+  q.Sv = sc_from_limbs(s, ovs);
+  q.ok = q.ok && !ovr && !ovs && !sc_is_zero(q.R) && !sc_is_zero(q.Sv);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q.xr[i] = q.R.v[i];  // recid < 2 on this path: x = r
+}
+
+template <class ST>
+DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
+  __shared__ BktLds S;
+  ST st_;
+  const Diag dg = diag_of(prm);
+  const uint32_t l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t idx = blockIdx.x * MID_L + l;
+  const bool live = idx < prm.n;
+  const bool wire = prm.wire_raw != nullptr;  // kernel-uniform
+  uint64_t stage_a0 = 0, stage_end = 0;
+  if (threadIdx.x < BF_N) S.flag[threadIdx.x] = 0u;
+  if (wire) wire_stage(S, prm, stage_a0, stage_end);
+  __syncthreads();  // the only barrier
+  LatParse q;
+  Payload m;
+  if (!wire) {
+    q = lat_parse(prm, live ? idx : prm.n - 1);
+  } else if (wv == 1) {
+    wire_parse(S, prm, live ? idx : prm.n - 1, stage_a0, stage_end, q, m);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) S.xr[i][l] = q.xr[i];
+    S.meta[l] = q.meta;
+    S.pok[l] = live && q.ok ? 1u : 0u;
+    mflag_set(&S.flag[BF_PARSED]);
+  } else if (wv == 0) {
+    mflag_wait(&S.flag[BF_PARSED]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q.xr[i] = S.xr[i][l];
+    q.ok = S.pok[l] != 0;
+  } else {
+    q.ok = false;  // Y waves: read from LDS at the end
+  }
+  auto stamp_out = [&] {
+    if constexpr (!std::is_same<ST, NoStamp>::value) {
+      if (l == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) stamps[((size_t)blockIdx.x * 4 + wv) * 8 + i] = st_.acc[i];
+      }
+    }
+  };
+  const bool pok = live && q.ok;
+  const ge G = gen_point();
+  const fe x = fe_select(pok, fe_from_u256(q.xr), G.x);
+  if (wv == 1) {  // ---- S: scalars, digits, y, u1 G
+    st_.mark(0);
+    const sc R = sc_select(pok, q.R, sc_one());
+    const sc rinv = EGES_BK_VARINV ? sc_inv_var(R) : sc_inv(R);
+    const sc u2 = sc_select(pok, sc_mul(rinv, q.Sv), sc_one());
+    st_.mark(1);
+    glv_half h1, h2;
+    glv_split(h1, h2, u2);
+    recode_bk(h1, S.dig[0], l);
+    recode_bk(h2, S.dig[1], l);
+    mflag_set(&S.flag[BF_DIG]);
+    st_.mark(2);
+    if (wire) {  // the signing hash (FrontierSigner / EIP155Signer.Hash) of the encoding, then z
+      uint8_t h[32];
+      keccak256_payload(m, h);
+      mflag_set(&S.flag[BF_STAGE_FREE]);
+      if (prm.wire_sighash && live) {  // zeros for an undecodable item, as tx_rows_kernel
+        const bool dec = ((q.meta >> 8) & 0xffu) != ST_DECODE_FAILED;
+        uint32_t* dst = reinterpret_cast<uint32_t*>(prm.wire_sighash + (size_t)idx * 32);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          dst[k] = dec ? (uint32_t)h[4 * k] | ((uint32_t)h[4 * k + 1] << 8) | ((uint32_t)h[4 * k + 2] << 16) |
+                             ((uint32_t)h[4 * k + 3] << 24)
+                       : 0u;
+      }
+      uint32_t zl[8];
+      limbs_from_be32(zl, h);
+      bool ovz;
+      q.Z = sc_from_limbs(zl, ovz);  // msg mod n (main_impl.h:183)
+      st_.mark(5);
+    }
+    const sc u1 = sc_neg(sc_mul(rinv, q.Z));  // main_impl.h:114-117
+    ge Rp;
+    const bool yok = ge_set_xo(Rp, x, pok && (q.recid & 1u) != 0);  // ge_set_xo_var, group_impl.h:216-237
+    lds_put_fe<FE_LIMBS>(S.y, Rp.y.v, l);
+    S.yok[l] = yok ? 1u : 0u;
+    mflag_set(&S.flag[BF_Y]);
+    st_.mark(3);
+    const uint32_t* gcomb = prm.gtab + (size_t)2 * GTAB * PT_WORDS;
+    gej Ga;
+    bool ginf;
+    comb_mid<false>(Ga, ginf, u1, gcomb, dg);
+    if (dg.force || __any(!ginf && fe_is_zero(Ga.z))) {
+      diag_bump(dg, EGES_DIAG_MID_REDO);
+      comb_mid<true>(Ga, ginf, u1, gcomb, dg);
+    }
+    lds_put_gej(S.u.part[0], Ga, l);
+    S.pinf[0][l] = ginf ? 1u : 0u;
+    mflag_set(&S.flag[BF_G]);
+    st_.mark(4);
+    stamp_out();
+    return;
+  }
+  // R' = (c x, c^2) on E': y^2 = x^3 + 7 c^3, c = x^3 + 7 (no square root on this path)
+  const fe c = fe_normalize_weak(fe_add(fe_mul(fe_sqr(x), x), fe_from_u32(7)));
+  if (wv == 0) {  // ---- X: the doubling chain
+    st_.mark(0);
+    gej P;
+    P.x = fe_mul(c, x);
+    P.y = fe_sqr(c);
+    P.z = fe_one();
+    uint32_t freed = BK_RING;  // slots known free: points < freed - BK_RING consumed by both halves
+#pragma unroll 1
+    for (int k = 0; k < BK_WIN; ++k) {
+      if (k > 0) {
+#pragma unroll 1
+        for (int i = 0; i < BK_BITS; ++i) P = gej_double(P);  // R' has odd order: never exceptional
+      }
+      if ((uint32_t)k >= freed) {  // slot k % BK_RING is free once both halves consumed point k - BK_RING
+        st_.mark(1);
+        cnt_wait(&S.flag[BF_CON0], (uint32_t)(k - BK_RING + 1));
+        cnt_wait(&S.flag[BF_CON1], (uint32_t)(k - BK_RING + 1));
+        const uint32_t c0 = cnt_get(&S.flag[BF_CON0]), c1 = cnt_get(&S.flag[BF_CON1]);
+        freed = (c0 < c1 ? c0 : c1) + BK_RING;
+        st_.mark(2);
+      }
+      lds_put_gej(S.ring[k % BK_RING], P, l);
+      cnt_set(&S.flag[BF_PUB], (uint32_t)(k + 1));
+    }
+    st_.mark(1);
+    stamp_out();
+    return;
+  }
+  // ---- Y1 / Y2: the buckets of one GLV half
+  const int h = (int)wv - 2;
+  st_.mark(0);
+#pragma unroll
+  for (int v = 0; v < BK_NB; ++v) S.binf[h][v][l] = 1u;
+  mflag_wait(&S.flag[BF_DIG]);
+  st_.mark(1);
+  uint32_t avail = 0;  // points known published
+#pragma unroll 1
+  for (int k = 0; k < BK_WIN; ++k) {
+    if ((uint32_t)k >= avail) {
+      st_.mark(2);
+      cnt_wait(&S.flag[BF_PUB], (uint32_t)(k + 1));
+      avail = cnt_get(&S.flag[BF_PUB]);
+      st_.mark(3);
+    }
+    gej P = lds_get_gej(S.ring[k % BK_RING], l);
+    const int d = (int)S.dig[h][k][l];
+    cnt_set(&S.flag[BF_CON0 + h], (uint32_t)(k + 1));  // LDS reads of one wave complete in order
+    const int a = d < 0 ? -d : d;
+    const int v = a > 0 ? a - 1 : 0;
+    P.y = fe_select(d < 0, fe_neg<1>(P.y), P.y);
+    const gej B = lds_get_gej(S.bucket[h][v], l);
+    const bool binf = S.binf[h][v][l] != 0;
+    const gej s = gej_select(binf, P, gej_add_fast(B, P));
+    if (d != 0) {
+      lds_put_gej(S.bucket[h][v], s, l);
+      S.binf[h][v][l] = 0u;
+    }
+  }
+  st_.mark(2);
+  // Q_h = B1 + 2 B2 + 3 B3 + 4 B4 = (B1 + B3) + 2 ((B2 + B3) + 2 B4): four joins, two doublings
+  static_assert(BK_NB == 4, "bucket sum written for 3-bit windows");
+  bool i1, i2, i3, i4, ia, ib, tinf;
+  const gej B3 = lds_get_gej(S.bucket[h][2], l);
+  i3 = S.binf[h][2][l] != 0;
+  i1 = S.binf[h][0][l] != 0;
+  const gej Ja = join_mid(lds_get_gej(S.bucket[h][0], l), i1, B3, i3, ia, dg);
+  i2 = S.binf[h][1][l] != 0;
+  gej Jb = join_mid(lds_get_gej(S.bucket[h][1], l), i2, B3, i3, ib, dg);
+  i4 = S.binf[h][3][l] != 0;
+  Jb = join_mid(Jb, ib, gej_double(lds_get_gej(S.bucket[h][3], l)), i4, ib, dg);
+  gej T = join_mid(Ja, ia, gej_double(Jb), ib, tinf, dg);
+  st_.mark(4);
+  if (h == 1) {
+    T.x = fe_mul(T.x, fe_const(FE_BETA));  // lambda (X, Y, Z) = (beta X, Y, Z)
+    if (wire) mflag_wait(&S.flag[BF_STAGE_FREE]);  // part[1] shares LDS with the stage
+    lds_put_gej(S.u.part[1], T, l);
+    S.pinf[1][l] = tinf ? 1u : 0u;
+    mflag_set(&S.flag[BF_Q2]);
+    stamp_out();
+    return;
+  }
+  // ---- Y1: the joins and the address
+  mflag_wait(&S.flag[BF_Q2]);
+  bool qinf, oinf;
+  gej Q = join_mid(T, tinf, lds_get_gej(S.u.part[1], l), S.pinf[1][l] != 0, qinf, dg);
+  mflag_wait(&S.flag[BF_Y]);
+  fe y;
+  lds_get_fe<FE_LIMBS>(S.y, y.v, l);
+  const bool yok = S.yok[l] != 0;
+  Q.z = fe_mul(Q.z, y);  // E' -> E: (X, Y, Z) is (X, Y, Z y)
+  mflag_wait(&S.flag[BF_G]);
+  st_.mark(5);
+  Q = join_mid(Q, qinf, lds_get_gej(S.u.part[0], l), S.pinf[0][l] != 0, oinf, dg);
+  qinf = oinf;
+  if (wire) {
+    mflag_wait(&S.flag[BF_PARSED]);
+    q.meta = S.meta[l];
+  }
+  const bool ok = (wire ? S.pok[l] != 0 : pok) && yok && !qinf;  // main_impl.h:120
+  if (__any(ok && fe_is_zero(Q.z))) diag_bump(dg, EGES_DIAG_MID_EXC);  // never (see above)
+  st_.mark(5);
+  const fe zq = fe_select(ok, Q.z, fe_one());
+  const fe zi = EGES_BK_VARINV ? fe_inv_var(zq) : fe_inv(zq);
+  const fe zi2 = fe_sqr(zi);
+  uint32_t X[8], Y[8];
+  fe_to_u256(X, fe_normalize(fe_mul(Q.x, zi2)));
+  fe_to_u256(Y, fe_normalize(fe_mul(Q.y, fe_mul(zi2, zi))));
+  st_.mark(6);
+  if (live) {
+    const uint32_t pre_st = (q.meta >> 8) & 0xffu;
+    prm.status[idx] = (uint8_t)(pre_st != ST_OK ? pre_st : (ok ? ST_OK : ST_RECOVER_FAILED));
+    if (prm.addr) {
+      uint32_t a[5];
+      pub_address(a, X, Y);
+      uint32_t* dst = reinterpret_cast<uint32_t*>(prm.addr + (size_t)idx * prm.addr_stride);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) dst[i] = ok ? a[i] : 0u;
+    }
+    if (prm.pub) {
+      uint8_t* dst = prm.pub + (size_t)idx * 65;
+      if (ok) {
+        dst[0] = 4;
+        write_be32(dst + 1, X);
+        write_be32(dst + 33, Y);
+      } else {
+        for (int i = 0; i < 65; ++i) dst[i] = 0;
+      }
+    }
+  }
+  st_.mark(7);
+  stamp_out();
+}
+
+__global__ void __launch_bounds__(MID_WG, 1) recover_bkt_kernel(RecoverParams prm) {
+  recover_bkt_body<NoStamp>(prm, nullptr);
+}
+
 __global__ void __launch_bounds__(MID_WG, 2) recover_mid_kernel(RecoverParams prm) {
   recover_mid_body<NoStamp>(prm, nullptr);
 }
@@ -444,8 +885,12 @@ __global__ void __launch_bounds__(MID_WG, 2) recover_mid_kernel(RecoverParams pr
 size_t mid_ws_bytes_per_block() { return MID_WS_WORDS * sizeof(uint32_t); }
 
 // ws must hold ceil(n / 64) blocks of mid_ws_bytes_per_block(); the caller checks
-hipError_t launch_recover_mid(const RecoverParams& p, size_t ws_bytes, hipStream_t st) {
+hipError_t launch_recover_mid(const RecoverParams& p, bool bucket, size_t ws_bytes, hipStream_t st) {
   if (p.n == 0) return hipSuccess;
+  if (bucket) {  // no workspace
+    hipLaunchKernelGGL(recover_bkt_kernel, dim3((p.n + MID_L - 1) / MID_L), dim3(MID_WG), 0, st, p);
+    return hipGetLastError();
+  }
   const uint32_t grid = (p.n + MID_L - 1) / MID_L;
   if ((size_t)grid * mid_ws_bytes_per_block() > ws_bytes) return hipErrorInvalidValue;
   hipLaunchKernelGGL(recover_mid_kernel, dim3(grid), dim3(MID_WG), 0, st, p);
@@ -456,8 +901,16 @@ hipError_t launch_recover_mid(const RecoverParams& p, size_t ws_bytes, hipStream
 __global__ void __launch_bounds__(MID_WG, 2) recover_mid_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
   recover_mid_body<Stamper>(prm, stamps);
 }
-hipError_t launch_recover_mid_stamped(const RecoverParams& p, size_t ws_bytes, hipStream_t st, uint64_t* stamps) {
+__global__ void __launch_bounds__(MID_WG, 1) recover_bkt_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
+  recover_bkt_body<Stamper>(prm, stamps);
+}
+hipError_t launch_recover_mid_stamped(const RecoverParams& p, bool bucket, size_t ws_bytes, hipStream_t st,
+                                      uint64_t* stamps) {
   if (p.n == 0) return hipSuccess;
+  if (bucket) {
+    hipLaunchKernelGGL(recover_bkt_kernel_stamped, dim3((p.n + MID_L - 1) / MID_L), dim3(MID_WG), 0, st, p, stamps);
+    return hipGetLastError();
+  }
   const uint32_t grid = (p.n + MID_L - 1) / MID_L;
   if ((size_t)grid * mid_ws_bytes_per_block() > ws_bytes) return hipErrorInvalidValue;
   hipLaunchKernelGGL(recover_mid_kernel_stamped, dim3(grid), dim3(MID_WG), 0, st, p, stamps);

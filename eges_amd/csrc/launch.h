@@ -47,6 +47,15 @@ struct RecoverParams {
   uint32_t* diag = nullptr;
   // tests only (KNOB_FORCE_REDO): run every exact-redo pass as if an accumulator was poisoned
   uint32_t force_redo = 0;
+  // mid-size bucket form only: wire-format transactions instead of record rows (tx_rows_kernel
+  // and prep_sender_kernel fused in): item i is wire_raw[wire_off[first + i] - wire_off[0],
+  // wire_off[first + i + 1] - wire_off[0]); wire_raw 4-byte aligned. wire_sighash: n x 32 or null.
+  const uint8_t* wire_raw = nullptr;
+  const uint64_t* wire_off = nullptr;  // item i's offsets at wire_off[wire_first + i (+ 1)]
+  uint64_t wire_first = 0;
+  int wire_signer = 0;
+  uint64_t wire_chain_id = 0;
+  uint8_t* wire_sighash = nullptr;
 };
 
 struct VerifyParams {
@@ -100,7 +109,8 @@ hipError_t launch_tx_rows(const uint8_t* raw, const uint64_t* offsets, uint64_t 
 #ifdef EGES_PHASE_STAMPS
 hipError_t launch_recover_stamped(const RecoverParams& p, int max_blocks, int ws_blocks, hipStream_t st, uint64_t* stamps);
 hipError_t launch_recover_lat_stamped(const RecoverParams& p, hipStream_t st, uint64_t* stamps);
-hipError_t launch_recover_mid_stamped(const RecoverParams& p, size_t ws_bytes, hipStream_t st, uint64_t* stamps);
+hipError_t launch_recover_mid_stamped(const RecoverParams& p, bool bucket, size_t ws_bytes, hipStream_t st,
+                                      uint64_t* stamps);
 size_t lat_waves(uint32_t n);
 #endif
 // max_blocks: the resident grid; ws_blocks: blocks the workspace p.ws was allocated for. A
@@ -110,9 +120,11 @@ hipError_t launch_recover(const RecoverParams& p, int max_blocks, int ws_blocks,
 // Same inputs (prep records) and outputs as launch_recover; no workspace.
 hipError_t launch_recover_lat(const RecoverParams& p, hipStream_t st);
 // Mid-size batches: 64 signatures per 4-wave workgroup, one role per wave (k_recover_mid.hip).
-// Uses p.ws (ceil(n / 64) blocks of mid_ws_bytes_per_block(), refused beyond ws_bytes).
-hipError_t launch_recover_mid(const RecoverParams& p, size_t ws_bytes, hipStream_t st);
+// bucket: the bucket form (no workspace, one workgroup per CU); else the windowed form, which
+// uses p.ws (ceil(n / 64) blocks of mid_ws_bytes_per_block(), refused beyond ws_bytes).
+hipError_t launch_recover_mid(const RecoverParams& p, bool bucket, size_t ws_bytes, hipStream_t st);
 size_t mid_ws_bytes_per_block();
+constexpr uint32_t MID_SIGS_PER_BLOCK = 64;
 hipError_t launch_verify(const VerifyParams& p, int max_blocks, int ws_blocks, hipStream_t st);
 // one item per 128-thread workgroup (k_recover_lat.hip; wide: 192 threads, three partial sums);
 // uses pub/publen/msg/sig/n/ok/gtab only

@@ -30,6 +30,27 @@ def oracle():
     return Oracle()
 
 
+# Wire-format sender paths (eges_sender_raw_batch / _dev, eges_block_senders_raw): the default
+# dispatch (small batches: tx_rows + prep_sender + the latency kernels) and the fused form, where
+# the mid-size kernel's bucket form decodes, hashes and classifies the encodings itself
+# (k_recover_mid.hip wire_stage / wire_parse), forced for every batch size with engine knobs.
+WIRE_FORMS = {
+    "tx_rows": {},
+    "fused": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2, "EGES_WIRE_FUSED": 1},
+}
+
+
+@pytest.fixture(params=sorted(WIRE_FORMS))
+def wire_form(request, engine):
+    kv = WIRE_FORMS[request.param]
+    old = {k: engine.get_knob(k) for k in kv}
+    for k, v in kv.items():
+        engine.set_knob(k, v)
+    yield request.param
+    for k, v in old.items():
+        engine.set_knob(k, v)
+
+
 def load_golden(name):
     import numpy as np
     return np.load(os.path.join(GOLDEN, name), allow_pickle=False)

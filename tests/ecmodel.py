@@ -10,6 +10,9 @@ in advance which addition of which form meets P == +-Q:
   narrow       u_r R over the 26 windows (wave 0) and u_g G by the 16-bit comb (wave 1), joined
   split        windows [0, 15) of both halves (wave 0), the rest in 4-bit windows per half
                against D = 2^75 R (waves 2, 3, joined), u_g G by the comb; joins (A + G) + H
+  bucket       the mid-size kernel: each GLV half in signed 3-bit windows, window k's digit d
+               adds sign(d) 2^(3k) R into bucket |d| (bottom-up), Q_h = (B1 + B3) +
+               2 ((B2 + B3) + 2 B4), then (Q_1 + Q_2) + u_g G (k_recover_mid.hip recover_bkt_body)
 
 Points are tracked by their discrete log to base G (R = rho G with rho known to the test), so
 "acc == +-P" is a congruence mod n. The reference resolves these sums with explicit branches
@@ -38,6 +41,7 @@ RBITS, RWIN = 5, 26          # core.cuh
 GBITS, GWIN, GSTEP = 20, 7, 4
 CBITS, CWIN = 16, 16         # comb
 SPLIT_W0, HBITS = 15, 4      # k_recover_lat.hip
+BK_BITS, BK_WIN, BK_NB = 3, 43, 4  # k_recover_mid.hip bucket form
 HWIN = (130 - RBITS * SPLIT_W0 + HBITS) // HBITS
 
 
@@ -233,6 +237,29 @@ def split(u_r, u_g, rho):
         hs.append(h)
     H = join(hs[0], hs[1], ev, "join_hi")
     q = join(join(a, comb(u_g, ev), ev, "join"), H, ev, "join")
+    return (None if q.inf else q.v), ev
+
+
+def bucket(u_r, u_g, rho):
+    """k_recover_mid.hip bucket form: buckets per half (tags bk0 / bk1, the unchecked additions),
+    running sums (bsum) and the joins (join12: Q_1 + Q_2, join: + u_g G), all exact."""
+    ev = []
+    qs = []
+    for h, k in enumerate(glv_split(u_r)):
+        d = recode(k, BK_BITS, BK_WIN)[0]
+        base = rho * (LAM if h else 1)
+        B = [Acc(ev, f"bk{h}") for _ in range(BK_NB)]
+        for j in range(BK_WIN):
+            if d[j]:
+                B[abs(d[j]) - 1].add((1 if d[j] > 0 else -1) * base * 2**(BK_BITS * j), j)
+        # (B1 + B3) + 2 ((B2 + B3) + 2 B4)
+        a = join(B[0], B[2], ev, "bsum")
+        b = join(B[1], B[2], ev, "bsum")
+        B[3].dbl(1)
+        b = join(b, B[3], ev, "bsum")
+        b.dbl(1)
+        qs.append(join(a, b, ev, "bsum"))
+    q = join(join(qs[0], qs[1], ev, "join12"), comb(u_g, ev), ev, "join")
     return (None if q.inf else q.v), ev
 
 

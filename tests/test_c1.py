@@ -69,7 +69,8 @@ def test_c1_senders_gpu(engine):
     r, s, v = txs.sender_rows(sig)
     # every recover form that can take the batch: the engine's default dispatch, the mid-size
     # kernel, the lane-serial kernel (knobs, eges_test_set_knob)
-    forms = [{}, {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20}, {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 0}]
+    forms = [{}, {"EGES_WIRE_FUSED": 0}, {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 0},
+             {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 0}]
     for kv in forms:
         old = {k: engine.get_knob(k) for k in kv}
         try:

@@ -79,7 +79,7 @@ def test_knobs_set_and_read_without_gpu():
     with eges_amd.knob("EGES_LAT_MAX", 17):
         assert eges_amd.get_knob("EGES_LAT_MAX") == 17
     assert eges_amd.get_knob("EGES_LAT_MAX") == old
-    for name in ("EGES_LAT_WIDE_MAX", "EGES_MID_MAX", "EGES_TXROWS_WAVE_MAX", "EGES_TEST_ROOT_HELPERS",
+    for name in ("EGES_LAT_WIDE_MAX", "EGES_MID_MAX", "EGES_MID_FORM", "EGES_WIRE_FUSED", "EGES_TXROWS_WAVE_MAX", "EGES_TEST_ROOT_HELPERS",
                  "EGES_OVERLAP", "EGES_TEST_FORCE_REDO", "EGES_COALESCE_GATHER_US", "EGES_COALESCE_SPIN_US",
                  "EGES_COALESCE_SPINNERS"):
         eges_amd.get_knob(name)

@@ -27,6 +27,8 @@ def test_glv_split_is_the_reduced_decomposition():
         k1, k2 = M.glv_split(k)
         assert (k1 + k2 * M.LAM - k) % M.N == 0
         assert abs(k1) < 2**129 and abs(k2) < 2**129
+        # the bound the bucket form's 43 windows rely on (k_recover_mid.hip BK_WIN)
+        assert abs(k1) < 0.64 * 2**128 and abs(k2) < 0.55 * 2**128
         # Babai coordinates of (k1, k2) in the basis v1 = (a1, -|b1|), v2 = (a2, a1) are within
         # 1/2 + 2^-120 of zero: (k1, k2) is the reduced representative of its coset
         det = M.GLV_A1 * M.GLV_A1 + M.GLV_A2 * M.GLV_B1  # == n
@@ -42,7 +44,7 @@ def test_random_scalars_meet_no_exceptional_sum():
         rho = rnd.randrange(1, M.N)
         u_r, u_g = rnd.randrange(1, M.N), rnd.randrange(1, M.N)
         want = (u_r * rho + u_g) % M.N
-        for form in (M.lane_serial, M.narrow, M.split):
+        for form in (M.lane_serial, M.narrow, M.split, M.bucket):
             q, ev = form(u_r, u_g, rho)
             assert q == want and ev == [], (form.__name__, ev)
 
@@ -62,9 +64,9 @@ def test_verdict_construction_does_not_poison_the_r_loops():
                 e = rnd.randrange(-15, 17)
                 u_r = ((a + b * M.LAM) * 32**(w + 1) + (j + e * M.LAM) * 32**w + low) % M.N
                 rho = rnd.randrange(1, M.N)
-                for form in (M.narrow, M.split):
+                for form in (M.narrow, M.split, M.bucket):
                     _, ev = form(u_r, rnd.randrange(1, M.N), rho)
-                    assert not [x for x in ev if x[0] in ("lat_r", "lat_lo", "lat_hi0", "lat_hi1")], (w, j, ev)
+                    assert not [x for x in ev if x[0] in ("lat_r", "lat_lo", "lat_hi0", "lat_hi1", "bk0", "bk1")], (w, j, ev)
                 _, ev = M.lane_serial(u_r, rnd.randrange(1, M.N), rho)
                 assert ev == [], (w, j, ev)
                 hits += 1
@@ -130,3 +132,48 @@ def test_verify_constructions():
             assert Q[0] % M.N == r  # a valid signature through the doubling branch
             valid += 1
     assert valid >= 1
+
+
+def small_u2_cases():
+    """u2 values whose digits leave buckets (or whole halves) empty: the bucket form's sums then
+    join infinities; tests/test_gpu_mid.py runs them."""
+    return [1, 2, 3, 4, 5, 6, 8, 16, 24, 2**3 * 3, 2**30 * 4, 2**129 - 1, M.LAM, 2 * M.LAM % M.N, M.N - 1, M.N - 2,
+            M.N - 4, 3 * 2**60 + 2]
+
+
+def test_bucket_form_schedule():
+    """The mid-size kernel's bucket form (k_recover_mid.hip): neither its unchecked bucket
+    additions nor its bucket sums ever meet +-P (edge, small and structured scalars included); the
+    final join with u1 G does for the "join" constructions tests/test_gpu_mid.py uses, and the
+    joined result is always u_r rho + u_g."""
+    rnd = random.Random(7)
+    for u2 in small_u2_cases() + [rnd.randrange(1, 2**k) for k in (3, 6, 9, 40, 130) for _ in range(20)]:
+        for u1 in (1, rnd.randrange(1, M.N)):
+            rho = rnd.randrange(1, M.N)
+            q, ev = M.bucket(u2, u1, rho)
+            assert (q if q is not None else 0) == (u2 * rho + u1) % M.N
+            assert not [x for x in ev if x[0] in ("bk0", "bk1", "bsum", "join12")], (u2, ev)
+    # the cases of tests/test_gpu_mid.py::test_bucket_exceptional_joins
+    seen = set()
+    for kind, sign, rho, R, u1, u2 in M.recover_cases(rnd, 6):
+        q, ev = M.bucket(u2, u1, rho)
+        assert (q if q is not None else 0) == (u2 * rho + u1) % M.N
+        assert not [x for x in ev if x[0] in ("bk0", "bk1", "bsum", "join12")]
+        if kind == "join":
+            assert ("join", "dbl" if sign == 1 else "inf") in {(t, b) for t, b, _ in ev}
+            seen.add(sign)
+    assert seen == {1, -1}
+
+
+def test_bucket_halves_never_join_exceptionally():
+    """Q_1 == +-Q_2 needs k1 == +-lambda k2 (mod n) for the split's own output: k1 == -lambda k2
+    means u2 == 0; k1 == lambda k2 puts (k1, k2) on the lattice {x == lambda y}, whose short
+    vectors are not reduced representatives of the split (Babai rounding maps them elsewhere)."""
+    v1, v2 = (M.GLV_A1, M.GLV_B1), (M.GLV_A2, -M.GLV_A1)
+    for a, b in (v1, v2):
+        assert (a - M.LAM * b) % M.N == 0
+    for i in range(-6, 7):
+        for j in range(-6, 7):
+            if i or j:
+                k = (i * v1[0] + j * v2[0], i * v1[1] + j * v2[1])
+                assert M.glv_split((k[0] + M.LAM * k[1]) % M.N) != k

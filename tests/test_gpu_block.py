@@ -9,7 +9,7 @@ import pytest
 from eges_amd import txs
 from oracle import txoracle as T
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("wire_form")]
 
 
 def signed_block(engine, first, n, payload=100):

@@ -29,7 +29,8 @@ FORMS = {  # knob settings per form (recovery / verification)
     "lane_serial": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 0},
     "narrow": {"EGES_LAT_MAX": LAT_ALL, "EGES_LAT_WIDE_MAX": 0},
     "split": {"EGES_LAT_MAX": LAT_ALL, "EGES_LAT_WIDE_MAX": LAT_ALL},
-    "mid": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": LAT_ALL},
+    "mid": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": LAT_ALL, "EGES_MID_FORM": 0},
+    "mid_bucket": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": LAT_ALL, "EGES_MID_FORM": 2},
 }
 
 
@@ -101,6 +102,9 @@ def test_recover_exceptional_sums_every_form(engine, oracle):
         elif form == "mid":
             # the split constructions meet the mid-size kernel's joins ((A + u1 G) + H, as split)
             assert d["mid_join"] > 0 and d["mid_redo"] == 0 and d["mid_exc"] == 0, d
+        elif form == "mid_bucket":
+            # the ls / join constructions (u2 R == +-u1 G) meet the bucket form's final join
+            assert d["mid_join"] > 0 and d["mid_redo"] == 0 and d["mid_exc"] == 0, d
         else:
             assert d["join_dbl"] > 0 and d["join_inf"] > 0, (form, d)
             assert d["lat_redo"] == 0 and d["comb_redo"] == 0 and d["lat_exc"] == 0, (form, d)
@@ -131,12 +135,12 @@ def test_precompile_and_single_item_exceptional(engine, oracle):
     cases, msg, sig = _recover_inputs(seed=12)
     est, epub = _expected_recover(oracle, msg, sig)
     inputs = [msg[i].tobytes() + bytes(31) + bytes([27 + sig[i, 64]]) + sig[i, :64].tobytes() for i in range(len(msg))]
-    for form in ("narrow", "split", "mid"):
+    for form in ("narrow", "split", "mid", "mid_bucket"):
         engine.diag_counters(reset=True)
         with knobs(engine, FORMS[form]):
             out, st = engine.ecrecover_precompile_batch(inputs)
         d = engine.diag_counters(reset=True)
-        if form == "mid":
+        if form in ("mid", "mid_bucket"):
             assert d["mid_join"] > 0, d
         else:
             assert d["join_dbl"] > 0 and d["join_inf"] > 0, (form, d)
@@ -178,7 +182,7 @@ def test_verify_exceptional_sums_every_form(engine, oracle):
         assert np.array_equal(ok, exp), (form, np.nonzero(ok != exp)[0])
         if form == "lane_serial":
             assert d["ls_redo"] > 0 and d["ls_exc"] > 0, d
-        elif form == "mid":  # (verification has no mid-size form: the lane-serial kernel runs)
+        elif form in ("mid", "mid_bucket"):  # (verification has no mid-size form: lane-serial runs)
             assert d["ls_redo"] > 0 and d["ls_exc"] > 0, d
         else:
             assert d["join_dbl"] > 0 and d["join_inf"] > 0, (form, d)
@@ -202,7 +206,7 @@ def test_forced_redo_every_form_golden(engine):
         assert np.array_equal(ok, gv["ok"]), form
         if form == "lane_serial":
             assert d["ls_redo"] > 0, d
-        elif form == "mid":
+        elif form in ("mid", "mid_bucket"):
             assert d["mid_redo"] > 0 and d["ls_redo"] > 0, d  # recovery: mid-size; verification: lane-serial
         else:
             assert d["lat_redo"] > 0 and d["comb_redo"] > 0, (form, d)

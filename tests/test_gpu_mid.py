@@ -2,8 +2,9 @@
 per wave) against the fixtures, the oracle and the other two recover forms.
 
 Forms are selected with engine knobs (eges_test_set_knob): EGES_LAT_MAX = 0 and EGES_MID_MAX
-large send every batch through the mid-size kernel; EGES_MID_MAX = 0 through the lane-serial
-kernel. Every output byte must agree across forms and with the reference-generated fixtures."""
+large send every batch through the mid-size kernel, in its bucket form (EGES_MID_FORM = 1, the
+default) or its windowed form (0); EGES_MID_MAX = 0 sends it through the lane-serial kernel.
+Every output byte must agree across forms and with the reference-generated fixtures."""
 import numpy as np
 import pytest
 
@@ -11,7 +12,9 @@ from conftest import load_golden
 
 pytestmark = pytest.mark.gpu
 
-MID = {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20}
+MID = {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2}
+MID_WIN = dict(MID, EGES_MID_FORM=0)
+FORMS = {"bucket": MID, "windowed": MID_WIN}
 LANE = {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 0}
 
 
@@ -29,9 +32,11 @@ class knobs:
             self.engine.set_knob(k, v)
 
 
-def test_mid_golden_recover_and_sender(engine):
+@pytest.mark.parametrize("form", sorted(FORMS))
+def test_mid_golden_recover_and_sender(engine, form):
     """every golden recovery item (all reject classes) and every golden sender item through the
     mid-size kernel: byte for byte the fixtures (reference libsecp256k1, oracle/_ref)"""
+    MID = FORMS[form]
     g = load_golden("recover.npz")
     with knobs(engine, MID):
         pub, addr, st = engine.ecrecover_batch(g["msg"], g["sig"])
@@ -52,10 +57,12 @@ def test_mid_golden_recover_and_sender(engine):
         assert np.array_equal(a, g2["addr"][sel]), (signer, cid)
 
 
-def test_mid_golden_tiled_ragged(engine):
+@pytest.mark.parametrize("form", sorted(FORMS))
+def test_mid_golden_tiled_ragged(engine, form):
     """the golden recovery set tiled to 10,007 items (ragged last workgroup), device-resident
     entry, mid-size kernel vs the fixtures item for item"""
     import torch
+    MID = FORMS[form]
     g = load_golden("recover.npz")
     n = 10007
     rep = -(-n // len(g["msg"]))
@@ -70,8 +77,9 @@ def test_mid_golden_tiled_ragged(engine):
     assert np.array_equal(pub, np.tile(g["pub"], (rep, 1))[:n])
 
 
+@pytest.mark.parametrize("form", sorted(FORMS))
 @pytest.mark.parametrize("n", [10000, 50000])
-def test_mid_adversarial_mix(engine, oracle, n):
+def test_mid_adversarial_mix(engine, oracle, n, form):
     """configs[4]'s mix at 10k and 50k through the mid-size kernel: statuses bit-exact against
     their expectation and equal to the lane-serial kernel's, addresses of accepted items the
     signers', a sample of every class against the oracle"""
@@ -87,7 +95,7 @@ def test_mid_adversarial_mix(engine, oracle, n):
     rows = [torch.from_numpy(x).cuda() for x in (r, s, v)]
     vf = torch.zeros(n, dtype=torch.uint8, device="cuda")
     out = {}
-    for name, kv in (("mid", MID), ("lane", LANE)):
+    for name, kv in (("mid", FORMS[form]), ("lane", LANE)):
         with knobs(engine, kv):
             pub, addr, st = engine.ecrecover_batch_dev(msg, sig_m, pub=torch.empty((n, 65), dtype=torch.uint8,
                                                                                     device="cuda"))
@@ -108,12 +116,13 @@ def test_mid_adversarial_mix(engine, oracle, n):
 
 
 def test_mid_exceptional_joins(engine, oracle):
-    """the split-form constructions (tests/ecmodel.py) meet the mid-size kernel's joins: both the
-    doubling and the infinity branch run, results equal the oracle's; forced redo of its loops
-    and comb leaves the golden outputs unchanged"""
+    """windowed form: the split-form constructions (tests/ecmodel.py) meet the mid-size kernel's
+    joins: both the doubling and the infinity branch run, results equal the oracle's; forced redo
+    of its loops and comb leaves the golden outputs unchanged"""
     import random
 
     import ecmodel as M
+    MID = MID_WIN
     cases = [c for c in M.recover_cases(random.Random(21), 8) if c[0] in ("split1", "split2")]
     msg = np.frombuffer(b"".join(M.recover_input(c[2], c[3], c[4], c[5])[0] for c in cases), np.uint8).reshape(-1, 32)
     sig = np.frombuffer(b"".join(M.recover_input(c[2], c[3], c[4], c[5])[1] for c in cases), np.uint8).reshape(-1, 65)
@@ -132,3 +141,42 @@ def test_mid_exceptional_joins(engine, oracle):
     d = engine.diag_counters(reset=True)
     assert np.array_equal(st, g["status"]) and np.array_equal(pub, g["pub"])
     assert d["mid_redo"] > 0, d
+
+
+def test_bucket_exceptional_joins(engine, oracle):
+    """bucket form: u2 values that leave buckets empty (the running sums meet a == b) and u1 chosen
+    against u2 R (the final join meets a == +-b, tests/ecmodel.py "join" cases), all through the
+    exact branches (mid_join > 0), no bucket addition poisoned (mid_exc == 0), every result the
+    oracle's and the lane-serial kernel's; forced redo of the comb keeps the golden outputs"""
+    import random
+
+    import ecmodel as M
+    from test_exceptional_model import small_u2_cases
+    rnd = random.Random(22)
+    items = []
+    for u2 in small_u2_cases():
+        rho, R = M.point_for(rnd.randrange(1, M.N))
+        items.append(M.recover_input(rho, R, rnd.randrange(1, M.N), u2))
+    for kind, sign, rho, R, u1, u2 in M.recover_cases(rnd, 8):
+        if kind == "join":
+            items.append(M.recover_input(rho, R, u1, u2))
+    msg = np.frombuffer(b"".join(m for m, _ in items), np.uint8).reshape(-1, 32)
+    sig = np.frombuffer(b"".join(s_ for _, s_ in items), np.uint8).reshape(-1, 65)
+    engine.diag_counters(reset=True)
+    with knobs(engine, MID):
+        pub, addr, st = engine.ecrecover_batch(msg, sig)
+    d = engine.diag_counters(reset=True)
+    assert d["mid_join"] > 0 and d["mid_exc"] == 0 and d["mid_redo"] == 0, d
+    with knobs(engine, LANE):
+        pub2, addr2, st2 = engine.ecrecover_batch(msg, sig)
+    assert np.array_equal(pub, pub2) and np.array_equal(st, st2)
+    for i in range(len(msg)):
+        ost, opub = oracle.recover_pubkey(msg[i].tobytes(), sig[i].tobytes())
+        assert ost == st[i] and (ost != 0 or opub == pub[i].tobytes()), i
+    assert (st == 6).any() and (st == 0).any()
+    g = load_golden("recover.npz")
+    with knobs(engine, dict(MID, EGES_TEST_FORCE_REDO=1)):
+        pub, addr, st = engine.ecrecover_batch(g["msg"], g["sig"])
+    d = engine.diag_counters(reset=True)
+    assert np.array_equal(st, g["status"]) and np.array_equal(pub, g["pub"])
+    assert d["mid_redo"] > 0 and d["mid_exc"] == 0, d

@@ -15,7 +15,7 @@ import pytest
 from conftest import GOLDEN
 from oracle import txoracle as T
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("wire_form")]
 
 CHAIN = 930412  # genesis.json.template chainId
 SIGNERS = (0, 1, 2)

@@ -16,7 +16,7 @@ import pytest
 
 from oracle import txoracle as T
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("wire_form")]
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 FIELDS = {"uint": (0, 2), "uint32": (0, 2), "bigint": (1, 4, 7, 8, 9), "bytes": (5,), "bool": (6,)}

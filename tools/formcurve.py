@@ -21,7 +21,9 @@ sys.path.insert(0, ROOT)
 
 FORMS = {
     "lat": {"EGES_LAT_MAX": 1 << 20, "EGES_MID_MAX": 0},
-    "mid": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20},
+    "mid": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2},
+    "midw": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 0},
+    "midnf": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2, "EGES_WIRE_FUSED": 0},
     "lane": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 0},
 }
 
@@ -49,6 +51,8 @@ def main():
     for n in sizes:
         packed = eges_amd.pack_raw(raws[:n])
         for form, kv in FORMS.items():
+            if form not in os.environ.get("FORMCURVE_FORMS", "lat,mid,midw,lane").split(","):
+                continue
             if form == "lat" and n > lat_cap:
                 continue
             old = {k: eges_amd.get_knob(k) for k in kv}

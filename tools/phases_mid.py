@@ -30,7 +30,19 @@ ROLES = {
     3: ("C", {0: "parse + R'", 1: "D = 2^75 R'", 2: "D table (8)", 3: "wait: digits", 4: "high windows"}),
 }
 
+BUCKET_ROLES = {
+    0: ("X", {0: "parse + R'", 1: "129 doublings", 2: "wait: ring slot"}),
+    1: ("S", {0: "parse", 1: "r^-1, u1, u2", 2: "GLV + digits", 5: "sighash (wire)", 3: "y (sqrt)",
+              4: "u1 G comb"}),
+    2: ("Y1", {0: "parse", 1: "wait: digits", 2: "bucket adds", 3: "wait: P_3k", 4: "bucket sums",
+               5: "joins (+ waits)", 6: "Z^-1 + affine", 7: "Keccak + stores"}),
+    3: ("Y2", {0: "parse", 1: "wait: digits", 2: "bucket adds", 3: "wait: P_3k", 4: "bucket sums"}),
+}
+FORM = int(os.environ.get("EGES_MID_FORM", "2"))
+if FORM:
+    ROLES = BUCKET_ROLES
 assert lib.eges_init(0, 0) == 0, lib.eges_last_error()
+assert lib.eges_test_set_knob(b"EGES_MID_FORM", FORM) == 0
 assert lib.eges_test_set_knob(b"EGES_LAT_MAX", 0) == 0 and lib.eges_test_set_knob(b"EGES_MID_MAX", 1 << 20) == 0
 dev = torch.device("cuda:0")
 for n in [int(x) for x in (sys.argv[1:] or ["10000"])]:
@@ -52,7 +64,8 @@ for n in [int(x) for x in (sys.argv[1:] or ["10000"])]:
     buf = (ctypes.c_uint64 * (rows * 8))()
     lib.eges_diag_read_stamps(buf, rows)
     a = np.frombuffer(buf, dtype=np.uint64).reshape(rows // 4, 4, 8).astype(np.float64)
-    print(f"n={n} launch {dt * 1e3:.3f} ms (stamped build, host-timed), workgroups={rows // 4}")
+    print(f"n={n} launch {dt * 1e3:.3f} ms (stamped build, host-timed), workgroups={rows // 4}, "
+          f"form {'bucket' if FORM else 'windowed'}")
     for w, (name, ph) in ROLES.items():
         tot = a[:, w, :].sum(axis=1)
         print(f"  wave {w} ({name}): total mean {tot.mean():.4g} max {tot.max():.4g} ticks")
