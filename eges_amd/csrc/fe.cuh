@@ -104,7 +104,9 @@ DEV fe fe_reduce_cols(uint64_t S[17]) {
   // than EGES_FOLD 0 (32 MADs, every hi folded down) and 2.5 % faster than EGES_FOLD 2 (push
   // from odd columns only: 29 MADs) on the same box — the serial chain costs nothing visible.
   // (The same push in the carry pass below, one MAD + 32-bit carry-in instead of a 64-bit
-  // shift + add, measured 1 % slower.)
+  // shift + add, measured 1 % slower; carries in two independent rounds instead of the serial
+  // pass, for a single wave per SIMD, measured 12 % slower on the mid-size kernel's doubling
+  // chain, r03: the chain is bound by issue, not by its dependences.)
   // Column 9 holds 8 products (< 2^63.7), so every pushed 8 hi < 2^35 keeps columns < 2^64.
 #if EGES_FOLD == 0
 #pragma unroll

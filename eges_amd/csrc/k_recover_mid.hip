@@ -518,9 +518,16 @@ DEV gej lds_get_gej(const uint32_t (*a)[MID_L], uint32_t l) {
   return p;
 }
 
-// LDS counters: the producer publishes a count (release), consumers wait until it reaches k.
+// LDS counters: the producer publishes a count, consumers wait until it reaches k. Only LDS
+// data is handed over this way, and the LDS performs one wave's DS instructions in order, so a
+// compiler barrier orders the data stores before the count store (a workgroup fence would also
+// wait for the stores to complete: measured ~4 % of the doubling chain).
+#ifndef EGES_BK_FENCE
+#define EGES_BK_FENCE 0
+#endif
 DEV void cnt_set(uint32_t* f, uint32_t v) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (EGES_BK_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  else __atomic_signal_fence(__ATOMIC_SEQ_CST);
   if ((threadIdx.x & 63) == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 DEV uint32_t cnt_get(const uint32_t* f) {
@@ -533,7 +540,8 @@ DEV void cnt_wait(const uint32_t* f, uint32_t k) {
     if (cnt_get(f) >= k) break;
     __builtin_amdgcn_s_sleep(1);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (EGES_BK_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  else __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
 // a + b, both Jacobian, neither at infinity, a != +-b (add-2007-bl, join_mid without the checks).
@@ -603,8 +611,10 @@ DEV void wire_stage(BktLds& S, const RecoverParams& prm, uint64_t& a0, uint64_t&
 // Wire form, wave S, one lane per transaction: tx_rows_kernel's decode (k_txhash.hip, rlp.cuh)
 // and prep_sender_kernel's classification (sender.cuh) of item idx. Fills q as lat_parse would
 // (except q.Z: the signing hash comes later, from m).
-DEV void wire_parse(const BktLds& S, const RecoverParams& prm, uint32_t idx, uint64_t a0, uint64_t end, LatParse& q,
-                    Payload& m) {
+// (Not inlined: the decoder's ten item heads would otherwise raise the register pressure of the
+// whole kernel, the doubling and bucket loops included.)
+__device__ __attribute__((noinline)) void wire_parse(const BktLds& S, const RecoverParams& prm, uint32_t idx,
+                                                     uint64_t a0, uint64_t end, LatParse& q, Payload& m) {
   const uint64_t base = prm.wire_off[0], a = prm.wire_off[prm.wire_first + idx], e = prm.wire_off[prm.wire_first + idx + 1];
   const bool span_ok = e >= a && a >= base;
   const uint64_t ra = span_ok ? a - base : 0, len = span_ok ? e - a : 0;
@@ -642,6 +652,8 @@ DEV void wire_parse(const BktLds& S, const RecoverParams& prm, uint32_t idx, uin
 #pragma unroll
   for (int i = 0; i < 8; ++i) q.xr[i] = q.R.v[i];  // recid < 2 on this path: x = r
 }
+
+__device__ __attribute__((noinline)) void wire_sighash(const Payload& m, uint8_t* h) { keccak256_payload(m, h); }
 
 template <class ST>
 DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
@@ -700,7 +712,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
     st_.mark(2);
     if (wire) {  // the signing hash (FrontierSigner / EIP155Signer.Hash) of the encoding, then z
       uint8_t h[32];
-      keccak256_payload(m, h);
+      wire_sighash(m, h);
       mflag_set(&S.flag[BF_STAGE_FREE]);
       if (prm.wire_sighash && live) {  // zeros for an undecodable item, as tx_rows_kernel
         const bool dec = ((q.meta >> 8) & 0xffu) != ST_DECODE_FAILED;

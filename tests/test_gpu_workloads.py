@@ -1,7 +1,10 @@
-"""GPU tests of the BASELINE configs beyond C2, at reduced sizes, through the C-ABI:
-C3 (a Geec block of EIP-155 transactions via eges_sender_batch), C5 (the adversarial mix:
-every status bit-exact against its by-construction expectation, a sample against the oracle)
+"""GPU tests of the BASELINE configs beyond C2 through the C-ABI: C3 (a Geec block of EIP-155
+transactions via eges_sender_batch), C5 (the adversarial mix: every status bit-exact against
+its by-construction expectation and a sample against the oracle at 20k; at the full 1M of
+configs[4], every item's result and address against the reference libsecp256k1, oracle/_ref)
 and VerifySignature mode (33/65-byte and hybrid keys, high-s, wrong key)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -53,6 +56,34 @@ def test_adversarial_mix_bit_exact(engine, oracle):
             ost2, _ = oracle.sender(2, txs.GEEC_CHAIN_ID, msg_h[i].tobytes(), r[i].tobytes(), s[i].tobytes(),
                                     v[i].tobytes(), 0)
             assert ost2 == st2[i]
+
+
+def test_adversarial_mix_1m_vs_reference(engine):
+    """configs[4] at its full size: 1,048,576 signatures, 10 % invalid over seven classes. Every
+    item through eges_ecrecover_batch_dev (the lane-serial kernel at this size) against the
+    reference libsecp256k1's secp256k1_ext_ecdsa_recover (oracle/_ref, compiled in place, run on
+    the host's cores): accepted exactly where the reference accepts, the same 65-byte key and
+    address everywhere; and every status equal to its by-construction expectation."""
+    import torch
+    from eges_amd import workloads
+    from oracle import RefLib, have_ref
+    if not have_ref():
+        pytest.skip("oracle/_ref not built")
+    n = 1 << 20
+    msg, sig, exp = engine.synth_sign_dev(7 << 40, n, 0)
+    torch.cuda.synchronize()
+    sig_h, msg_h = sig.cpu().numpy(), msg.cpu().numpy()
+    kind = workloads.adversarial_mix(sig_h, frac=0.10, seed=4)
+    pub, addr, st = engine.ecrecover_batch_dev(msg, torch.from_numpy(sig_h).cuda(),
+                                               pub=torch.empty((n, 65), dtype=torch.uint8, device="cuda"))
+    torch.cuda.synchronize()
+    pub, addr, st = pub.cpu().numpy(), addr.cpu().numpy(), st.cpu().numpy()
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    rpub, raddr, ret = RefLib().ecrecover_batch_mt(msg_h, sig_h, threads)
+    assert np.array_equal(st == 0, ret == 1), np.nonzero((st == 0) != (ret == 1))[0][:10]
+    assert np.array_equal(pub, rpub) and np.array_equal(addr[st == 0], raddr[st == 0])
+    assert np.array_equal(st, workloads.expected_status(kind, "ecrecover"))
+    assert (st != 0).sum() > n // 20
 
 
 def test_verify_mode_mix(engine, oracle):
