@@ -13,7 +13,8 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-KERNELS = ("eges::recover_kernel", "eges::verify_kernel", "eges::recover_lat_kernel")
+KERNELS = ("eges::recover_kernel", "eges::verify_kernel", "eges::recover_lat_kernel", "eges::recover_bkt_kernel",
+           "eges::recover_mid_kernel")
 
 
 def summarise(root):
