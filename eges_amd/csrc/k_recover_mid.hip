@@ -633,14 +633,9 @@ __device__ __attribute__((noinline)) void wire_parse(const BktLds& S, const Reco
     limbs_from_be32(r, b);
     fl |= rlp_to_be32(p, f[9], b) ? 0u : 4u;  // EGES_VF_S_WIDE
     limbs_from_be32(s, b);
-  } else {
+  } else {  // (no sponge for it: wave S skips undecodable items)
 #pragma unroll
     for (int k = 0; k < 8; ++k) r[k] = s[k] = v[k] = 0;
-    m.p = p;  // an empty payload: the sponge absorbs one block
-    m.hlen = 0;
-    m.mid_len = 0;
-    m.tlen = 0;
-    m.to_patch = false;
   }
   q.meta = sender_meta(r, s, v, fl, prm.wire_signer, prm.wire_chain_id);
   q.recid = q.meta & 3u;
@@ -712,7 +707,12 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
     st_.mark(2);
     if (wire) {  // the signing hash (FrontierSigner / EIP155Signer.Hash) of the encoding, then z
       uint8_t h[32];
-      wire_sighash(m, h);
+      if (((q.meta >> 8) & 0xffu) != ST_DECODE_FAILED) {
+        wire_sighash(m, h);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 32; ++k) h[k] = 0;
+      }
       mflag_set(&S.flag[BF_STAGE_FREE]);
       if (prm.wire_sighash && live) {  // zeros for an undecodable item, as tx_rows_kernel
         const bool dec = ((q.meta >> 8) & 0xffu) != ST_DECODE_FAILED;

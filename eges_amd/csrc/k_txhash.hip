@@ -71,7 +71,8 @@ constexpr int TXW_STAGE = 1024;   // staged bytes per wave; longer encodings dec
 DEV uint32_t rlp_be32_byte(const uint8_t* __restrict__ p, const RlpHead& h, uint32_t lane) {
   const uint64_t len = h.kind == RK_BYTE ? 1 : h.size;
   const int j = (int)lane - (32 - (int)len);
-  return (len <= 32 && j >= 0) ? p[h.off + j] : 0u;
+  const uint32_t b = p[(len <= 32 && j >= 0) ? h.off + j : h.start];  // in-bounds either way (rlp.cuh)
+  return (len <= 32 && j >= 0) ? b : 0u;
 }
 
 __global__ void __launch_bounds__(64 * TXW_WAVES) tx_rows_wave_kernel(

@@ -50,7 +50,7 @@ DEV bool rlp_head(const uint8_t* __restrict__ p, uint64_t pos, uint64_t lim, Rlp
   h.off = off;
   h.size = size;
   h.next = off + size;
-  h.b = size ? p[off] : 0u;
+  h.b = p[size ? off : pos] & (size ? 0xffu : 0u);  // (both addresses inside the item: see Payload::at)
   return true;
 }
 
@@ -88,7 +88,8 @@ DEV bool rlp_to_be32(const uint8_t* __restrict__ p, const RlpHead& h, uint8_t* _
   const uint64_t src = h.off;
   for (int k = 0; k < 32; ++k) {
     const int j = k - (32 - (int)len);
-    out[k] = j >= 0 ? p[src + j] : (uint8_t)0;
+    const uint8_t b = p[j >= 0 ? src + j : h.start];  // in-bounds whichever way the select goes
+    out[k] = j >= 0 ? b : (uint8_t)0;
   }
   return true;
 }
@@ -103,13 +104,18 @@ struct Payload {
   bool to_patch;
   uint64_t tail0, tail1;
   uint32_t tlen;
+  // The one memory read is at an index clamped into [mid0, mid0 + mid_len) (mid_len >= 1 for a
+  // decoded txdata) whatever j is: when the compiler turns the branches into selects and loads
+  // unconditionally, the address still lies inside the item. (Unclamped, a header byte j of a
+  // payload whose header is longer than the transaction's, mid0 < hlen, became p[-1]: one byte
+  // before the first encoding, an aperture violation when p is the start of a wave's LDS stage.)
   DEV uint32_t at(uint64_t j) const {
+    const uint64_t k = j - hlen;  // wraps below hlen
+    const uint64_t q = mid0 + (k < mid_len ? k : 0);
+    const uint32_t mb = (to_patch && q == to_pos) ? 0x80u : (uint32_t)p[q];
     if (j < hlen) return j < 8 ? (uint32_t)(hdr0 >> (8 * j)) & 0xffu : (uint32_t)hdr1 & 0xffu;
     j -= hlen;
-    if (j < mid_len) {
-      const uint64_t q = mid0 + j;
-      return (to_patch && q == to_pos) ? 0x80u : (uint32_t)p[q];
-    }
+    if (j < mid_len) return mb;
     j -= mid_len;
     if (j < tlen) return j < 8 ? (uint32_t)(tail0 >> (8 * j)) & 0xffu : (uint32_t)(tail1 >> (8 * (j - 8))) & 0xffu;
     return 0;

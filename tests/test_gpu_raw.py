@@ -229,3 +229,26 @@ def test_ecrecover_precompile(engine, oracle):
     o2, s2 = engine.ecrecover_precompile_batch_dev(torch.from_numpy(buf).cuda(), torch.from_numpy(ln).cuda())
     torch.cuda.synchronize()
     assert np.array_equal(o2.cpu().numpy(), out) and np.array_equal(s2.cpu().numpy(), st)
+
+
+def test_short_tx_with_long_signing_header(engine, oracle):
+    """Unsigned Geec transactions with short payloads: the encoding's list header is one byte (a
+    body <= 55 bytes) while the EIP-155 signing payload's is two (the chain-id tail pushes it past
+    55). Regression: the signing-payload reader once loaded the byte before such an encoding (an
+    aperture violation when it sat at the start of a wave's LDS stage, found by
+    tools/sanitize_host.cpp). Alone, first in a batch, between signed items, and as an unselected
+    (decode-only) and a selected list of a block; every result against the oracle."""
+    from eges_amd import txs
+    short = [txs.encode_geec_tx(0, 1, 21000, b"\x22" * 20, 7, b"\x41" * n, True, 0, 0, 0) for n in (22, 23, 10, 30)]
+    assert len(short[0]) == 55 and len(short[1]) == 56  # one-byte list headers; payload bodies 56, 57
+    for signer in SIGNERS:
+        _check(engine, oracle, short, signer, CHAIN)
+        _check(engine, oracle, short[:1], signer, CHAIN)
+    tx_raws = _signed_txs(engine, 770_000, 40, lambda i: i % 50, np.random.default_rng(5))[0]
+    mixed = [short[1]] + tx_raws[:20] + short + tx_raws[20:]
+    _check(engine, oracle, mixed, 2, CHAIN)
+    for lists in (0, 2, 4, 7):
+        raw = txs.geec_extblock(short[:2], short, tx_raws)
+        addr, st, counts, bst = engine.block_senders_raw(raw, lists=lists)
+        ost, oaddr, _, obst = T.block_senders(oracle, raw, lists, 2, txs.GEEC_CHAIN_ID)
+        assert bst == obst and st.tolist() == ost and [a.tobytes() for a in addr] == oaddr, lists

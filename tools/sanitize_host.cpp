@@ -353,9 +353,17 @@ int main(int argc, char** argv) {
   const int mutations = argc > 1 ? std::atoi(argv[1]) : 20000;
   int ndev = 0;
   g_nodev = hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0;
+  const bool trace = std::getenv("SANITIZE_TRACE") != nullptr;
+  auto step = [&](const char* s) {
+    if (trace) std::fprintf(stderr, "== step %s\n", s), std::fflush(stderr);
+  };
+  step("keccak");
   keccak_known_answers();
+  step("arguments");
   argument_validation();
+  step("block structure");
   block_structure(mutations);
+  step("init");
   const bool gpu = eges_init(1, 0) == EGES_SUCCESS;
   if (!gpu) {
     std::printf("no GPU engine (%s): host-only paths\n", eges_last_error());
