@@ -483,7 +483,14 @@ constexpr int BK_NB = 1 << (BK_BITS - 1);             // buckets for |digit| = 1
 constexpr int BK_RING = EGES_BK_RING;
 constexpr int GJ_WORDS = 3 * FE_LIMBS;
 
-enum { BF_DIG = 0, BF_Y, BF_G, BF_Q2, BF_PUB, BF_CON0, BF_CON1, BF_PARSED, BF_STAGE_FREE, BF_N };
+enum {
+  BF_DIG = 0, BF_Y, BF_G, BF_Q2, BF_PUB, BF_CON0, BF_CON1, BF_PARSED, BF_STAGE_FREE, BF_FIN0, BF_FIN1, BF_A0, BF_A1,
+  BF_N
+};
+// ring slots that hold wave X's partial bucket sums B1 + B3 of each half once the ring is drained
+// (their points, 33 and 34, are consumed by both halves before either finishes)
+constexpr int BK_ASLOT = 3;
+static_assert(BK_RING > BK_ASLOT + 1 && BK_WIN - BK_RING > BK_ASLOT + 1, "partial-sum slots");
 
 constexpr int BK_STAGE_WORDS = 2 * GJ_WORDS * MID_L;  // wire form: staged encodings (13.5 KB)
 struct BktLds {
@@ -499,6 +506,7 @@ struct BktLds {
   uint32_t y[FE_LIMBS][MID_L];
   uint8_t binf[2][BK_NB][MID_L];
   uint8_t pinf[2][MID_L];
+  uint8_t ainf[2][MID_L];
   uint8_t yok[MID_L];
   int8_t dig[2][BK_WIN][MID_L];
   uint32_t flag[BF_N];
@@ -778,6 +786,22 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
       cnt_set(&S.flag[BF_PUB], (uint32_t)(k + 1));
     }
     st_.mark(1);
+    // then, per half, B1 + B3 of its final buckets (the halves' own waves do the rest of the sum
+    // meanwhile), into a drained ring slot
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+      mflag_wait(&S.flag[BF_FIN0 + h]);
+      const uint32_t slot = (uint32_t)(BK_ASLOT + h), pt = slot + (uint32_t)BK_RING * ((BK_WIN - 1 - slot) / BK_RING);
+      cnt_wait(&S.flag[BF_CON0], pt + 1);  // the last point that slot held, consumed by both halves
+      cnt_wait(&S.flag[BF_CON1], pt + 1);
+      bool ia;
+      const gej a = join_mid(lds_get_gej(S.bucket[h][0], l), S.binf[h][0][l] != 0, lds_get_gej(S.bucket[h][2], l),
+                             S.binf[h][2][l] != 0, ia, dg);
+      lds_put_gej(S.ring[slot], a, l);
+      S.ainf[h][l] = ia ? 1u : 0u;
+      mflag_set(&S.flag[BF_A0 + h]);
+    }
+    st_.mark(2);
     stamp_out();
     return;
   }
@@ -812,18 +836,17 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
     }
   }
   st_.mark(2);
-  // Q_h = B1 + 2 B2 + 3 B3 + 4 B4 = (B1 + B3) + 2 ((B2 + B3) + 2 B4): four joins, two doublings
+  // Q_h = B1 + 2 B2 + 3 B3 + 4 B4 = (B1 + B3) + 2 ((B2 + B3) + 2 B4): wave X joins B1 + B3
+  // (its chain is done), this wave the rest: three joins and two doublings on this path
   static_assert(BK_NB == 4, "bucket sum written for 3-bit windows");
-  bool i1, i2, i3, i4, ia, ib, tinf;
-  const gej B3 = lds_get_gej(S.bucket[h][2], l);
-  i3 = S.binf[h][2][l] != 0;
-  i1 = S.binf[h][0][l] != 0;
-  const gej Ja = join_mid(lds_get_gej(S.bucket[h][0], l), i1, B3, i3, ia, dg);
-  i2 = S.binf[h][1][l] != 0;
-  gej Jb = join_mid(lds_get_gej(S.bucket[h][1], l), i2, B3, i3, ib, dg);
-  i4 = S.binf[h][3][l] != 0;
-  Jb = join_mid(Jb, ib, gej_double(lds_get_gej(S.bucket[h][3], l)), i4, ib, dg);
-  gej T = join_mid(Ja, ia, gej_double(Jb), ib, tinf, dg);
+  mflag_set(&S.flag[BF_FIN0 + h]);
+  bool ib, tinf;
+  const bool i3 = S.binf[h][2][l] != 0;
+  gej Jb = join_mid(lds_get_gej(S.bucket[h][1], l), S.binf[h][1][l] != 0, lds_get_gej(S.bucket[h][2], l), i3, ib, dg);
+  Jb = join_mid(Jb, ib, gej_double(lds_get_gej(S.bucket[h][3], l)), S.binf[h][3][l] != 0, ib, dg);
+  Jb = gej_double(Jb);
+  mflag_wait(&S.flag[BF_A0 + h]);
+  gej T = join_mid(lds_get_gej(S.ring[BK_ASLOT + h], l), S.ainf[h][l] != 0, Jb, ib, tinf, dg);
   st_.mark(4);
   if (h == 1) {
     T.x = fe_mul(T.x, fe_const(FE_BETA));  // lambda (X, Y, Z) = (beta X, Y, Z)
