@@ -500,8 +500,7 @@ struct BktLds {
     uint32_t part[2][GJ_WORDS][MID_L];               // 0: u1 G (E), 1: Q2 (E')
     uint32_t stage[BK_STAGE_WORDS];                  // wire form: the workgroup's encodings, until
   } u;                                               //   wave S has hashed them (BF_STAGE_FREE)
-  uint32_t xr[8][MID_L];                             // wire form: R's x, the pre-check meta, ok
-  uint32_t meta[MID_L];
+  uint32_t meta[MID_L];                              // wire form: wave S's pre-check meta and ok
   uint8_t pok[MID_L];
   uint32_t y[FE_LIMBS][MID_L];
   uint8_t binf[2][BK_NB][MID_L];
@@ -658,6 +657,31 @@ __device__ __attribute__((noinline)) void wire_parse(const BktLds& S, const Reco
 
 __device__ __attribute__((noinline)) void wire_sighash(const Payload& m, uint8_t* h) { keccak256_payload(m, h); }
 
+// Wire form, wave X: only R's 32 bytes (item 8 of the txdata list) as x, by walking the item
+// heads. An item S rejects (decode, V / chain id, range checks) is invalid whatever x is (its
+// result is discarded), and for every valid one this is S's r: the chain needs no S flag.
+__device__ __attribute__((noinline)) bool wire_r_only(const BktLds& S, const RecoverParams& prm, uint32_t idx,
+                                                      uint64_t a0, uint64_t end, uint32_t xr[8]) {
+  const uint64_t base = prm.wire_off[0], a = prm.wire_off[prm.wire_first + idx], e = prm.wire_off[prm.wire_first + idx + 1];
+  if (!(e >= a && a >= base)) return false;
+  const uint64_t ra = a - base, len = e - a;
+  const uint8_t* p = (ra >= a0 && ra + len <= end) ? reinterpret_cast<const uint8_t*>(S.u.stage) + (ra - a0)
+                                                   : prm.wire_raw + ra;
+  RlpHead L{}, f{};
+  bool ok = rlp_head(p, 0, len, L) && L.kind == RK_LIST;
+  uint64_t pos = L.off;
+  const uint64_t lend = L.off + L.size;
+#pragma unroll 1
+  for (int k = 0; k < 9 && ok; ++k) {
+    ok = rlp_head(p, pos, lend, f);
+    pos = f.next;
+  }
+  uint8_t b[32];
+  ok = ok && rlp_to_be32(p, f, b);
+  if (ok) limbs_from_be32(xr, b);
+  return ok;
+}
+
 template <class ST>
 DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
   __shared__ BktLds S;
@@ -677,16 +701,11 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
     q = lat_parse(prm, live ? idx : prm.n - 1);
   } else if (wv == 1) {
     wire_parse(S, prm, live ? idx : prm.n - 1, stage_a0, stage_end, q, m);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) S.xr[i][l] = q.xr[i];
     S.meta[l] = q.meta;
     S.pok[l] = live && q.ok ? 1u : 0u;
     mflag_set(&S.flag[BF_PARSED]);
-  } else if (wv == 0) {
-    mflag_wait(&S.flag[BF_PARSED]);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) q.xr[i] = S.xr[i][l];
-    q.ok = S.pok[l] != 0;
+  } else if (wv == 0) {  // R's x straight from the encoding, without waiting for S's checks
+    q.ok = live && wire_r_only(S, prm, idx, stage_a0, stage_end, q.xr);
   } else {
     q.ok = false;  // Y waves: read from LDS at the end
   }
