@@ -368,7 +368,7 @@ hipError_t launch_recover_pass(Dev& d, const RecoverParams& p0, hipStream_t st) 
   // the split form (four waves per signature) while the batch leaves SIMDs idle
   p.wide = p.n <= wide_max() ? 1u : 0u;
   const bool mid = use_mid(d, p.n);
-  if (p.wire_raw && !(mid && mid_bucket(d, p.n))) return hipErrorInvalidValue;  // wire_fused() decides
+  if (p.wire_raw && !(mid ? mid_bucket(d, p.n) : p.n <= lat_max())) return hipErrorInvalidValue;  // wire_fused() decides
 #ifdef EGES_PHASE_STAMPS
   if (mid) {
     hipError_t e = stamp_buf((p.n + 63) / 64 * 4, st);  // one row per wave
@@ -484,11 +484,14 @@ int run_sender_dev(Dev& d, const uint8_t* sighash, const uint8_t* r, const uint8
 // Wire-format transactions: tx_rows_kernel (decode + sighash) writes the sender rows into device
 // scratch after the recovery records; then the sender pipeline runs unchanged.
 inline size_t tx_rows_bytes(size_t m) { return align_up(m * (4 * 32 + 1), 256); }
-// Batches the bucket form takes run their wire-format decode, sighash and Sender checks inside
-// the recovery kernel (RecoverParams::wire_*): no tx_rows / prep_sender launches and no rows in
-// between (EGES_WIRE_FUSED = 0 turns it off for A/B).
+// Batches the bucket form or the latency kernels take run their wire-format decode, sighash and
+// Sender checks inside the recovery kernel (RecoverParams::wire_*): no tx_rows / prep_sender
+// launches and no rows in between. EGES_WIRE_FUSED: 1 both (default), 2 the bucket form only,
+// 0 neither (A/B and tests).
 bool wire_fused(const Dev& d, size_t m, const uint8_t* raw) {
-  return knob(KNOB_WIRE_FUSED) != 0 && use_mid(d, m) && mid_bucket(d, m) && ((uintptr_t)raw & 3u) == 0;
+  const long long f = knob(KNOB_WIRE_FUSED);
+  if (f == 0 || ((uintptr_t)raw & 3u) != 0) return false;
+  return (f == 1 && m <= lat_max()) || (use_mid(d, m) && mid_bucket(d, m));
 }
 
 int run_sender_raw_dev(Dev& d, const uint8_t* raw, const uint64_t* offsets, size_t n, int signer, uint64_t chain_id,

@@ -31,11 +31,13 @@
 #include "frg.cuh"
 #include "keccak_wave.cuh"
 #include "modinv_row.cuh"
+#include "sender.cuh"
 
 namespace eges {
 
 // One signature per workgroup of two waves (narrow form); the split form has four (LAT_WG_SPLIT).
 constexpr int LAT_WG = 128;
+constexpr int LAT_STAGE = 512;  // wire form: encodings up to this size decode out of LDS
 // Split form: windows [0, SPLIT_W0) of both GLV halves against the R' table on wave 0, windows
 // [SPLIT_W0, RWIN) against a table of D = 2^(RBITS SPLIT_W0) R' on waves 2 (R) and 3 (lambda R).
 #ifndef EGES_SPLIT_W0
@@ -69,6 +71,7 @@ struct LatLds {
   uint32_t yok;
   uint32_t flag[NFLAGS];
   uint64_t w1t[2];            // diagnostic build: wave 1's r^-1 and u1 / u2 / GLV / digits ticks
+  uint8_t stage[LAT_STAGE];   // wire form: the transaction's encoding
 };
 
 // Producer / consumer hand-off between the waves of one workgroup through LDS (split form): the
@@ -184,7 +187,7 @@ DEV void recode_split(const glv_half& h, int8_t* lo, int8_t* hi) {
 // GLV split of u_r into signed 5-bit windows (core.cuh ecmult_core's digits; the split form's
 // high part in 4-bit ones), u_g for the comb
 template <bool SPLIT>
-DEV void recode_digits(const sc& u_r, const sc& u_g, LatLds& S) {
+DEV void recode_r(const sc& u_r, LatLds& S) {
   glv_half h1, h2;
   glv_split(h1, h2, u_r);
   if (SPLIT) {
@@ -194,9 +197,70 @@ DEV void recode_digits(const sc& u_r, const sc& u_g, LatLds& S) {
     recode_row<RBITS, RWIN, int8_t>(h1, S.rdig[0]);
     recode_row<RBITS, RWIN, int8_t>(h2, S.rdig[1]);
   }
-  // u_g in unsigned 16-bit digits for the comb (every lane writes the same values)
+}
+// u_g in unsigned 16-bit digits for the comb (every lane writes the same values)
+DEV void recode_g(const sc& u_g, LatLds& S) {
 #pragma unroll
   for (int k = 0; k < CWIN; ++k) S.cdig[k] = (uint16_t)(u_g.v[k >> 1] >> (16 * (k & 1)));
+}
+template <bool SPLIT>
+DEV void recode_digits(const sc& u_r, const sc& u_g, LatLds& S) {
+  recode_r<SPLIT>(u_r, S);
+  recode_g(u_g, S);
+}
+
+// ---- wire form (RecoverParams::wire_*): the transaction's encoding instead of record rows.
+// Item idx's bytes [a, e) relative to wire_raw.
+DEV bool wire_span(const RecoverParams& prm, uint32_t idx, uint64_t& ra, uint64_t& len) {
+  const uint64_t base = prm.wire_off[0], a = prm.wire_off[prm.wire_first + idx], e = prm.wire_off[prm.wire_first + idx + 1];
+  const bool ok = e >= a && a >= base;
+  ra = ok ? a - base : 0;
+  len = ok ? e - a : 0;
+  return ok;
+}
+// The signing hash of m across the wave (keccak_wave.cuh, as tx_rows_wave_kernel), as z mod n;
+// zeros for an undecodable item. Optionally written out (lanes 0..3, 8 bytes each).
+DEV sc wire_sighash_wave(const Payload& m, bool decoded, uint8_t* out32) {
+  const uint32_t lane = lane_id();
+  uint64_t st = 0;
+  if (decoded) {
+    const uint64_t M = m.length();
+    const uint64_t nblk = M / 136 + 1;
+#pragma unroll 1
+    for (uint64_t b = 0; b < nblk; ++b) {
+      if (lane < 17) {
+        uint64_t x = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint64_t j = b * 136 + 8 * lane + k;
+          uint64_t byte = j < M ? m.at(j) : 0u;
+          if (j == M) byte ^= 0x01u;
+          if (b + 1 == nblk && 8 * lane + k == 135) byte ^= 0x80u;
+          x |= byte << (8 * k);
+        }
+        st ^= x;
+      }
+      keccak_f1600_wave(st);
+    }
+  }
+  if (out32 && lane < 4) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out32[8 * lane + k] = (uint8_t)(st >> (8 * k));
+  }
+  uint8_t h[32];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)st, w, 64), hi = (uint32_t)__shfl((int)(uint32_t)(st >> 32), w, 64);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      h[8 * w + k] = (uint8_t)(lo >> (8 * k));
+      h[8 * w + 4 + k] = (uint8_t)(hi >> (8 * k));
+    }
+  }
+  uint32_t zl[8];
+  limbs_from_be32(zl, h);
+  bool ovz;
+  return sc_from_limbs(zl, ovz);  // msg mod n (main_impl.h:183)
 }
 
 template <int NT>
@@ -495,7 +559,15 @@ DEV uint32_t* root_area(const RecoverParams& prm) {
 DEV void root_helper(const RecoverParams& prm) {
   const uint32_t j = blockIdx.x * ROOT_WG + threadIdx.x;
   if (j >= prm.n) return;
-  const LatParse q = lat_parse(prm, j);
+  LatParse q;
+  if (prm.wire_raw) {  // wire form: this lane decodes item j itself (x, recid, ok: the waves' record)
+    uint64_t ra, len;
+    const bool sp = wire_span(prm, j, ra, len);
+    Payload m;
+    wire_item(prm.wire_raw + ra, len, sp, prm.wire_signer, prm.wire_chain_id, q, m);
+  } else {
+    q = lat_parse(prm, j);
+  }
   const ge G = gen_point();
   const fe x = q.ok ? fe_from_u256(q.xr) : G.x;  // the row-form waves use the same substitute
   ge r;
@@ -561,12 +633,27 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   // the helpers' lane-serial roots are a dense VALU stream: the signature waves (latency-bound
   // chains) take issue priority over them on a shared SIMD
   if (!SPLIT) __builtin_amdgcn_s_setprio(2);
-  if (SPLIT) {
-    if (threadIdx.x < NFLAGS) S.flag[threadIdx.x] = 0u;
-    __syncthreads();  // the only barrier of the split form
+  const bool wire = prm.wire_raw != nullptr;  // kernel-uniform
+  uint64_t wra = 0, wlen = 0;
+  bool wspan = false;
+  if (wire) {  // the encoding into LDS (one byte per thread per step, coalesced)
+    wspan = wire_span(prm, idx, wra, wlen);
+    if (wlen <= LAT_STAGE)
+      for (uint32_t j = threadIdx.x; j < wlen; j += blockDim.x) S.stage[j] = prm.wire_raw[wra + j];
   }
-  // --- parse (every lane reads the same record)
-  const LatParse q = lat_parse(prm, idx);
+  if (SPLIT && threadIdx.x < NFLAGS) S.flag[threadIdx.x] = 0u;
+  if (SPLIT || wire) __syncthreads();  // (split form: the only barrier besides; narrow: the stage)
+  // --- parse (every lane reads the same record; wire form: every lane decodes the same item)
+  LatParse q;
+  Payload m;
+  bool decoded = false;
+  if (wire) {
+    const uint8_t* p = wlen <= LAT_STAGE ? S.stage : prm.wire_raw + wra;
+    decoded = wire_item(p, wlen, wspan, prm.wire_signer, prm.wire_chain_id, q, m);
+    q.Z = sc_zero();  // (wave 1 hashes m for z)
+  } else {
+    q = lat_parse(prm, idx);
+  }
   const uint32_t meta = q.meta, recid = q.recid;
   bool ok = q.ok;
   sc R = q.R;
@@ -589,18 +676,27 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
     R = sc_select(ok, R, sc_one());
     const sc rinv = sc_inv_row_var(R);  // wave-uniform data: variable-time safegcd, limb-parallel
     const uint64_t t1 = stamped ? __builtin_amdgcn_s_memtime() : 0;
-    const sc u1 = sc_neg(sc_mul(rinv, Z));
     const sc u2 = sc_select(ok, sc_mul(rinv, Sv), sc_one());
-    recode_digits<SPLIT>(u2, u1, S);
+    if (wire) {
+      // the R digits first (wave 0 is waiting for them), then the signing hash for z and u1
+      recode_r<SPLIT>(u2, S);
+      if (SPLIT) flag_set(&S.flag[F_DIG]);
+      else __syncthreads();  // digits ready (and the table)
+      uint8_t* hs = prm.wire_sighash ? prm.wire_sighash + (size_t)idx * 32 : nullptr;
+      recode_g(sc_neg(sc_mul(rinv, wire_sighash_wave(m, decoded, hs))), S);
+    } else {
+      const sc u1 = sc_neg(sc_mul(rinv, Z));
+      recode_digits<SPLIT>(u2, u1, S);
+    }
     if (stamped && lane_id() == 0) {
       S.w1t[0] = t1 - t0;
       S.w1t[1] = __builtin_amdgcn_s_memtime() - t1;
     }
     if (SPLIT) {
-      flag_set(&S.flag[F_DIG]);
+      if (!wire) flag_set(&S.flag[F_DIG]);
       helper_split(S, gcomb, true, c, odd, fr_zero(), dg);
     } else {
-      __syncthreads();  // digits ready (and the table)
+      if (!wire) __syncthreads();  // digits ready (and the table)
       helper_wave(S, gcomb, false, c, odd, fr_zero(), dg);  // y: the helper workgroups (root_fetch)
     }
     return;

@@ -26,7 +26,6 @@
 #include <type_traits>
 
 #include "core.cuh"
-#include "rlp.cuh"
 #include "sender.cuh"
 
 namespace eges {
@@ -627,32 +626,7 @@ __device__ __attribute__((noinline)) void wire_parse(const BktLds& S, const Reco
   const uint64_t ra = span_ok ? a - base : 0, len = span_ok ? e - a : 0;
   const uint8_t* p = (ra >= a0 && ra + len <= end) ? reinterpret_cast<const uint8_t*>(S.u.stage) + (ra - a0)
                                                    : prm.wire_raw + ra;
-  RlpHead f[10]{};
-  const bool ok = span_ok && tx_parse(p, len, prm.wire_signer, prm.wire_chain_id, f, m);
-  uint32_t r[8], s[8], v[8];
-  uint32_t fl = VF_DECODE_ERR;
-  if (ok) {
-    uint8_t b[32];
-    fl = 0;
-    fl |= rlp_to_be32(p, f[7], b) ? 0u : 1u;  // EGES_VF_V_WIDE
-    limbs_from_be32(v, b);
-    fl |= rlp_to_be32(p, f[8], b) ? 0u : 2u;  // EGES_VF_R_WIDE
-    limbs_from_be32(r, b);
-    fl |= rlp_to_be32(p, f[9], b) ? 0u : 4u;  // EGES_VF_S_WIDE
-    limbs_from_be32(s, b);
-  } else {  // (no sponge for it: wave S skips undecodable items)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) r[k] = s[k] = v[k] = 0;
-  }
-  q.meta = sender_meta(r, s, v, fl, prm.wire_signer, prm.wire_chain_id);
-  q.recid = q.meta & 3u;
-  q.ok = ((q.meta >> 8) & 0xffu) == ST_OK;
-  bool ovr, ovs;
-  q.R = sc_from_limbs(r, ovr);
-  q.Sv = sc_from_limbs(s, ovs);
-  q.ok = q.ok && !ovr && !ovs && !sc_is_zero(q.R) && !sc_is_zero(q.Sv);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) q.xr[i] = q.R.v[i];  // recid < 2 on this path: x = r
+  wire_item(p, len, span_ok, prm.wire_signer, prm.wire_chain_id, q, m);
 }
 
 __device__ __attribute__((noinline)) void wire_sighash(const Payload& m, uint8_t* h) { keccak256_payload(m, h); }

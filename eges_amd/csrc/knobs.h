@@ -15,7 +15,8 @@ enum KnobId : int {
   KNOB_MID_MAX,           // batches above LAT_MAX and at most this many take the mid-size kernel
   KNOB_MID_FORM,          // mid-size kernel: 1 auto (bucket form while the grid fits one workgroup
                           //   per CU, windowed beyond), 0 windowed form, 2 bucket form
-  KNOB_WIRE_FUSED,        // wire-format batches on the bucket form decode inside the recover kernel
+  KNOB_WIRE_FUSED,        // wire-format batches decode inside the recover kernel: 1 latency kernels and
+                          //   bucket form, 2 bucket form only, 0 neither
   KNOB_TXROWS_WAVE_MAX,   // wire-format batches of at most this many decode one tx per wave
   KNOB_ROOT_HELPERS,      // 0: the narrow form launches no root-helper workgroups (tests)
   KNOB_OVERLAP,           // device-resident recover batches as S overlapped launches (-1 = auto)

@@ -4,6 +4,7 @@
 // the C call get their Go error as status; the rest become ecrecover records with recid = v.
 // Shared by prep_sender_kernel (k_prep.hip) and the fused wire-format mid-size kernel.
 #include "core.cuh"
+#include "rlp.cuh"
 
 namespace eges {
 
@@ -95,6 +96,42 @@ DEV uint32_t sender_meta(const uint32_t r[8], const uint32_t s[8], const uint32_
     }
   }
   return recid | (status << 8);
+}
+
+// One wire-format transaction p[0, len) (span_ok: its offsets were consistent) -> the record
+// lat_parse builds from rows (R, S, meta = recid | status << 8, R's x; z is left to the caller,
+// who hashes m, the signing payload) — tx_rows_kernel's decode and prep_sender_kernel's
+// classification in one: the fused wire paths of the mid-size and latency kernels. Returns
+// whether the transaction decoded (m is valid only then).
+DEV bool wire_item(const uint8_t* p, uint64_t len, bool span_ok, int signer, uint64_t chain_id, LatParse& q,
+                   Payload& m) {
+  RlpHead f[10]{};
+  const bool ok = span_ok && tx_parse(p, len, signer, chain_id, f, m);
+  uint32_t r[8], s[8], v[8];
+  uint32_t fl = VF_DECODE_ERR;
+  if (ok) {
+    uint8_t b[32];
+    fl = 0;
+    fl |= rlp_to_be32(p, f[7], b) ? 0u : 1u;  // EGES_VF_V_WIDE
+    limbs_from_be32(v, b);
+    fl |= rlp_to_be32(p, f[8], b) ? 0u : 2u;  // EGES_VF_R_WIDE
+    limbs_from_be32(r, b);
+    fl |= rlp_to_be32(p, f[9], b) ? 0u : 4u;  // EGES_VF_S_WIDE
+    limbs_from_be32(s, b);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] = s[k] = v[k] = 0;
+  }
+  q.meta = sender_meta(r, s, v, fl, signer, chain_id);
+  q.recid = q.meta & 3u;
+  q.ok = ((q.meta >> 8) & 0xffu) == ST_OK;
+  bool ovr, ovs;
+  q.R = sc_from_limbs(r, ovr);
+  q.Sv = sc_from_limbs(s, ovs);
+  q.ok = q.ok && !ovr && !ovs && !sc_is_zero(q.R) && !sc_is_zero(q.Sv);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q.xr[i] = q.R.v[i];  // recid < 2 on this path: x = r
+  return ok;
 }
 
 }  // namespace eges

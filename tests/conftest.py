@@ -30,13 +30,15 @@ def oracle():
     return Oracle()
 
 
-# Wire-format sender paths (eges_sender_raw_batch / _dev, eges_block_senders_raw): the default
-# dispatch (small batches: tx_rows + prep_sender + the latency kernels) and the fused form, where
-# the mid-size kernel's bucket form decodes, hashes and classifies the encodings itself
-# (k_recover_mid.hip wire_stage / wire_parse), forced for every batch size with engine knobs.
+# Wire-format sender paths (eges_sender_raw_batch / _dev, eges_block_senders_raw): separate
+# tx_rows + prep_sender launches before the recovery (EGES_WIRE_FUSED = 0), and the fused forms,
+# where the recovery kernel decodes, hashes and classifies the encodings itself — the mid-size
+# kernel's bucket form (k_recover_mid.hip wire_stage / wire_parse) or the latency kernels
+# (k_recover_lat.hip, narrow and split), each forced for every batch size with engine knobs.
 WIRE_FORMS = {
-    "tx_rows": {},
+    "tx_rows": {"EGES_WIRE_FUSED": 0},
     "fused": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2, "EGES_WIRE_FUSED": 1},
+    "fused_lat": {"EGES_LAT_MAX": 1 << 20, "EGES_WIRE_FUSED": 1},
 }
 
 
