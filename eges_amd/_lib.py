@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libeges.so")
+# EGES_LIB: another build of the library in this directory (same-box A/B runs); default libeges.so
+LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ.get("EGES_LIB", "libeges.so")))
 
 # include/eges.h
 EGES_OK = 0

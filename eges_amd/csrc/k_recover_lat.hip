@@ -612,6 +612,14 @@ DEV void root_fetch(const RecoverParams& prm, uint32_t idx, const fr& c, bool od
   if (lane_id() == 0) S.yok = ok ? 1u : 0u;
 }
 
+// diagnostic build: where this wave runs, XCC_ID << 16 | HW_ID[15:0] (wave slot, SIMD, CU, SH, SE)
+DEV uint32_t hw_place() {
+  uint32_t hw, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  return (xcc & 0xfu) << 16 | (hw & 0xffffu);
+}
+
 // Phase marks of wave 0 (diagnostic build only): 0 parse + x, c, 3 table, 1 wait for wave 1's
 // r^-1 / u1 / u2 / digits, 4 Strauss + join (including the waits for the other parts and y),
 // 5 Z^-1 + affine, 6 Keccak + stores.
@@ -689,7 +697,7 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
       recode_digits<SPLIT>(u2, u1, S);
     }
     if (stamped && lane_id() == 0) {
-      S.w1t[0] = t1 - t0;
+      S.w1t[0] = (t1 - t0) | ((uint64_t)hw_place() << 32);
       S.w1t[1] = __builtin_amdgcn_s_memtime() - t1;
     }
     if (SPLIT) {
@@ -756,8 +764,10 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
     st_.acc[2] = mprof[0];
     st_.acc[7] = mprof[1];
 #else
-    st_.acc[2] = S.w1t[0];  // wave 1's phases in the unused slots (not part of wave 0's total)
-    st_.acc[7] = S.w1t[1];
+    // wave 1's phases in the unused slots (not part of wave 0's total); the high words carry
+    // where wave 1 (slot 2) and wave 0 (slot 7) ran (hw_place)
+    st_.acc[2] = S.w1t[0];
+    st_.acc[7] = S.w1t[1] | ((uint64_t)hw_place() << 32);
 #endif
     if (lane_id() == 0) {
 #pragma unroll

@@ -55,7 +55,13 @@ buf = (ctypes.c_uint64 * (waves * 8))()
 lib.eges_diag_read_stamps(buf, waves)
 import numpy as np  # noqa: E402
 
-a = np.frombuffer(buf, dtype=np.uint64).reshape(waves, 8).astype(np.float64)
+raw = np.frombuffer(buf, dtype=np.uint64).reshape(waves, 8)
+place = None
+if LAT:  # slots 2 / 7 carry wave 1's / wave 0's hw_place in their high words (k_recover_lat.hip)
+    place = (raw[:, [2, 7]] >> np.uint64(32)).astype(np.int64)
+    raw = raw.copy()
+    raw[:, [2, 7]] &= np.uint64(0xFFFFFFFF)
+a = raw.astype(np.float64)
 tot = (a.sum(axis=1) - a[:, 2] - a[:, 7]) if LAT else a.sum(axis=1)
 print(f"n={n} launch {dt * 1e3:.2f} ms ({n / dt / 1e6:.2f} M sigs/s, stamped build), waves={waves}")
 print(f"per-wave total: mean {tot.mean():.4g} min {tot.min():.4g} max {tot.max():.4g} (s_memtime ticks)")
@@ -63,3 +69,25 @@ tiles_per_wave = max(n / 256 / (waves / 4), 1e-9)
 for i in range(8 if LAT else 7):
     m = a[:, i].mean()
     print(f"  {PHASES[i]:18s} {m:12.4g} ticks/wave  {100 * m / tot.mean():5.1f}%  {m / tiles_per_wave:10.4g}/tile")
+
+if place is not None and place.any():
+    # SIMD sharing: key = (XCC, SE, SH, CU, SIMD); wave 0 is the heavy chain, wave 1 the scalar one
+    def key(h):
+        return (h >> 16, (h >> 13) & 7, (h >> 12) & 1, (h >> 8) & 15, (h >> 4) & 3)
+    from collections import Counter
+    heavy = Counter(key(int(h)) for h in place[:, 1])
+    light = Counter(key(int(h)) for h in place[:, 0])
+    cus = Counter(key(int(h))[:4] for h in place[:, 1])
+    print(f"placement: {len(cus)} CUs, {len(heavy)} SIMDs with a wave 0; signatures per CU "
+          f"{sorted(Counter(cus.values()).items())}; same-SIMD wave 0 / wave 1 pairs "
+          f"{sum(key(int(p0)) == key(int(p1)) for p1, p0 in place)}")
+    groups = {}
+    for i, (p1, p0) in enumerate(place):
+        k = key(int(p0))
+        groups.setdefault((heavy[k], light.get(k, 0)), []).append(i)
+    for (h, l), ix in sorted(groups.items()):
+        print(f"  SIMD with {h} wave-0s and {l} wave-1s: {len(ix):5d} signatures, Strauss {a[ix, 4].mean():.4g}, "
+              f"total {tot[ix].mean():.4g} ticks")
+    sims = Counter(int(h) >> 4 & 3 for h in place[:, 1])
+    print(f"  wave 0 SIMD ids {sorted(sims.items())}; wave 1 SIMD ids "
+          f"{sorted(Counter(int(h) >> 4 & 3 for h in place[:, 0]).items())}")
