@@ -164,6 +164,13 @@ DEV fr fr_reduce(uint64_t col, uint64_t tail) {
   return fr{low9(((uint32_t)z & M29) + shr<1>(e + zc))};
 }
 
+// a * b on top of a per-lane column preset (quad steps whose rows subtract different values)
+DEV fr fr_mul_col(fr a, fr b, uint64_t col) {
+  uint64_t tail;
+  fr_cols(col, tail, a, b);
+  return fr_reduce(col, tail);
+}
+
 DEV fr fr_mul(fr a, fr b) {
   uint64_t col = 0, tail;
   fr_cols(col, tail, a, b);

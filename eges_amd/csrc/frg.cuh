@@ -10,6 +10,8 @@
 //   mixed addition  8M + 3S in 5 quad steps  {Z1^2, y2 Z1} {U2 - X1, S2 - Y1} {H^2, Z1 H, R^2}
 //                                            {H I, X1 I} {R2 (V - X3), Y1 J}   (+1 for ZINV)
 //   co-Z addition   4M + 2S in 4 quad steps
+//   mixed addition after a doubling or a mixed addition: 3 quad steps (gejq_double_pre /
+//   gejq_add_pre: its first two levels run in the previous operation's idle rows)
 // where a lane-serial kernel pays one product after another.
 #include "fr.cuh"
 
@@ -67,6 +69,65 @@ DEV gejr gejq_add_ge_t(const gejr& a, const ger& b, const fr* bzinv, bool& h_zer
   fr_mul2(W, YJ, R2, fr_sub<1>(V, r.x), a.y, J);
   r.y = fr_normalize_weak(fr_sub<2>(W, fr_add(YJ, YJ)));             // R2 (V - X3) - 2 Y1 J
   r.z = fr_add(zh, zh);                                               // 2 Z1 H
+  return r;
+}
+
+// ---- hoisted mixed additions (the latency kernels' Strauss windows). A doubling's last level
+// has one product and a mixed addition's last two have two or three, so three rows idle. The
+// first two levels of the next mixed addition (Z1^2, then H = x2 Z1^2 - X1 and Z1^3) depend only
+// on the operation's Z3, X3 and the next point's x, so they run in those idle rows: a mixed
+// addition after a doubling or after another mixed addition costs 3 quad levels instead of 5.
+struct AddPre {
+  fr h, z13;  // H = x2 Z1^2 - X1 (m1), Z1^3 (m1) of the addition that follows
+};
+
+// gejq_double, with the start of the mixed addition of a point with x = x2 to the result
+DEV gejr gejq_double_pre(const gejr& a, const fr& x2, AddPre& pre) {
+  fr A, B, YZ;
+  fr_mul3(A, B, YZ, a.x, a.x, a.y, a.y, a.y, a.z);
+  const fr E = fr_normalize_weak(fr_add(fr_add(A, A), A));  // 3 X^2
+  const fr XB = fr_add(a.x, B);
+  gejr r;
+  r.z = fr_add(YZ, YZ);                                             // 2 Y Z, m2
+  fr C, T, F, ZZ;
+  fr_mul4(C, T, F, ZZ, B, B, XB, XB, E, E, r.z, r.z);
+  const fr D = fr_normalize_weak(fr_sub<2>(T, fr_add(A, C)));       // 2 X Y^2
+  r.x = fr_normalize_weak(fr_sub<3>(F, fr_mul_small(D, 4)));        // E^2 - 4D
+  // row 0: E (2D - X3) - 8C (gejq_double's Y3); row 1: x2 Z3^2 - X3; row 2: Z3^3
+  const uint32_t p32 = rowsel(kconst<1>() - C.v, kconst<1>() - r.x.v, 0u, 0u);
+  const uint64_t col = (uint64_t)p32 << (row_id() == 0 ? 3 : 0);
+  fr u;
+  rep4(fr_mul_col(rowsel(E, x2, r.z, r.z), rowsel(fr_sub<1>(fr_add(D, D), r.x), ZZ, ZZ, ZZ), col), r.y, pre.h,
+       pre.z13, u);
+  return r;
+}
+
+// a + b (gejq_add_ge_t<ADD_PLAIN, false>'s values) from its hoisted start pre. NEXT: the idle rows
+// also start the mixed addition of a point with x = x2n to the result (into nxt).
+template <bool NEXT>
+DEV gejr gejq_add_pre(const gejr& a, const ger& b, const AddPre& pre, const fr& x2n, AddPre& nxt) {
+  // R = y2 Z1^3 - Y1 (row 0), H^2, Z1 H
+  const uint64_t c1 = (uint64_t)rowsel(kconst<2>() - a.y.v, 0u, 0u, 0u);
+  fr R, HH, zh, u;
+  rep4(fr_mul_col(rowsel(b.y, pre.h, a.z, a.z), rowsel(pre.z13, pre.h, pre.h, pre.h), c1), R, HH, zh, u);
+  const fr HH2 = fr_add(HH, HH);
+  const fr I = fr_add(HH2, HH2);                                      // 4 HH, m4
+  gejr r;
+  r.z = fr_add(zh, zh);                                               // 2 Z1 H, m2
+  fr RR, J, V, ZZ;
+  if (NEXT) fr_mul4(RR, J, V, ZZ, R, R, pre.h, I, a.x, I, r.z, r.z);
+  else fr_mul3(RR, J, V, R, R, pre.h, I, a.x, I);
+  const fr R2sq = fr_normalize_weak(fr_mul_small(RR, 4));            // (2R)^2
+  r.x = fr_normalize_weak(fr_sub<2>(R2sq, fr_add(J, fr_add(V, V))));  // R2^2 - J - 2V
+  const fr R2 = fr_add(R, R);
+  fr W, YJ;
+  if (NEXT) {  // rows 2, 3: x2n Z3^2 - X3, Z3^3
+    const uint64_t c3 = (uint64_t)rowsel(0u, 0u, kconst<1>() - r.x.v, 0u);
+    rep4(fr_mul_col(rowsel(R2, a.y, x2n, r.z), rowsel(fr_sub<1>(V, r.x), J, ZZ, ZZ), c3), W, YJ, nxt.h, nxt.z13);
+  } else {
+    fr_mul2(W, YJ, R2, fr_sub<1>(V, r.x), a.y, J);
+  }
+  r.y = fr_normalize_weak(fr_sub<2>(W, fr_add(YJ, YJ)));             // R2 (V - X3) - 2 Y1 J
   return r;
 }
 

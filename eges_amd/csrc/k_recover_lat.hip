@@ -37,6 +37,9 @@ namespace eges {
 
 // One signature per workgroup of two waves (narrow form); the split form has four (LAT_WG_SPLIT).
 constexpr int LAT_WG = 128;
+#ifndef EGES_LAT_HOIST
+#define EGES_LAT_HOIST 1  // hoisted additions in the Strauss windows (strauss_win_fast); 0: plain steps
+#endif
 constexpr int LAT_STAGE = 512;  // wire form: encodings up to this size decode out of LDS
 // Split form: windows [0, SPLIT_W0) of both GLV halves against the R' table on wave 0, windows
 // [SPLIT_W0, RWIN) against a table of D = 2^(RBITS SPLIT_W0) R' on waves 2 (R) and 3 (lambda R).
@@ -348,10 +351,66 @@ DEV void strauss_win(gejr& acc, bool& inf, const TabT<NT>& tab, const ColT<NT>& 
     }
   }
 }
+// window point +-T[|d| - 1] of half j (j = 1: lambda, (beta x, y)); d != 0
+template <int NT>
+DEV ger win_point(const TabT<NT>& tab, const ColT<NT>& btab, int d, int j) {
+  const int e = (d < 0 ? -d : d) - 1;
+  ger p = lds_pt(tab[e]);
+  if (j == 1) p.x.v = btab[e][row_lane()];
+  return ger_neg_if(p, d < 0);
+}
+// strauss_win<false>'s sums with hoisted additions (frg.cuh gejq_double_pre / gejq_add_pre): each
+// window's last doubling starts its first addition and that addition starts the second, so a
+// window of BITS doublings and two additions is 3 BITS + 6 quad levels instead of 3 BITS + 10.
+// Zero digits are skipped (wave-uniform); windows that start at infinity (the top one, or while
+// every digit so far was zero) take the plain steps.
+template <int BITS, int NT>
+DEV void strauss_win_fast(gejr& acc, bool& inf, const TabT<NT>& tab, const ColT<NT>& btab, const int8_t* d0,
+                          const int8_t* d1, int jmask, int wlo, int whi, const Diag& dg) {
+  inf = true;
+  acc.x = fr_zero();
+  acc.y = fr_zero();
+  acc.z = fr_zero();
+#pragma unroll 1
+  for (int w = whi - 1; w >= wlo; --w) {
+    const int da = (jmask & 1) ? (int)d0[w] : 0;
+    const int db = (jmask & 2) ? (int)d1[w] : 0;
+    if (inf) {
+      if (w != whi - 1) {
+#pragma unroll 1
+        for (int k = 0; k < BITS; ++k) acc = gejq_double(acc);
+      }
+      if (da) add_r<false>(acc, inf, win_point(tab, btab, da, 0), true, dg);
+      if (db) add_r<false>(acc, inf, win_point(tab, btab, db, 1), true, dg);
+      continue;
+    }
+#pragma unroll 1
+    for (int k = 0; k < BITS - 1; ++k) acc = gejq_double(acc);
+    if (!da && !db) {
+      acc = gejq_double(acc);
+      continue;
+    }
+    const ger first = da ? win_point(tab, btab, da, 0) : win_point(tab, btab, db, 1);
+    AddPre pre;
+    acc = gejq_double_pre(acc, first.x, pre);
+    if (da && db) {
+      const ger second = win_point(tab, btab, db, 1);
+      AddPre pre2;
+      acc = gejq_add_pre<true>(acc, first, pre, second.x, pre2);
+      acc = gejq_add_pre<false>(acc, second, pre2, second.x, pre2);
+    } else {
+      acc = gejq_add_pre<false>(acc, first, pre, first.x, pre);
+    }
+  }
+}
 template <int BITS, int NT>
 DEV void strauss_win_exact(gejr& acc, bool& inf, const TabT<NT>& tab, const ColT<NT>& btab, const int8_t* d0,
                            const int8_t* d1, int jmask, int wlo, int whi, const Diag& dg) {
+#if EGES_LAT_HOIST
+  strauss_win_fast<BITS, NT>(acc, inf, tab, btab, d0, d1, jmask, wlo, whi, dg);
+#else
   strauss_win<false, BITS, NT>(acc, inf, tab, btab, d0, d1, jmask, wlo, whi, dg);
+#endif
   if (dg.force || __any(!inf && fr_is_zero(acc.z))) {
     diag_bump(dg, EGES_DIAG_LAT_REDO);
     strauss_win<true, BITS, NT>(acc, inf, tab, btab, d0, d1, jmask, wlo, whi, dg);
