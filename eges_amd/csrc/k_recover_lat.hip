@@ -206,11 +206,6 @@ DEV void recode_g(const sc& u_g, LatLds& S) {
 #pragma unroll
   for (int k = 0; k < CWIN; ++k) S.cdig[k] = (uint16_t)(u_g.v[k >> 1] >> (16 * (k & 1)));
 }
-template <bool SPLIT>
-DEV void recode_digits(const sc& u_r, const sc& u_g, LatLds& S) {
-  recode_r<SPLIT>(u_r, S);
-  recode_g(u_g, S);
-}
 
 // ---- wire form (RecoverParams::wire_*): the transaction's encoding instead of record rows.
 // Item idx's bytes [a, e) relative to wire_raw.
@@ -430,10 +425,54 @@ DEV void strauss_gcomb(gejr& acc, bool& inf, const LatLds& S, const uint32_t* gc
     add_r<CHECKED>(acc, inf, p, d != 0, dg);
   }
 }
+// strauss_gcomb<false>'s sum with hoisted additions (frg.cuh gejq_add_pre): the first nonzero
+// digit's point starts the sum, every later addition is 3 quad levels and starts the next one.
+DEV ger gcomb_pt(const uint32_t* gcomb, int k, int d) {
+  return gtab_pt(gcomb + ((size_t)k * CTAB + (d > 0 ? d - 1 : 0)) * PT_WORDS);
+}
+DEV void strauss_gcomb_fast(gejr& acc, bool& inf, const LatLds& S, const uint32_t* gcomb) {
+  int k = 0;
+  while (k < CWIN && S.cdig[k] == 0) ++k;
+  inf = k == CWIN;
+  acc.x = fr_zero();
+  acc.y = fr_zero();
+  acc.z = fr_zero();
+  if (inf) return;
+  const ger p0 = gcomb_pt(gcomb, k, S.cdig[k]);
+  acc.x = p0.x;
+  acc.y = p0.y;
+  acc.z = fr_one();
+  int kn = k + 1;
+  while (kn < CWIN && S.cdig[kn] == 0) ++kn;
+  if (kn == CWIN) return;
+  ger p = gcomb_pt(gcomb, kn, S.cdig[kn]);
+  AddPre pre;  // acc is affine: H = x2 - X1, Z1^3 = 1
+  pre.h = fr_normalize_weak(fr_sub<1>(p.x, acc.x));
+  pre.z13 = fr_one();
+#pragma unroll 1
+  for (;;) {
+    int kk = kn + 1;
+    while (kk < CWIN && S.cdig[kk] == 0) ++kk;
+    if (kk == CWIN) {
+      acc = gejq_add_pre<false>(acc, p, pre, p.x, pre);
+      return;
+    }
+    const ger q = gcomb_pt(gcomb, kk, S.cdig[kk]);
+    AddPre nxt;
+    acc = gejq_add_pre<true>(acc, p, pre, q.x, nxt);
+    p = q;
+    pre = nxt;
+    kn = kk;
+  }
+}
 // u_g G, unchecked, with the exact redo (every digit is nonzero-checked, so a poisoned sum
 // shows as Z == 0 and not infinity)
 DEV void gcomb_exact(gejr& A, bool& ainf, const LatLds& S, const uint32_t* gcomb, const Diag& dg) {
+#if EGES_LAT_HOIST
+  strauss_gcomb_fast(A, ainf, S, gcomb);
+#else
   strauss_gcomb<false>(A, ainf, S, gcomb, dg);
+#endif
   if (dg.force || __any(!ainf && fr_is_zero(A.z))) {
     diag_bump(dg, EGES_DIAG_COMB_REDO);
     strauss_gcomb<true>(A, ainf, S, gcomb, dg);
@@ -752,20 +791,17 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
       uint8_t* hs = prm.wire_sighash ? prm.wire_sighash + (size_t)idx * 32 : nullptr;
       recode_g(sc_neg(sc_mul(rinv, wire_sighash_wave(m, decoded, hs))), S);
     } else {
-      const sc u1 = sc_neg(sc_mul(rinv, Z));
-      recode_digits<SPLIT>(u2, u1, S);
+      recode_r<SPLIT>(u2, S);  // the R digits first: wave 0 is waiting for them
+      if (SPLIT) flag_set(&S.flag[F_DIG]);
+      else __syncthreads();  // digits ready (and the table)
+      recode_g(sc_neg(sc_mul(rinv, Z)), S);  // u1 = -z / r, for this wave's comb
     }
     if (stamped && lane_id() == 0) {
       S.w1t[0] = (t1 - t0) | ((uint64_t)hw_place() << 32);
       S.w1t[1] = __builtin_amdgcn_s_memtime() - t1;
     }
-    if (SPLIT) {
-      if (!wire) flag_set(&S.flag[F_DIG]);
-      helper_split(S, gcomb, true, c, odd, fr_zero(), dg);
-    } else {
-      if (!wire) __syncthreads();  // digits ready (and the table)
-      helper_wave(S, gcomb, false, c, odd, fr_zero(), dg);  // y: the helper workgroups (root_fetch)
-    }
+    if (SPLIT) helper_split(S, gcomb, true, c, odd, fr_zero(), dg);
+    else helper_wave(S, gcomb, false, c, odd, fr_zero(), dg);  // y: the helper workgroups (root_fetch)
     return;
   }
   if (SPLIT && (wv == 2 || wv == 3)) {
@@ -887,17 +923,14 @@ DEV void verify_lat_body(const VerifyParams& prm) {
   const uint32_t wv = threadIdx.x >> 6;
   if (wv == 1) {
     const sc sinv = sc_inv_row_var(sc_select(sig_ok, Sv, sc_one()));
-    const sc u1 = sc_mul(sinv, Z);
     const sc u2 = sc_select(sig_ok, sc_mul(sinv, R), sc_one());
-    recode_digits<SPLIT>(u2, u1, S);
+    recode_r<SPLIT>(u2, S);  // the key's digits first: wave 0 is waiting for them
+    if (SPLIT) flag_set(&S.flag[F_DIG]);
+    else __syncthreads();  // digits ready (and the table)
+    recode_g(sc_mul(sinv, Z), S);  // u1 = z / s
     // the square root only for 33-byte keys; 65-byte keys give y
-    if (SPLIT) {
-      flag_set(&S.flag[F_DIG]);
-      helper_split(S, gcomb, c33, c, pfx == 3, Y, dg);
-    } else {
-      __syncthreads();  // digits ready (and the table)
-      helper_wave(S, gcomb, c33, c, pfx == 3, Y, dg);
-    }
+    if (SPLIT) helper_split(S, gcomb, c33, c, pfx == 3, Y, dg);
+    else helper_wave(S, gcomb, c33, c, pfx == 3, Y, dg);
     return;
   }
   if (SPLIT && (wv == 2 || wv == 3)) {
