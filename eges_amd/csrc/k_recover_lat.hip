@@ -60,10 +60,12 @@ enum { F_DIG = 0, F_Y, F_G, F_LHI, F_HI, NFLAGS };
 
 struct LatLds {
   uint32_t tab[PTAB][2][16];  // {1..16} * R' (x, y), row form (all four rows read the same words)
-  uint32_t zr[PTAB][16];      // Z ratios while the table is built
+  uint32_t zr[PTAB][16];      // Z ratios while the table is built (then their cubes)
+  uint32_t zq[PTAB][16];      //   and their squares
   uint32_t btab[PTAB][16];    // beta x of the table entries (the lambda R' additions)
   uint32_t dtab[2][HTAB][2][16];  // split form: {1..8} * D, one copy per high-part wave
   uint32_t dzr[2][HTAB][16];
+  uint32_t dzq[2][HTAB][16];
   uint32_t dbtab[HTAB][16];       //   and beta x for the lambda half (wave 3)
   int8_t rdig[2][RWIN];       // R / lambda R window digits
   int8_t hdig[2][HWIN];       // split form: the high parts in 4-bit windows
@@ -270,48 +272,76 @@ using ColT = uint32_t[NT][16];
 // P may be the (X, Y) of a Jacobian point: the formulas do not involve the curve's b, so the
 // entries are then points of the curve y^2 = x^3 + b Z^6 on which (X, Y) is affine.
 template <int NT>
-DEV fr build_table_wave(const ger& P, TabT<NT>& tab, ColT<NT>& zrs) {
-  fr zeta;
-  {
-    const uint32_t L = row_lane();
-    lds_put_pt(tab[0], P);
-    gejr D;
-    ger B;
-    gejq_dblu(D, B, P);
-    zrs[0][L] = D.z.v;  // Z_2 / Z_1 = 2y
-    ger T;
-    T.x = D.x;
-    T.y = D.y;
-    lds_put_pt(tab[1], T);
+DEV fr build_table_wave(const ger& P, TabT<NT>& tab, ColT<NT>& zrs, ColT<NT>& zq2) {
+  static_assert(NT >= 3, "co-Z chain");
+  const uint32_t L = row_lane();
+  lds_put_pt(tab[0], P);
+  gejr D;
+  ger B;
+  gejq_dblu(D, B, P);
+  zrs[0][L] = D.z.v;  // Z_2 / Z_1 = 2y
+  ger T;
+  T.x = D.x;
+  T.y = D.y;
+  lds_put_pt(tab[1], T);
+  // co-Z additions T += B (gejq_zaddu's values), two quad levels each: the level that forms
+  // E = B.y (C - B.x') and T.y also squares the next step's dx = T.x' - B.x', and the next
+  // step's dy^2 shares a level with its B.x A, T.x A products. The spare rows square every Z
+  // ratio (zq2) and run the product of all of them (zeta, the table's global Z).
+  fr dx = fr_normalize_weak(fr_sub<1>(T.x, B.x));
+  fr dy = fr_normalize_weak(fr_sub<1>(T.y, B.y));
+  fr A, dy2, Bn, C, q, zp;
+  fr_mul3(A, dy2, q, dx, dx, dy, dy, D.z, D.z);
+  zq2[0][L] = q.v;
+  fr_mul3(Bn, C, zp, B.x, A, T.x, A, D.z, dx);
 #pragma unroll 1
-    for (int i = 2; i < NT; ++i) {
-      const fr zr = gejq_zaddu(T, B);  // T = (i+1) P
-      lds_put_pt(tab[i], T);
-      zrs[i - 1][L] = zr.v;
-    }
-    // entry i (< NT - 1) is rescaled by rho_i = prod_{k=i}^{NT-2} Z_{k+2}/Z_{k+1} = Z_NT / Z_{i+1}:
-    // x rho^2, y rho^3, software-pipelined two quad steps per entry
-    fr rho{zrs[NT - 2][L]};
-    fr s2 = fr_sqr(rho);
-#pragma unroll 1
-    for (int i = NT - 2; i >= 0; --i) {
-      const ger J = lds_pt(tab[i]);
-      const fr zn{zrs[i > 0 ? i - 1 : 0][L]};
-      fr ax, s3, rho_n;
-      fr_mul3(ax, s3, rho_n, J.x, s2, s2, rho, rho, zn);   // x rho^2, rho^3, next rho
-      fr ay, s2_n;
-      fr_mul2(ay, s2_n, J.y, s3, rho_n, rho_n);            // y rho^3, next rho^2
-      ger a;
-      a.x = ax;
-      a.y = ay;
-      lds_put_pt(tab[i], a);
-      if (i == 0) break;
-      rho = rho_n;
-      s2 = s2_n;
-    }
-    zeta = rho;  // rho_0 = Z_NT / Z_1 with Z_1 = 1
+  for (int i = 2; i < NT; ++i) {  // T = (i+1) P; this step's Z ratio is dx
+    const fr tx = fr_normalize_weak(fr_sub<2>(dy2, fr_add(Bn, C)));
+    const fr dxn = fr_normalize_weak(fr_sub<1>(tx, Bn));
+    fr E, Pd, An;
+    fr_mul4(E, Pd, An, q, B.y, fr_sub<1>(C, Bn), dy, fr_sub<1>(Bn, tx), dxn, dxn, dx, dx);
+    T.x = tx;
+    T.y = fr_normalize_weak(fr_sub<1>(Pd, E));  // dy (B.x' - T.x') - E
+    B.x = Bn;
+    B.y = E;
+    lds_put_pt(tab[i], T);
+    zrs[i - 1][L] = dx.v;
+    zq2[i - 1][L] = q.v;
+    if (i == NT - 1) break;
+    dx = dxn;
+    dy = fr_normalize_weak(fr_sub<1>(T.y, B.y));
+    A = An;
+    fr_mul4(dy2, Bn, C, zp, dy, dy, B.x, A, T.x, A, zp, dx);
   }
-  return zeta;
+  // entry i (< NT - 1) is rescaled by rho_i = prod_{k=i}^{NT-2} Z_{k+2}/Z_{k+1} = Z_NT / Z_{i+1}:
+  // x rho^2, y rho^3. The cubes of the ratios first (four per quad step, over zrs), then one
+  // quad step per entry: x rho_i^2, y rho_i^3, rho_(i-1)^2 = rho_i^2 z^2, rho_(i-1)^3 = rho_i^3 z^3.
+#pragma unroll 1
+  for (int k = 0; k < NT - 1; k += 4) {
+    const int k1 = k + 1 < NT - 1 ? k + 1 : k, k2 = k + 2 < NT - 1 ? k + 2 : k, k3 = k + 3 < NT - 1 ? k + 3 : k;
+    fr c0, c1, c2, c3;
+    fr_mul4(c0, c1, c2, c3, fr{zrs[k][L]}, fr{zq2[k][L]}, fr{zrs[k1][L]}, fr{zq2[k1][L]}, fr{zrs[k2][L]},
+            fr{zq2[k2][L]}, fr{zrs[k3][L]}, fr{zq2[k3][L]});
+    zrs[k][L] = c0.v;
+    zrs[k1][L] = c1.v;
+    zrs[k2][L] = c2.v;
+    zrs[k3][L] = c3.v;
+  }
+  fr s2{zq2[NT - 2][L]}, s3{zrs[NT - 2][L]};
+#pragma unroll 1
+  for (int i = NT - 2; i >= 0; --i) {
+    const ger J = lds_pt(tab[i]);
+    const int n = i > 0 ? i - 1 : 0;
+    fr ax, ay, s2n, s3n;
+    fr_mul4(ax, ay, s2n, s3n, J.x, s2, J.y, s3, s2, fr{zq2[n][L]}, s3, fr{zrs[n][L]});
+    ger a;
+    a.x = ax;
+    a.y = ay;
+    lds_put_pt(tab[i], a);
+    s2 = s2n;
+    s3 = s3n;
+  }
+  return zp;  // rho_0 = Z_NT / Z_1 with Z_1 = 1
 }
 
 // ---- Strauss parts. R' = (c x, c^2) lives on E': y^2 = x^3 + 7 c^3 with c = x^3 + 7 (the image
@@ -574,7 +604,7 @@ DEV void high_wave(LatLds& S, const fr& x, const fr& c, int j, const Diag& dg) {
   ger Dp;
   Dp.x = D.x;
   Dp.y = D.y;
-  const fr zd = build_table_wave<HTAB>(Dp, S.dtab[j], S.dzr[j]);
+  const fr zd = build_table_wave<HTAB>(Dp, S.dtab[j], S.dzr[j], S.dzq[j]);
   if (j == 1) build_btab<HTAB>(S.dtab[1], S.dbtab);
   const fr scale = fr_mul(zd, D.z);
   flag_wait(&S.flag[F_DIG]);
@@ -612,7 +642,7 @@ DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& 
                          const RootSrc* root = nullptr) {
   ger Rp;
   fr_mul2(Rp.x, Rp.y, c, x, c, c);  // (c x, c^2)
-  const fr zeta = build_table_wave<PTAB>(Rp, S.tab, S.zr);
+  const fr zeta = build_table_wave<PTAB>(Rp, S.tab, S.zr, S.zq);
   build_btab<PTAB>(S.tab, S.btab);
   st->mark(3);
   if (SPLIT) flag_wait(&S.flag[F_DIG]);

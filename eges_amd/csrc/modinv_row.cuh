@@ -59,6 +59,11 @@ DEV int32_t divsteps_30_var_s(int32_t eta, uint32_t f0, uint32_t g0, trans2x2& t
   uint32_t u = 1, v = 0, q = 0, r = 1;
   uint32_t f = f0, g = g0;
   int i = 30;
+  // f^-1 mod 2^12 (Newton from 3 bits), recomputed only when f changes (the swaps)
+  uint32_t x = f;
+  x *= 2u - f * x;
+  x *= 2u - f * x;
+  uint32_t nx = 0u - x;
 #pragma unroll 1
   for (;;) {
     const int zeros = __builtin_ctz(g | (0xFFFFFFFFu << i));  // sentinel: at most i
@@ -77,15 +82,16 @@ DEV int32_t divsteps_30_var_s(int32_t eta, uint32_t f0, uint32_t g0, trans2x2& t
       g = 0u - tf;
       q = 0u - tu;
       r = 0u - tv;
+      x = f;
+      x *= 2u - f * x;
+      x *= 2u - f * x;
+      nx = 0u - x;
     }
     int limit = eta + 1 < i ? eta + 1 : i;
     asm volatile("" : "+s"(limit));  // s_min_i32, then s_min_i32 (no VALU min3)
     limit = limit < 12 ? limit : 12;
-    uint32_t x = f;   // f^-1 mod 2^3
-    x *= 2u - f * x;  // mod 2^6
-    x *= 2u - f * x;  // mod 2^12
     const uint32_t m = (0xFFFFFFFFu >> (32 - limit));
-    const uint32_t w = (g * (0u - x)) & m;
+    const uint32_t w = (g * nx) & m;
     g += f * w;
     q += u * w;
     r += v * w;
