@@ -25,3 +25,35 @@ def gather_shards(parts):
     import numpy as np
     parts = [np.asarray(p) for p in parts]
     return np.concatenate(parts, axis=0) if parts else np.zeros(0)
+
+
+RECORD = 21  # one item's result: 20-byte address + 1 status byte (eges_recover_* outputs)
+
+
+def all_gather_records(local, n, group=None):
+    """Optional exchange for consumers that want the whole batch's senders on every rank
+    (no reference analog — the Go node recovers on one host).
+
+    `local` is this rank's [hi - lo, 21] uint8 tensor of (address, status) records for its
+    shard_range(n, rank, world) slice, on the rank's device (RCCL over xGMI with the "nccl"
+    backend) or on the CPU (gloo). Every shard is padded to ceil(n / world) records so the
+    collective is one fixed-size all-gather; the result is the [n, 21] batch in index order on
+    every rank. It is outside the recovery path: bench.py's timed region never calls it.
+    """
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    lo, hi = shard_range(n, rank, world)
+    if local.dtype != torch.uint8 or local.dim() != 2 or local.shape != (hi - lo, RECORD):
+        raise ValueError(f"rank {rank}: expected uint8 [{hi - lo}, {RECORD}] records, got "
+                         f"{local.dtype} {tuple(local.shape)}")
+    per = -(-n // world) if n else 0
+    if per == 0:
+        return local.new_zeros((0, RECORD))
+    send = local.new_zeros((per, RECORD))
+    send[: hi - lo] = local
+    recv = [local.new_empty((per, RECORD)) for _ in range(world)]
+    dist.all_gather(recv, send, group=group)
+    rows = [recv[g][: shard_range(n, g, world)[1] - shard_range(n, g, world)[0]] for g in range(world)]
+    return torch.cat(rows, 0)

@@ -76,6 +76,52 @@ def test_gloo_two_ranks_gather_equals_single(n):
     assert np.array_equal(got, _item_work(range(n)))
 
 
+def _records(idx):
+    """[len(idx), 21] (address, status) records of the stand-in work, status = index mod 7."""
+    addr = _item_work(idx)
+    st = np.array([i % 7 for i in idx], np.uint8).reshape(-1, 1)
+    return np.concatenate([addr, st], 1) if len(addr) else np.zeros((0, 21), np.uint8)
+
+
+def _rank_all_gather(rank, world, port, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch
+    import torch.distributed as dist
+    from eges_amd.shard import all_gather_records
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard_range(n, rank, world)
+    got = all_gather_records(torch.from_numpy(_records(range(lo, hi))), n)
+    bad = 0
+    try:
+        all_gather_records(torch.zeros((hi - lo + 1, 21), dtype=torch.uint8), n)
+    except ValueError:
+        bad = 1
+    q.put((rank, got.numpy().copy(), bad))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [1001, 2, 1])
+def test_gloo_all_gather_records_every_rank(n):
+    """eges_amd.shard.all_gather_records (the optional exchange of SURVEY §8(e)): every rank
+    ends with the whole batch's records in index order, shards ragged or empty."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_all_gather, args=(r, 2, port, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    want = _records(range(n))
+    for rank, got, bad in outs:
+        assert got.shape == (n, 21) and np.array_equal(got, want), rank
+        assert bad == 1  # a shard of the wrong size is refused before the collective
+
+
 def _bench(args, env_extra=None, timeout=240):
     """bench.py as the driver runs it (no launcher: --gpus N starts torch.distributed.run itself)."""
     import json
