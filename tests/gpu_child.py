@@ -69,7 +69,35 @@ def logical_devices():
     return {"devices": ndev, "same_as_single": same, "correct": correct, "golden": golden}
 
 
+def allgather_nccl():
+    """eges_amd.shard.all_gather_records over the "nccl" backend (RCCL), world size 1: the
+    device-resident (address, status) records of a golden batch go through the collective and
+    come back equal (the exchange of SURVEY §8(e) on the real backend; N > 1 is gloo-tested)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import eges_amd
+    from eges_amd.shard import all_gather_records
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("EGES_TEST_PORT", "29541"),
+                      RANK="0", WORLD_SIZE="1")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    eges_amd.init(1)
+    n = 4099
+    msg, sig, pub, st = tiled_golden(n)
+    _, addr, sd = eges_amd.ecrecover_batch_dev(torch.from_numpy(msg).to(dev), torch.from_numpy(sig).to(dev))
+    rec = torch.cat([addr.reshape(n, 20), sd.reshape(n, 1).to(torch.uint8)], 1).contiguous()
+    got = all_gather_records(rec, n)
+    torch.cuda.synchronize()
+    ok = bool(got.device.type == "cuda" and torch.equal(got, rec)
+              and np.array_equal(got[:, 20].cpu().numpy(), st.astype(np.uint8)))
+    backend = dist.get_backend()
+    dist.destroy_process_group()
+    return {"ok": ok, "backend": backend}
+
+
 if __name__ == "__main__":
     mode = sys.argv[1]
-    out = {"small_grid": small_grid, "logical_devices": logical_devices}[mode]()
+    out = {"small_grid": small_grid, "logical_devices": logical_devices, "allgather_nccl": allgather_nccl}[mode]()
     print(json.dumps(out), flush=True)
