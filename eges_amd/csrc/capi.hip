@@ -141,6 +141,7 @@ const KnobDef KNOB_DEFS[KNOB_COUNT] = {
     {"EGES_COALESCE_GATHER_US", 20},
     {"EGES_COALESCE_SPIN_US", 2000},
     {"EGES_COALESCE_SPINNERS", 8},
+    {"EGES_TEST_SKIP_FLAG", 0},
 };
 std::atomic<long long> g_knob[KNOB_COUNT];
 std::once_flag g_knob_once;
@@ -160,14 +161,31 @@ int knob_index(const char* name) {
   return -1;
 }
 
-static int overlap_parts(size_t n) {
-  const long long v = knob(KNOB_OVERLAP);
-  if (v >= 0) return (int)std::min<long long>(v, 64);
+// The routing knobs of one call, read once at its start (a knob flipped while a call
+// runs must not send part of it one way and part another, e.g. a small-lane call onto the
+// windowed form's shared workspace).
+struct Route {
+  size_t lat_max = 0, mid_max = 0;
+  uint32_t wide_max = 0;
+  long long mid_form = 1, wire_fused = 1, overlap = -1;
+  uint32_t force_redo = 0, skip_flag = 0;
+  static Route now() {
+    Route r;
+    r.lat_max = (size_t)std::max<long long>(0, knob(KNOB_LAT_MAX));
+    r.mid_max = (size_t)std::max<long long>(0, knob(KNOB_MID_MAX));
+    r.wide_max = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_LAT_WIDE_MAX), 1u << 30));
+    r.mid_form = knob(KNOB_MID_FORM);
+    r.wire_fused = knob(KNOB_WIRE_FUSED);
+    r.overlap = knob(KNOB_OVERLAP);
+    r.force_redo = knob(KNOB_FORCE_REDO) != 0 ? 1u : 0u;
+    r.skip_flag = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TEST_SKIP_FLAG), 64));
+    return r;
+  }
+};
+static int overlap_parts(const Route& rt, size_t n) {
+  if (rt.overlap >= 0) return (int)std::min<long long>(rt.overlap, 64);
   return n > CHUNK ? 2 : 0;
 }
-static size_t lat_max() { return (size_t)std::max<long long>(0, knob(KNOB_LAT_MAX)); }
-static size_t mid_max() { return (size_t)std::max<long long>(0, knob(KNOB_MID_MAX)); }
-static uint32_t wide_max() { return (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_LAT_WIDE_MAX), 1u << 30)); }
 
 std::mutex g_mu;
 std::vector<DevPtr> g_devs;
@@ -317,11 +335,13 @@ struct Serial {
   ~Serial() { (void)hipEventRecord(d.last, st); }
 };
 
-// The device's diagnostic counters and the test-only redo knob, on every launch's parameters.
+// The device's diagnostic counters and the test-only knobs, on every launch's parameters.
 template <class P>
-P with_diag(const Dev& d, P p) {
+P with_diag(const Dev& d, P p, const Route& rt) {
   p.diag = d.diag;
-  p.force_redo = knob(KNOB_FORCE_REDO) != 0 ? 1u : 0u;
+  p.force_redo = rt.force_redo;
+  p.test_skip_flag = rt.skip_flag;
+  p.test_skip_block = 0;
   return p;
 }
 
@@ -350,37 +370,37 @@ size_t dev_ws_bytes(const Dev& d) { return ws_bytes_per_block() * (size_t)d.ws_b
 // The bucket form (k_recover_mid.hip) holds 138 KB of LDS: one workgroup per CU. It is the
 // faster form while the grid fits one generation (n <= 64 x CUs); beyond that the windowed form
 // (two workgroups per CU) is (tools/formcurve.py).
-bool mid_bucket(const Dev& d, size_t n) {
-  const long long f = knob(KNOB_MID_FORM);
+bool mid_bucket(const Dev& d, const Route& rt, size_t n) {
+  const long long f = rt.mid_form;
   if (f == 0) return false;
   if (f >= 2) return true;
   return (n + MID_SIGS_PER_BLOCK - 1) / MID_SIGS_PER_BLOCK <= (size_t)d.cus;
 }
-bool use_mid(const Dev& d, size_t n) {
-  if (n <= lat_max() || n > mid_max()) return false;
-  return mid_bucket(d, n) || (n + 63) / 64 * mid_ws_bytes_per_block() <= dev_ws_bytes(d);
+bool use_mid(const Dev& d, const Route& rt, size_t n) {
+  if (n <= rt.lat_max || n > rt.mid_max) return false;
+  return mid_bucket(d, rt, n) || (n + 63) / 64 * mid_ws_bytes_per_block() <= dev_ws_bytes(d);
 }
 // the recover kernels that parse msg / sig bytes themselves (no prep launch)
-bool fused_parse(const Dev& d, size_t n) { return n <= lat_max() || use_mid(d, n); }
+bool fused_parse(const Dev& d, const Route& rt, size_t n) { return n <= rt.lat_max || use_mid(d, rt, n); }
 
-hipError_t launch_recover_pass(Dev& d, const RecoverParams& p0, hipStream_t st) {
-  RecoverParams p = with_diag(d, p0);
+hipError_t launch_recover_pass(Dev& d, const Route& rt, const RecoverParams& p0, hipStream_t st) {
+  RecoverParams p = with_diag(d, p0, rt);
   // the split form (four waves per signature) while the batch leaves SIMDs idle
-  p.wide = p.n <= wide_max() ? 1u : 0u;
-  const bool mid = use_mid(d, p.n);
-  if (p.wire_raw && !(mid ? mid_bucket(d, p.n) : p.n <= lat_max())) return hipErrorInvalidValue;  // wire_fused() decides
+  p.wide = p.n <= rt.wide_max ? 1u : 0u;
+  const bool mid = use_mid(d, rt, p.n);
+  if (p.wire_raw && !(mid ? mid_bucket(d, rt, p.n) : p.n <= rt.lat_max)) return hipErrorInvalidValue;  // wire_fused() decides
 #ifdef EGES_PHASE_STAMPS
   if (mid) {
     hipError_t e = stamp_buf((p.n + 63) / 64 * 4, st);  // one row per wave
-    return e != hipSuccess ? e : launch_recover_mid_stamped(p, mid_bucket(d, p.n), dev_ws_bytes(d), st, g_stamps);
+    return e != hipSuccess ? e : launch_recover_mid_stamped(p, mid_bucket(d, rt, p.n), dev_ws_bytes(d), st, g_stamps);
   }
-  if (p.n <= lat_max() || p.raw_sig) {
+  if (p.n <= rt.lat_max || p.raw_sig) {
     hipError_t e = stamp_buf(lat_waves(p.n), st);
     return e != hipSuccess ? e : launch_recover_lat_stamped(p, st, g_stamps);
   }
 #endif
-  if (mid) return launch_recover_mid(p, mid_bucket(d, p.n), dev_ws_bytes(d), st);
-  if (p.n <= lat_max() || p.raw_sig) return launch_recover_lat(p, st);
+  if (mid) return launch_recover_mid(p, mid_bucket(d, rt, p.n), dev_ws_bytes(d), st);
+  if (p.n <= rt.lat_max || p.raw_sig) return launch_recover_lat(p, st);
   return launch_recover(p, d.mb_recover, d.ws_blocks, st);
 }
 
@@ -398,7 +418,7 @@ extern "C" size_t eges_diag_read_stamps(uint64_t* out, size_t max_waves) {
 }
 #endif
 
-int run_recover_dev_overlap(Dev& d, const uint8_t* msg, const uint8_t* sig, size_t n, uint8_t* pub, uint8_t* addr,
+int run_recover_dev_overlap(Dev& d, const Route& rt, const uint8_t* msg, const uint8_t* sig, size_t n, uint8_t* pub, uint8_t* addr,
                             uint8_t* status, hipStream_t st, int parts) {
   const size_t per = std::min(CHUNK, (n + parts - 1) / parts);
   const size_t n_pad = align_up(per, 64);
@@ -422,18 +442,18 @@ int run_recover_dev_overlap(Dev& d, const uint8_t* msg, const uint8_t* sig, size
     HIPCHK(launch_prep_ecrecover(msg + off * 32, sig + off * 65, m, (uint32_t)n_pad, rec, sj));
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr ? addr + off * 20 : nullptr, pub ? pub + off * 65 : nullptr,
                     d.gtab, (j & 1) ? d.ws2 : d.ws};
-    HIPCHK(launch_recover(with_diag(d, p), d.mb_recover, d.ws_blocks, sj));
+    HIPCHK(launch_recover(with_diag(d, p, rt), d.mb_recover, d.ws_blocks, sj));
   }
   HIPCHK(hipEventRecord(d.ev_join, d.aux));
   HIPCHK(hipStreamWaitEvent(st, d.ev_join, 0));
   return EGES_SUCCESS;
 }
 
-int run_recover_dev(Dev& d, const uint8_t* msg, const uint8_t* sig, size_t n, uint8_t* pub, uint8_t* addr,
-                    uint8_t* status, hipStream_t st) {
-  const int parts = overlap_parts(n);
+int run_recover_dev(Dev& d, const Route& rt, const uint8_t* msg, const uint8_t* sig, size_t n, uint8_t* pub,
+                    uint8_t* addr, uint8_t* status, hipStream_t st) {
+  const int parts = overlap_parts(rt, n);
   if (parts >= 2 && n >= (size_t)parts * 64 * 1024)
-    return run_recover_dev_overlap(d, msg, sig, n, pub, addr, status, st, parts);
+    return run_recover_dev_overlap(d, rt, msg, sig, n, pub, addr, status, st, parts);
   const size_t c = std::min(n, CHUNK);
   const size_t n_pad = align_up(c, 64);
   int rc = dev_ensure_buf(d, recover_scratch_bytes(n_pad));
@@ -444,25 +464,25 @@ int run_recover_dev(Dev& d, const uint8_t* msg, const uint8_t* sig, size_t n, ui
     const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr ? addr + off * 20 : nullptr, pub ? pub + off * 65 : nullptr,
                     d.gtab, d.ws};
-    if (fused_parse(d, m)) {  // the latency / mid-size kernels parse the bytes themselves
+    if (fused_parse(d, rt, m)) {  // the latency / mid-size kernels parse the bytes themselves
       p.raw_msg = msg + off * 32;
       p.raw_sig = sig + off * 65;
     } else {
       HIPCHK(launch_prep_ecrecover(msg + off * 32, sig + off * 65, m, (uint32_t)n_pad, rec, st));
     }
 #ifdef EGES_PHASE_STAMPS
-    if (!fused_parse(d, p.n)) {
+    if (!fused_parse(d, rt, p.n)) {
       HIPCHK(stamp_buf((size_t)d.ws_blocks * 4 /* waves per block */, st));
-      HIPCHK(launch_recover_stamped(with_diag(d, p), d.mb_recover, d.ws_blocks, st, g_stamps));
+      HIPCHK(launch_recover_stamped(with_diag(d, p, rt), d.mb_recover, d.ws_blocks, st, g_stamps));
       continue;
     }
 #endif
-    HIPCHK(launch_recover_pass(d, p, st));
+    HIPCHK(launch_recover_pass(d, rt, p, st));
   }
   return EGES_SUCCESS;
 }
 
-int run_sender_dev(Dev& d, const uint8_t* sighash, const uint8_t* r, const uint8_t* s, const uint8_t* v,
+int run_sender_dev(Dev& d, const Route& rt, const uint8_t* sighash, const uint8_t* r, const uint8_t* s, const uint8_t* v,
                    const uint8_t* vflags, size_t n, int signer, uint64_t chain_id, uint8_t* addr, uint8_t* status,
                    hipStream_t st) {
   const size_t c = std::min(n, CHUNK);
@@ -476,7 +496,7 @@ int run_sender_dev(Dev& d, const uint8_t* sighash, const uint8_t* r, const uint8
     HIPCHK(launch_prep_sender(sighash + off * 32, r + off * 32, s + off * 32, v + off * 32, vflags ? vflags + off : nullptr,
                               m, (uint32_t)n_pad, signer, chain_id, rec, st));
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr + off * 20, nullptr, d.gtab, d.ws};
-    HIPCHK(launch_recover_pass(d, p, st));
+    HIPCHK(launch_recover_pass(d, rt, p, st));
   }
   return EGES_SUCCESS;
 }
@@ -488,13 +508,13 @@ inline size_t tx_rows_bytes(size_t m) { return align_up(m * (4 * 32 + 1), 256); 
 // Sender checks inside the recovery kernel (RecoverParams::wire_*): no tx_rows / prep_sender
 // launches and no rows in between. EGES_WIRE_FUSED: 1 both (default), 2 the bucket form only,
 // 0 neither (A/B and tests).
-bool wire_fused(const Dev& d, size_t m, const uint8_t* raw) {
-  const long long f = knob(KNOB_WIRE_FUSED);
+bool wire_fused(const Dev& d, const Route& rt, size_t m, const uint8_t* raw) {
+  const long long f = rt.wire_fused;
   if (f == 0 || ((uintptr_t)raw & 3u) != 0) return false;
-  return (f == 1 && m <= lat_max()) || (use_mid(d, m) && mid_bucket(d, m));
+  return (f == 1 && m <= rt.lat_max) || (use_mid(d, rt, m) && mid_bucket(d, rt, m));
 }
 
-int run_sender_raw_dev(Dev& d, const uint8_t* raw, const uint64_t* offsets, size_t n, int signer, uint64_t chain_id,
+int run_sender_raw_dev(Dev& d, const Route& rt, const uint8_t* raw, const uint64_t* offsets, size_t n, int signer, uint64_t chain_id,
                        uint8_t* addr, uint8_t* status, uint8_t* sighash_out, hipStream_t st) {
   const size_t c = std::min(n, CHUNK);
   const size_t n_pad = align_up(c, 64);
@@ -512,7 +532,7 @@ int run_sender_raw_dev(Dev& d, const uint8_t* raw, const uint64_t* offsets, size
     uint8_t* vr = sr + (size_t)m * 32;
     uint8_t* vf = vr + (size_t)m * 32;
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr + off * 20, nullptr, d.gtab, d.ws};
-    if (wire_fused(d, m, raw)) {
+    if (wire_fused(d, rt, m, raw)) {
       p.wire_raw = raw;
       p.wire_off = offsets;
       p.wire_first = off;
@@ -523,14 +543,14 @@ int run_sender_raw_dev(Dev& d, const uint8_t* raw, const uint64_t* offsets, size
       HIPCHK(launch_tx_rows(raw, offsets, off, m, signer, chain_id, hs, rr, sr, vr, vf, st));
       HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, m, (uint32_t)n_pad, signer, chain_id, rec, st));
     }
-    HIPCHK(launch_recover_pass(d, p, st));
+    HIPCHK(launch_recover_pass(d, rt, p, st));
   }
   return EGES_SUCCESS;
 }
 
 // EVM precompile: 32-byte output words (12 zero bytes + address) written in place by the
 // recover kernel (addr_stride 32) after the words are cleared.
-int run_precompile_dev(Dev& d, const uint8_t* input, const uint32_t* inlen, size_t n, uint8_t* out32, uint8_t* status,
+int run_precompile_dev(Dev& d, const Route& rt, const uint8_t* input, const uint32_t* inlen, size_t n, uint8_t* out32, uint8_t* status,
                        hipStream_t st) {
   const size_t c = std::min(n, CHUNK);
   const size_t n_pad = align_up(c, 64);
@@ -543,12 +563,12 @@ int run_precompile_dev(Dev& d, const uint8_t* input, const uint32_t* inlen, size
     const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
     HIPCHK(launch_prep_precompile(input + off * 128, inlen ? inlen + off : nullptr, m, (uint32_t)n_pad, rec, st));
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, out32 + off * 32 + 12, nullptr, d.gtab, d.ws, 32};
-    HIPCHK(launch_recover_pass(d, p, st));
+    HIPCHK(launch_recover_pass(d, rt, p, st));
   }
   return EGES_SUCCESS;
 }
 
-int run_verify_dev(Dev& d, const uint8_t* pub, const uint8_t* publen, const uint8_t* msg, const uint8_t* sig, size_t n,
+int run_verify_dev(Dev& d, const Route& rt, const uint8_t* pub, const uint8_t* publen, const uint8_t* msg, const uint8_t* sig, size_t n,
                    uint8_t* ok, hipStream_t st) {
   const size_t n_pad = align_up(std::min(n, CHUNK), 64);
   int rc = dev_ensure_buf(d, verify_scratch_bytes(n_pad));
@@ -558,8 +578,8 @@ int run_verify_dev(Dev& d, const uint8_t* pub, const uint8_t* publen, const uint
     const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
     VerifyParams p{pub + off * 65, publen + off, msg + off * 32, sig + off * 64, m, ok + off, d.gtab, d.ws};
     verify_scratch_bind(p, d.buf, n_pad);
-    p = with_diag(d, p);
-    if (m <= lat_max()) HIPCHK(launch_verify_lat(p, p.n <= wide_max(), st));
+    p = with_diag(d, p, rt);
+    if (m <= rt.lat_max) HIPCHK(launch_verify_lat(p, p.n <= rt.wide_max, st));
     else HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
   }
   return EGES_SUCCESS;
@@ -610,7 +630,7 @@ Region region_for(const HostJob& j, size_t base, size_t m) {
 // compute stream runs chunk i, the copy stream stages chunk i+1's inputs and returns chunk
 // i-1's outputs (host order H2D(i+1), K(i+1), D2H(i): the pageable D2H blocks this thread
 // until K(i) is done, by which time K(i+1) is queued behind it). Synchronous overall.
-int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
+int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t cnt) {
   DevGuard g(d.id);
   // a shard big enough to pipeline runs as >= 2 chunks (each still a full resident grid)
   size_t c = std::min(CHUNK, cnt);
@@ -621,7 +641,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
   const bool pinned = nreg == 1 && worst <= PIN_BYTES;
   // Small calls on the latency kernel (no shared workspace) run on one of the device's lanes,
   // concurrently with each other; everything else on the device's main resources, in order.
-  const bool small = pinned && cnt <= lat_max();
+  const bool small = pinned && cnt <= rt.lat_max;
   Lane* lane = nullptr;
   std::unique_lock<std::mutex> lk;
   if (small) {
@@ -761,13 +781,13 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       JOIN_IN(r);
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, j.addr ? o_addr : nullptr, j.pub ? o_pub : nullptr,
                       d.gtab, d.ws};
-      if (fused_parse(d, m)) {  // the latency / mid-size kernels parse the bytes themselves
+      if (fused_parse(d, rt, m)) {  // the latency / mid-size kernels parse the bytes themselves
         p.raw_msg = dm;
         p.raw_sig = ds;
       } else {
         HIPCHK(launch_prep_ecrecover(dm, ds, (uint32_t)m, (uint32_t)m_pad, rec, st));
       }
-      HIPCHK(launch_recover_pass(d, p, st));
+      HIPCHK(launch_recover_pass(d, rt, p, st));
     } else if (j.kind == HostJob::SENDER) {
       uint8_t* dh = I;
       uint8_t* dr = dh + m * 32;
@@ -784,7 +804,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       HIPCHK(launch_prep_sender(dh, dr, dsv, dv, j.e ? df : nullptr, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id,
                                 rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
-      HIPCHK(launch_recover_pass(d, p, st));
+      HIPCHK(launch_recover_pass(d, rt, p, st));
     } else if (j.kind == HostJob::PRECOMPILE) {
       uint8_t* din = I;
       uint32_t* dlen = reinterpret_cast<uint32_t*>(din + m * 128);
@@ -796,7 +816,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       else HIPCHK(hipMemsetAsync(o_addr, 0, m * 32, st));
       HIPCHK(launch_prep_precompile(din, j.inlen ? dlen : nullptr, (uint32_t)m, (uint32_t)m_pad, rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr + 12, nullptr, d.gtab, d.ws, 32};
-      HIPCHK(launch_recover_pass(d, p, st));
+      HIPCHK(launch_recover_pass(d, rt, p, st));
     } else if (j.kind == HostJob::SENDER_RAW) {
       uint8_t* draw = I;
       uint64_t* doff = reinterpret_cast<uint64_t*>(draw + align_up(rg.raw_len, 8));
@@ -807,7 +827,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       uint8_t* vf = vr + m * 32;
       // (the fused form reads the encodings straight from the pinned buffer: a pipelined host copy
       // + DMA into device memory measured 0.486-0.508 ms against 0.450 ms for C1, same kernel)
-      const bool fused = !j.decode_only && wire_fused(d, m, draw);
+      const bool fused = !j.decode_only && wire_fused(d, rt, m, draw);
       if (rg.raw_len) H2D(B, draw, j.a + rg.raw_lo, rg.raw_len);
       H2D(B, reinterpret_cast<uint8_t*>(doff), j.offsets + base, 8 * (m + 1));
       FLUSH_IN(B);
@@ -826,7 +846,7 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
           HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, vf, st));
           HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, st));
         }
-        HIPCHK(launch_recover_pass(d, p, st));
+        HIPCHK(launch_recover_pass(d, rt, p, st));
       }
     } else {
       uint8_t* dp = I;
@@ -841,9 +861,9 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
       JOIN_IN(r);
       VerifyParams p{dp, dl, dm, ds, (uint32_t)m, o_st, d.gtab, d.ws};
       verify_scratch_bind(p, B + rg.o_rec, m_pad);
-      p = with_diag(d, p);
+      p = with_diag(d, p, rt);
       // small (lane) calls must not touch the device's shared workspace: latency kernel
-      if (small || m <= lat_max()) HIPCHK(launch_verify_lat(p, p.n <= wide_max(), st));
+      if (small || m <= rt.lat_max) HIPCHK(launch_verify_lat(p, p.n <= rt.wide_max, st));
       else HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
     }
     if (sx != st) HIPCHK(hipEventRecord(ev_k[r], st));
@@ -864,6 +884,10 @@ int run_host_shard(Dev& d, const HostJob& j, size_t off, size_t cnt) {
   if (sx != st) HIPCHK(hipStreamSynchronize(st));  // (st's last work is already behind sx's events)
   drain.armed = false;
   if (pinned && have_prev) unpack(prev);
+  // items a kernel marked EGES_ENGINE_FAULT (a wave hand-off timed out, handoff.cuh) have no
+  // result: the call fails rather than return them
+  if (j.status && !j.decode_only && std::memchr(j.status + off, EGES_ENGINE_FAULT, cnt))
+    return set_err(EGES_E_HIP, "a kernel hand-off timed out (EGES_ENGINE_FAULT items; EGES_DIAG_HANDOFF)");
   return EGES_SUCCESS;
 #undef H2D
 #undef FLUSH_IN
@@ -881,10 +905,11 @@ int run_host(const HostJob& j, size_t n) {
     devs = g_devs;
   }
   if (devs.empty()) return set_err(EGES_E_NODEVICE, "no gfx950 device available");
+  const Route rt = Route::now();
   // small batches stay on one device (a Geec block of 1000 txs is one tile set)
   size_t ndev = std::min(devs.size(), std::max<size_t>(1, n / 65536));
   const size_t per = (n + ndev - 1) / ndev;
-  if (ndev == 1) return run_host_shard(*devs[0], j, 0, n);
+  if (ndev == 1) return run_host_shard(*devs[0], rt, j, 0, n);
   std::vector<int> rcs(ndev, EGES_SUCCESS);
   std::vector<std::string> errs(ndev);
   std::vector<std::thread> th;
@@ -892,7 +917,7 @@ int run_host(const HostJob& j, size_t n) {
     const size_t lo = i * per, hi = std::min(n, lo + per);
     if (lo >= hi) continue;
     th.emplace_back([&, i, lo, hi] {
-      rcs[i] = run_host_shard(*devs[i], j, lo, hi - lo);
+      rcs[i] = run_host_shard(*devs[i], rt, j, lo, hi - lo);
       if (rcs[i]) errs[i] = t_err;
     });
   }
@@ -1311,8 +1336,9 @@ int eges_block_senders_raw(const uint8_t* block, size_t len, uint32_t lists, int
     *block_status = EGES_DECODE_FAILED;
     return EGES_SUCCESS;
   }
-  // the structure decodes: *block_status and counts are valid from here on, also when the
-  // selected lists exceed cap (the caller's sizing call)
+  // the structure decodes: counts are valid from here on, also when the selected lists exceed
+  // cap (the caller's sizing call, which returns before any transaction is decoded: its
+  // *block_status then covers the structure only, include/eges.h)
   *block_status = EGES_OK;
   size_t total = 0;
   for (int k = 0; k < 3; ++k) {
@@ -1402,7 +1428,7 @@ int eges_ecrecover_batch_dev(int device, const uint8_t* msg, const uint8_t* sig,
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
-  return run_recover_dev(*d, msg, sig, n, pub_out, addr_out, status, (hipStream_t)stream);
+  return run_recover_dev(*d, Route::now(), msg, sig, n, pub_out, addr_out, status, (hipStream_t)stream);
 }
 
 int eges_sender_batch_dev(int device, const uint8_t* sighash, const uint8_t* r, const uint8_t* s, const uint8_t* v,
@@ -1417,7 +1443,7 @@ int eges_sender_batch_dev(int device, const uint8_t* sighash, const uint8_t* r, 
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
-  return run_sender_dev(*d, sighash, r, s, v, vflags, n, signer, chain_id, addr_out, status,
+  return run_sender_dev(*d, Route::now(), sighash, r, s, v, vflags, n, signer, chain_id, addr_out, status,
                         (hipStream_t)stream);
 }
 
@@ -1433,7 +1459,7 @@ int eges_sender_raw_batch_dev(int device, const uint8_t* raw, const uint64_t* of
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
-  return run_sender_raw_dev(*d, raw, offsets, n, signer, chain_id, addr_out, status, sighash_out,
+  return run_sender_raw_dev(*d, Route::now(), raw, offsets, n, signer, chain_id, addr_out, status, sighash_out,
                             (hipStream_t)stream);
 }
 
@@ -1447,7 +1473,7 @@ int eges_ecrecover_precompile_batch_dev(int device, const uint8_t* input, const 
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
-  return run_precompile_dev(*d, input, inlen, n, out32, status, (hipStream_t)stream);
+  return run_precompile_dev(*d, Route::now(), input, inlen, n, out32, status, (hipStream_t)stream);
 }
 
 int eges_verify_batch_dev(int device, const uint8_t* pub, const uint8_t* publen, const uint8_t* msg, const uint8_t* sig,
@@ -1460,7 +1486,7 @@ int eges_verify_batch_dev(int device, const uint8_t* pub, const uint8_t* publen,
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
-  return run_verify_dev(*d, pub, publen, msg, sig, n, ok_out, (hipStream_t)stream);
+  return run_verify_dev(*d, Route::now(), pub, publen, msg, sig, n, ok_out, (hipStream_t)stream);
 }
 
 static int synth_common(int device, uint64_t first_index, size_t n, const uint8_t* msg_in, uint8_t* msg, uint8_t* sig,

@@ -57,7 +57,7 @@ using gdig_t = std::conditional_t<(GBITS > 16), int32_t, int16_t>;
 
 enum : uint32_t {
   ST_OK = 0, ST_INVALID_CHAIN_ID = 1, ST_INVALID_SIG = 2, ST_INVALID_RECOVERY_ID = 5, ST_RECOVER_FAILED = 6,
-  ST_DECODE_FAILED = 7
+  ST_DECODE_FAILED = 7, ST_ENGINE_FAULT = 0xFF
 };
 
 __constant__ const uint32_t FE_BETA[8] = {0x719501EEu, 0xC1396C28u, 0x12F58995u, 0x9CF04975u,

@@ -1,0 +1,55 @@
+#pragma once
+// Hand-offs between the waves of one workgroup through LDS (the mid-size kernel's roles,
+// k_recover_mid.hip, and the latency kernels' split form, k_recover_lat.hip).
+//
+// A producer publishes a value (a flag 1, or a running count) after its LDS data with a
+// workgroup release fence; consumers poll until the value reaches what they need, then acquire.
+// Every wait is bounded (~1 s at the shader clock, against microseconds in normal operation): a
+// wait that runs out, or that sees another wave of the workgroup give up first, marks the
+// workgroup's error word and returns false. The wave that writes the outputs checks that word
+// after its last wait (every other wave's last wait precedes a value that wave consumes), and
+// then writes ST_ENGINE_FAULT and no address for the workgroup's items: the host-buffer entries
+// return EGES_E_HIP for such a call, and EGES_DIAG_HANDOFF counts it. So a logic error can
+// neither hang the device nor yield a status-OK result computed from LDS that was never written.
+#include "core.cuh"
+
+namespace eges {
+
+DEV uint32_t ho_load(const uint32_t* f) {
+  return __hip_atomic_load(const_cast<uint32_t*>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// publish v (after this wave's earlier LDS writes); skip: tests only (KNOB_TEST_SKIP_FLAG)
+DEV void ho_set(uint32_t* f, uint32_t v = 1u, bool skip = false) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (!skip && (threadIdx.x & 63) == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// wait until *f >= k; false (and *err set) on timeout or when another wave has already failed
+template <int SLEEP>
+DEV bool ho_wait(const uint32_t* f, uint32_t k, uint32_t* err) {
+  constexpr uint32_t POLLS = (1u << 25) / SLEEP;  // x (64 SLEEP + ~20) cycles: ~1 s
+#pragma unroll 1
+  for (uint32_t it = 0; it < POLLS; ++it) {
+    if (ho_load(f) >= k) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      return true;
+    }
+    if (ho_load(err) != 0u) break;
+    __builtin_amdgcn_s_sleep(SLEEP);
+  }
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  return false;
+}
+// the output wave, after its last wait: did any hand-off of this workgroup fail?
+DEV bool ho_failed(const uint32_t* err, const Diag& dg) {
+  const bool bad = ho_load(err) != 0u;
+  if (bad) diag_bump(dg, EGES_DIAG_HANDOFF);
+  return bad;
+}
+// tests only: workgroup 0's producer of flag k skips publishing it once per launch
+template <class P>
+DEV bool ho_skip(const P& prm, int k) {
+  return prm.test_skip_flag == (uint32_t)k + 1u && blockIdx.x == prm.test_skip_block;
+}
+
+}  // namespace eges

@@ -29,6 +29,7 @@
 
 #include "core.cuh"
 #include "frg.cuh"
+#include "handoff.cuh"
 #include "keccak_wave.cuh"
 #include "modinv_row.cuh"
 #include "sender.cuh"
@@ -56,7 +57,7 @@ constexpr int HTAB = 1 << (HBITS - 1);
 constexpr int HWIN = (130 - RBITS * SPLIT_W0 + HBITS) / HBITS;
 
 // LDS flags of the split form (set once by their producer wave, polled by the consumers)
-enum { F_DIG = 0, F_Y, F_G, F_LHI, F_HI, NFLAGS };
+enum { F_DIG = 0, F_Y, F_G, F_LHI, F_HI, F_ERR, NFLAGS };
 
 struct LatLds {
   uint32_t tab[PTAB][2][16];  // {1..16} * R' (x, y), row form (all four rows read the same words)
@@ -75,20 +76,16 @@ struct LatLds {
   uint32_t ylift[16];         // y of R (the square root, from the helper wave)
   uint32_t yok;
   uint32_t flag[NFLAGS];
+  uint32_t skip;              // tests only: 1 + the flag this workgroup's producer skips (ho_skip)
   uint64_t w1t[2];            // diagnostic build: wave 1's r^-1 and u1 / u2 / GLV / digits ticks
   uint8_t stage[LAT_STAGE];   // wire form: the transaction's encoding
 };
 
-// Producer / consumer hand-off between the waves of one workgroup through LDS (split form): the
-// producer's LDS writes are ordered before the flag by the release fence; consumers poll.
-DEV void flag_set(uint32_t* f) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if (lane_id() == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-DEV void flag_wait(uint32_t* f) {
-  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) __builtin_amdgcn_s_sleep(1);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
+// Producer / consumer hand-off between the waves of one workgroup through LDS (split form,
+// handoff.cuh): the producer's LDS writes are ordered before the flag by the release fence;
+// consumers poll, bounded; a failed hand-off makes wave 0 write ST_ENGINE_FAULT.
+DEV void flag_set(LatLds& S, int k) { ho_set(&S.flag[k], 1u, S.skip == (uint32_t)k + 1u); }
+DEV void flag_wait(LatLds& S, int k) { (void)ho_wait<1>(&S.flag[k], 1u, &S.flag[F_ERR]); }
 
 // signed fixed-window recoding (core.cuh recode) into this row's digit array
 template <int W, int NW, class D>
@@ -584,12 +581,12 @@ DEV void helper_split(LatLds& S, const uint32_t* gcomb, bool need_y, const fr& c
   if (need_y) ok = lift_y(y, c, odd);
   S.ylift[row_lane()] = y.v;
   if (lane_id() == 0) S.yok = ok ? 1u : 0u;
-  flag_set(&S.flag[F_Y]);
+  flag_set(S, F_Y);
   gejr A;
   bool ainf;
   gcomb_exact(A, ainf, S, gcomb, dg);
   put_part(S, 2, A, ainf);
-  flag_set(&S.flag[F_G]);
+  flag_set(S, F_G);
 }
 // Split form, waves 2 (j = 0: R) and 3 (j = 1: lambda R): D = 2^(RBITS SPLIT_W0) R' by doublings
 // (each wave its own copy, no hand-off), the table of D's (X, Y) on the curve where it is affine,
@@ -607,23 +604,23 @@ DEV void high_wave(LatLds& S, const fr& x, const fr& c, int j, const Diag& dg) {
   const fr zd = build_table_wave<HTAB>(Dp, S.dtab[j], S.dzr[j], S.dzq[j]);
   if (j == 1) build_btab<HTAB>(S.dtab[1], S.dbtab);
   const fr scale = fr_mul(zd, D.z);
-  flag_wait(&S.flag[F_DIG]);
+  flag_wait(S, F_DIG);
   gejr A;
   bool ainf;
   strauss_win_exact<HBITS, HTAB>(A, ainf, S.dtab[j], S.dbtab, S.hdig[0], S.hdig[1], 1 << j, 0, HWIN, dg);
-  flag_wait(&S.flag[F_Y]);
+  flag_wait(S, F_Y);
   A.z = fr_mul(A.z, fr_mul(scale, fr{S.ylift[row_lane()]}));
   if (j == 1) {
     put_part(S, 4, A, ainf);
-    flag_set(&S.flag[F_LHI]);
+    flag_set(S, F_LHI);
     return;
   }
-  flag_wait(&S.flag[F_LHI]);
+  flag_wait(S, F_LHI);
   bool linf;
   const gejr Lp = get_part(S, 4, linf);
   A = join_parts(A, ainf, Lp, linf, ainf, dg);
   put_part(S, 3, A, ainf);
-  flag_set(&S.flag[F_HI]);
+  flag_set(S, F_HI);
 }
 
 // Wave 0: u_r * (x, y) + u_g G with y deferred. R' = (c x, c^2) on E', its table, the digits,
@@ -645,22 +642,22 @@ DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& 
   const fr zeta = build_table_wave<PTAB>(Rp, S.tab, S.zr, S.zq);
   build_btab<PTAB>(S.tab, S.btab);
   st->mark(3);
-  if (SPLIT) flag_wait(&S.flag[F_DIG]);
+  if (SPLIT) flag_wait(S, F_DIG);
   else __syncthreads();  // digits ready
   st->mark(1);
   gejr A;
   bool ainf;
   strauss_win_exact<RBITS, PTAB>(A, ainf, S.tab, S.btab, S.rdig[0], S.rdig[1], 3, 0, SPLIT ? SPLIT_W0 : RWIN, dg);
-  if (SPLIT) flag_wait(&S.flag[F_Y]);
+  if (SPLIT) flag_wait(S, F_Y);
   else __syncthreads();  // partial sums (and y) ready
   if (root) root_fetch(*root->prm, root->idx, c, root->odd, S);  // (this wave's own LDS words)
   A.z = fr_mul(A.z, fr_mul(zeta, fr{S.ylift[row_lane()]}));  // the true curve
   bool ginf;
-  if (SPLIT) flag_wait(&S.flag[F_G]);
+  if (SPLIT) flag_wait(S, F_G);
   const gejr Gp = get_part(S, 2, ginf);
   Q = join_parts(A, ainf, Gp, ginf, qinf, dg);
   if (SPLIT) {
-    flag_wait(&S.flag[F_HI]);
+    flag_wait(S, F_HI);
     bool hinf;
     const gejr Hp = get_part(S, 3, hinf);
     Q = join_parts(Q, qinf, Hp, hinf, qinf, dg);
@@ -778,6 +775,7 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
       for (uint32_t j = threadIdx.x; j < wlen; j += blockDim.x) S.stage[j] = prm.wire_raw[wra + j];
   }
   if (SPLIT && threadIdx.x < NFLAGS) S.flag[threadIdx.x] = 0u;
+  if (SPLIT && threadIdx.x == 0) S.skip = blockIdx.x == prm.test_skip_block ? prm.test_skip_flag : 0u;
   if (SPLIT || wire) __syncthreads();  // (split form: the only barrier besides; narrow: the stage)
   // --- parse (every lane reads the same record; wire form: every lane decodes the same item)
   LatParse q;
@@ -816,13 +814,13 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
     if (wire) {
       // the R digits first (wave 0 is waiting for them), then the signing hash for z and u1
       recode_r<SPLIT>(u2, S);
-      if (SPLIT) flag_set(&S.flag[F_DIG]);
+      if (SPLIT) flag_set(S, F_DIG);
       else __syncthreads();  // digits ready (and the table)
       uint8_t* hs = prm.wire_sighash ? prm.wire_sighash + (size_t)idx * 32 : nullptr;
       recode_g(sc_neg(sc_mul(rinv, wire_sighash_wave(m, decoded, hs))), S);
     } else {
       recode_r<SPLIT>(u2, S);  // the R digits first: wave 0 is waiting for them
-      if (SPLIT) flag_set(&S.flag[F_DIG]);
+      if (SPLIT) flag_set(S, F_DIG);
       else __syncthreads();  // digits ready (and the table)
       recode_g(sc_neg(sc_mul(rinv, Z)), S);  // u1 = -z / r, for this wave's comb
     }
@@ -844,7 +842,8 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   bool qinf;
   const RootSrc root{&prm, idx, odd};
   ecmult_deferred<ST, SPLIT>(Q, qinf, x, c, S, st, dg, SPLIT ? nullptr : &root);
-  ok = ok && S.yok != 0 && !qinf;  // ge_set_xo_var failure, main_impl.h:120
+  const bool fault = SPLIT && ho_failed(&S.flag[F_ERR], dg);  // after wave 0's last wait (F_HI)
+  ok = ok && S.yok != 0 && !qinf && !fault;  // ge_set_xo_var failure, main_impl.h:120
   // --- affine, serialize, address
   const fr zq = fr_select(ok, Q.z, fr_one());
 #ifdef EGES_STAMP_MODINV  // diagnostic: slots 2 / 7 carry Z^-1's divsteps / update ticks instead
@@ -866,7 +865,7 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   pub_address_wave(a, X, Y);  // Keccak across the wave's lanes (keccak_wave.cuh)
   if (lane_id() == 0) {
     const uint32_t pre_st = (meta >> 8) & 0xffu;
-    prm.status[idx] = (uint8_t)(pre_st != ST_OK ? pre_st : (ok ? ST_OK : ST_RECOVER_FAILED));
+    prm.status[idx] = (uint8_t)(fault ? ST_ENGINE_FAULT : pre_st != ST_OK ? pre_st : (ok ? ST_OK : ST_RECOVER_FAILED));
     if (prm.addr) {
       uint32_t* dst = reinterpret_cast<uint32_t*>(prm.addr + (size_t)idx * prm.addr_stride);
 #pragma unroll
@@ -915,6 +914,7 @@ DEV void verify_lat_body(const VerifyParams& prm) {
   const uint32_t idx = blockIdx.x;  // grid = n
   if (SPLIT) {
     if (threadIdx.x < NFLAGS) S.flag[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) S.skip = blockIdx.x == prm.test_skip_block ? prm.test_skip_flag : 0u;
     __syncthreads();  // the only barrier of the split form
   }
   uint32_t l[8];
@@ -955,7 +955,7 @@ DEV void verify_lat_body(const VerifyParams& prm) {
     const sc sinv = sc_inv_row_var(sc_select(sig_ok, Sv, sc_one()));
     const sc u2 = sc_select(sig_ok, sc_mul(sinv, R), sc_one());
     recode_r<SPLIT>(u2, S);  // the key's digits first: wave 0 is waiting for them
-    if (SPLIT) flag_set(&S.flag[F_DIG]);
+    if (SPLIT) flag_set(S, F_DIG);
     else __syncthreads();  // digits ready (and the table)
     recode_g(sc_mul(sinv, Z), S);  // u1 = z / s
     // the square root only for 33-byte keys; 65-byte keys give y
@@ -971,6 +971,7 @@ DEV void verify_lat_body(const VerifyParams& prm) {
   gejr Q;
   bool qinf;
   ecmult_deferred<NoStamp, SPLIT>(Q, qinf, x, c, S, &st_, dg);
+  const bool fault = SPLIT && ho_failed(&S.flag[F_ERR], dg);  // after wave 0's last wait (F_HI)
   const bool pk_ok = c33 ? (x_ok && S.yok != 0) : (c65 && x_ok && y_ok && !hybrid_bad && on);
   bool ok = sig_ok && pk_ok && !qinf;
   // x(Q) mod n == r  <=>  r Z^2 == X  or  (r < p - n and (r + n) Z^2 == X)  (ecdsa_impl.h:246-270)
@@ -987,7 +988,7 @@ DEV void verify_lat_body(const VerifyParams& prm) {
     }
     eq = fr_equal(Q.x, fr_mul(fe_to_fr(fe_from_u256(rn)), z2));
   }
-  if (lane_id() == 0) prm.ok[idx] = (ok && eq) ? 1 : 0;
+  if (lane_id() == 0) prm.ok[idx] = fault ? (uint8_t)ST_ENGINE_FAULT : (ok && eq) ? 1 : 0;
 }
 
 constexpr int LAT_WG_SPLIT = 256;  // split form: four waves

@@ -26,6 +26,7 @@
 #include <type_traits>
 
 #include "core.cuh"
+#include "handoff.cuh"
 #include "sender.cuh"
 
 namespace eges {
@@ -41,7 +42,7 @@ constexpr int MID_HTAB = 1 << (MID_HBITS - 1);
 constexpr int MID_HWIN = (130 - RBITS * MID_W0 + MID_HBITS) / MID_HBITS;
 static_assert(MID_W0 * RBITS + MID_HWIN * MID_HBITS >= 130, "windows cover a GLV half + carry");
 
-enum { MF_DIG = 0, MF_Y, MF_G, MF_HB, MF_HC, MF_N };
+enum { MF_DIG = 0, MF_Y, MF_G, MF_HB, MF_HC, MF_ERR, MF_N };
 
 struct MidLds {
   int8_t lo[2][MID_W0][MID_L];    // 5-bit digits of both halves, windows [0, MID_W0)
@@ -63,20 +64,11 @@ constexpr size_t MID_ZR_B = MID_ZR_A + (size_t)(PTAB - 1) * MID_L * ZR_WORDS;
 constexpr size_t MID_ZR_C = MID_ZR_B + (size_t)(MID_HTAB - 1) * MID_L * ZR_WORDS;
 constexpr size_t MID_WS_WORDS = MID_ZR_C + (size_t)(MID_HTAB - 1) * MID_L * ZR_WORDS;
 
-DEV void mflag_set(uint32_t* f) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if ((threadIdx.x & 63) == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// Every producer sets its flags unconditionally; the bound (~1 s) only keeps a logic error from
-// hanging the device (the results would then be wrong, and the tests say so).
-DEV void mflag_wait(uint32_t* f) {
-#pragma unroll 1
-  for (uint32_t it = 0; it < (1u << 24); ++it) {
-    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) break;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
+// Flags between the roles (handoff.cuh): every producer sets its flags unconditionally; the
+// bounded waits only keep a logic error from hanging the device or from yielding a result
+// computed from unwritten LDS (the output wave then writes ST_ENGINE_FAULT).
+#define MFLAG_SET(k) ho_set(&S.flag[k], 1u, ho_skip(prm, k))
+#define MFLAG_WAIT(k) ho_wait<2>(&S.flag[k], 1u, &S.flag[MF_ERR])
 
 template <int N>
 DEV void lds_put_fe(uint32_t (*a)[MID_L], const uint32_t* v, uint32_t l) {
@@ -316,13 +308,13 @@ DEV void recover_mid_body(const RecoverParams& prm, uint64_t* stamps) {
     glv_split(h1, h2, u2);
     recode_mid(h1, S.lo[0], S.hi[0], l);
     recode_mid(h2, S.lo[1], S.hi[1], l);
-    mflag_set(&S.flag[MF_DIG]);
+    MFLAG_SET(MF_DIG);
     st_.mark(2);
     ge Rp;
     const bool yok = ge_set_xo(Rp, x, pok && (q.recid & 1u) != 0);  // ge_set_xo_var, group_impl.h:216-237
     lds_put_fe<FE_LIMBS>(S.y, Rp.y.v, l);
     S.yok[l] = yok ? 1u : 0u;
-    mflag_set(&S.flag[MF_Y]);
+    MFLAG_SET(MF_Y);
     st_.mark(3);
     const uint32_t* gcomb = prm.gtab + (size_t)2 * GTAB * PT_WORDS;
     gej Ga;
@@ -333,7 +325,7 @@ DEV void recover_mid_body(const RecoverParams& prm, uint64_t* stamps) {
       comb_mid<true>(Ga, ginf, u1, gcomb, dg);
     }
     put_part_ls(S, 0, Ga, ginf, l);
-    mflag_set(&S.flag[MF_G]);
+    MFLAG_SET(MF_G);
     st_.mark(4);
     stamp_out();
     return;
@@ -359,7 +351,7 @@ DEV void recover_mid_body(const RecoverParams& prm, uint64_t* stamps) {
     const fe zd = build_table_mid<MID_HTAB>(tab, ws + (j ? MID_ZR_C : MID_ZR_B), Dp, l);
     const fe scale = fe_mul(zd, D.z);
     st_.mark(2);
-    mflag_wait(&S.flag[MF_DIG]);
+    MFLAG_WAIT(MF_DIG);
     st_.mark(3);
     gej H;
     bool hinf;
@@ -367,7 +359,7 @@ DEV void recover_mid_body(const RecoverParams& prm, uint64_t* stamps) {
     else strauss_mid_exact<MID_HBITS, MID_HTAB, MID_HWIN, 2>(H, hinf, tab, S.hi[0], S.hi[1], l, dg);
     H.z = fe_mul(H.z, scale);  // E' coordinates
     put_part_ls(S, 1 + j, H, hinf, l);
-    mflag_set(&S.flag[j ? MF_HC : MF_HB]);
+    MFLAG_SET(j ? MF_HC : MF_HB);
     st_.mark(4);
     stamp_out();
     return;
@@ -377,7 +369,7 @@ DEV void recover_mid_body(const RecoverParams& prm, uint64_t* stamps) {
   st_.mark(0);
   const fe zeta = build_table_mid<PTAB>(tab, ws + MID_ZR_A, Rp, l);
   st_.mark(3);
-  mflag_wait(&S.flag[MF_DIG]);
+  MFLAG_WAIT(MF_DIG);
   st_.mark(1);
   gej A;
   bool ainf;
@@ -385,19 +377,19 @@ DEV void recover_mid_body(const RecoverParams& prm, uint64_t* stamps) {
   st_.mark(4);
   // back to E: an E' Jacobian point (X, Y, Z) is (X, Y, Z y) on E; the table curve adds zeta.
   // A + u1 G first (both are usually ready before the high waves finish), then the high parts.
-  mflag_wait(&S.flag[MF_Y]);
+  MFLAG_WAIT(MF_Y);
   fe y;
   lds_get_fe<FE_LIMBS>(S.y, y.v, l);
   const bool yok = S.yok[l] != 0;
   A.z = fe_mul(A.z, fe_mul(zeta, y));
   bool binf, cinf, ginf, hinf, qinf;
-  mflag_wait(&S.flag[MF_G]);
+  MFLAG_WAIT(MF_G);
   st_.mark(7);
   const gej Gp = get_part_ls(S, 0, ginf, l);
   gej Q = join_mid(A, ainf, Gp, ginf, qinf, dg);
   st_.mark(2);
-  mflag_wait(&S.flag[MF_HB]);
-  mflag_wait(&S.flag[MF_HC]);
+  MFLAG_WAIT(MF_HB);
+  MFLAG_WAIT(MF_HC);
   st_.mark(7);
   gej Hb = get_part_ls(S, 1, binf, l), Hc = get_part_ls(S, 2, cinf, l);
   Hb.z = fe_mul(Hb.z, y);
@@ -405,7 +397,8 @@ DEV void recover_mid_body(const RecoverParams& prm, uint64_t* stamps) {
   const gej H = join_mid(Hb, binf, Hc, cinf, hinf, dg);
   Q = join_mid(Q, qinf, H, hinf, qinf, dg);
   st_.mark(2);
-  const bool ok = pok && yok && !qinf;  // main_impl.h:120
+  const bool fault = ho_failed(&S.flag[MF_ERR], dg);  // after A's last wait
+  const bool ok = pok && yok && !qinf && !fault;  // main_impl.h:120
   // affine, serialize, address
   const fe zi = fe_inv(fe_select(ok, Q.z, fe_one()));
   const fe zi2 = fe_sqr(zi);
@@ -415,7 +408,7 @@ DEV void recover_mid_body(const RecoverParams& prm, uint64_t* stamps) {
   st_.mark(5);
   if (live) {
     const uint32_t pre_st = (q.meta >> 8) & 0xffu;
-    prm.status[idx] = (uint8_t)(pre_st != ST_OK ? pre_st : (ok ? ST_OK : ST_RECOVER_FAILED));
+    prm.status[idx] = (uint8_t)(fault ? ST_ENGINE_FAULT : pre_st != ST_OK ? pre_st : (ok ? ST_OK : ST_RECOVER_FAILED));
     if (prm.addr) {
       uint32_t a[5];
       pub_address(a, X, Y);
@@ -484,7 +477,7 @@ constexpr int GJ_WORDS = 3 * FE_LIMBS;
 
 enum {
   BF_DIG = 0, BF_Y, BF_G, BF_Q2, BF_PUB, BF_CON0, BF_CON1, BF_PARSED, BF_STAGE_FREE, BF_FIN0, BF_FIN1, BF_A0, BF_A1,
-  BF_N
+  BF_ERR, BF_N
 };
 // ring slots that hold wave X's partial bucket sums B1 + B3 of each half once the ring is drained
 // (their points, 33 and 34, are consumed by both halves before either finishes)
@@ -524,31 +517,12 @@ DEV gej lds_get_gej(const uint32_t (*a)[MID_L], uint32_t l) {
   return p;
 }
 
-// LDS counters: the producer publishes a count, consumers wait until it reaches k. Only LDS
-// data is handed over this way, and the LDS performs one wave's DS instructions in order, so a
-// compiler barrier orders the data stores before the count store (a workgroup fence would also
-// wait for the stores to complete: measured ~4 % of the doubling chain).
-#ifndef EGES_BK_FENCE
-#define EGES_BK_FENCE 0
-#endif
-DEV void cnt_set(uint32_t* f, uint32_t v) {
-  if (EGES_BK_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  else __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  if ((threadIdx.x & 63) == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-DEV uint32_t cnt_get(const uint32_t* f) {
-  return __hip_atomic_load(const_cast<uint32_t*>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// The bound (~1 s) only keeps a logic error from hanging the device (results would be wrong).
-DEV void cnt_wait(const uint32_t* f, uint32_t k) {
-#pragma unroll 1
-  for (uint32_t it = 0; it < (1u << 24); ++it) {
-    if (cnt_get(f) >= k) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  if (EGES_BK_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  else __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
+// Flags and LDS counters (handoff.cuh): the producer publishes a flag or a running count after
+// a workgroup release fence, consumers wait (bounded) until it reaches k and acquire.
+#define BFLAG_SET(k) ho_set(&S.flag[k], 1u, ho_skip(prm, k))
+#define BFLAG_WAIT(k) ho_wait<2>(&S.flag[k], 1u, &S.flag[BF_ERR])
+#define CNT_SET(k, v) ho_set(&S.flag[k], (v))
+#define CNT_WAIT(k, v) ho_wait<1>(&S.flag[k], (v), &S.flag[BF_ERR])
 
 // a + b, both Jacobian, neither at infinity, a != +-b (add-2007-bl, join_mid without the checks).
 // In: X m1, Y <= 2, Z <= 2. Out: X, Y m1, Z m2.
@@ -677,7 +651,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
     wire_parse(S, prm, live ? idx : prm.n - 1, stage_a0, stage_end, q, m);
     S.meta[l] = q.meta;
     S.pok[l] = live && q.ok ? 1u : 0u;
-    mflag_set(&S.flag[BF_PARSED]);
+    BFLAG_SET(BF_PARSED);
   } else if (wv == 0) {  // R's x straight from the encoding, without waiting for S's checks
     q.ok = live && wire_r_only(S, prm, idx, stage_a0, stage_end, q.xr);
   } else {
@@ -704,7 +678,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
     glv_split(h1, h2, u2);
     recode_bk(h1, S.dig[0], l);
     recode_bk(h2, S.dig[1], l);
-    mflag_set(&S.flag[BF_DIG]);
+    BFLAG_SET(BF_DIG);
     st_.mark(2);
     if (wire) {  // the signing hash (FrontierSigner / EIP155Signer.Hash) of the encoding, then z
       uint8_t h[32];
@@ -714,7 +688,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
 #pragma unroll
         for (int k = 0; k < 32; ++k) h[k] = 0;
       }
-      mflag_set(&S.flag[BF_STAGE_FREE]);
+      BFLAG_SET(BF_STAGE_FREE);
       if (prm.wire_sighash && live) {  // zeros for an undecodable item, as tx_rows_kernel
         const bool dec = ((q.meta >> 8) & 0xffu) != ST_DECODE_FAILED;
         uint32_t* dst = reinterpret_cast<uint32_t*>(prm.wire_sighash + (size_t)idx * 32);
@@ -735,7 +709,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
     const bool yok = ge_set_xo(Rp, x, pok && (q.recid & 1u) != 0);  // ge_set_xo_var, group_impl.h:216-237
     lds_put_fe<FE_LIMBS>(S.y, Rp.y.v, l);
     S.yok[l] = yok ? 1u : 0u;
-    mflag_set(&S.flag[BF_Y]);
+    BFLAG_SET(BF_Y);
     st_.mark(3);
     const uint32_t* gcomb = prm.gtab + (size_t)2 * GTAB * PT_WORDS;
     gej Ga;
@@ -745,9 +719,13 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
       diag_bump(dg, EGES_DIAG_MID_REDO);
       comb_mid<true>(Ga, ginf, u1, gcomb, dg);
     }
+    // part[0] shares LDS with the wire stage: wave X reads its R from the stage (wire_r_only) before
+    // it publishes its first point, so that count is the stage's release for this write (wave S's
+    // own reads end at BF_STAGE_FREE; part[1] is written after BF_A1, i.e. after X's whole chain)
+    if (wire) CNT_WAIT(BF_PUB, 1u);
     lds_put_gej(S.u.part[0], Ga, l);
     S.pinf[0][l] = ginf ? 1u : 0u;
-    mflag_set(&S.flag[BF_G]);
+    BFLAG_SET(BF_G);
     st_.mark(4);
     stamp_out();
     return;
@@ -769,30 +747,30 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
       }
       if ((uint32_t)k >= freed) {  // slot k % BK_RING is free once both halves consumed point k - BK_RING
         st_.mark(1);
-        cnt_wait(&S.flag[BF_CON0], (uint32_t)(k - BK_RING + 1));
-        cnt_wait(&S.flag[BF_CON1], (uint32_t)(k - BK_RING + 1));
-        const uint32_t c0 = cnt_get(&S.flag[BF_CON0]), c1 = cnt_get(&S.flag[BF_CON1]);
+        CNT_WAIT(BF_CON0, (uint32_t)(k - BK_RING + 1));
+        CNT_WAIT(BF_CON1, (uint32_t)(k - BK_RING + 1));
+        const uint32_t c0 = ho_load(&S.flag[BF_CON0]), c1 = ho_load(&S.flag[BF_CON1]);
         freed = (c0 < c1 ? c0 : c1) + BK_RING;
         st_.mark(2);
       }
       lds_put_gej(S.ring[k % BK_RING], P, l);
-      cnt_set(&S.flag[BF_PUB], (uint32_t)(k + 1));
+      CNT_SET(BF_PUB, (uint32_t)(k + 1));
     }
     st_.mark(1);
     // then, per half, B1 + B3 of its final buckets (the halves' own waves do the rest of the sum
     // meanwhile), into a drained ring slot
 #pragma unroll 1
     for (int h = 0; h < 2; ++h) {
-      mflag_wait(&S.flag[BF_FIN0 + h]);
+      BFLAG_WAIT(BF_FIN0 + h);
       const uint32_t slot = (uint32_t)(BK_ASLOT + h), pt = slot + (uint32_t)BK_RING * ((BK_WIN - 1 - slot) / BK_RING);
-      cnt_wait(&S.flag[BF_CON0], pt + 1);  // the last point that slot held, consumed by both halves
-      cnt_wait(&S.flag[BF_CON1], pt + 1);
+      CNT_WAIT(BF_CON0, pt + 1);  // the last point that slot held, consumed by both halves
+      CNT_WAIT(BF_CON1, pt + 1);
       bool ia;
       const gej a = join_mid(lds_get_gej(S.bucket[h][0], l), S.binf[h][0][l] != 0, lds_get_gej(S.bucket[h][2], l),
                              S.binf[h][2][l] != 0, ia, dg);
       lds_put_gej(S.ring[slot], a, l);
       S.ainf[h][l] = ia ? 1u : 0u;
-      mflag_set(&S.flag[BF_A0 + h]);
+      BFLAG_SET(BF_A0 + h);
     }
     st_.mark(2);
     stamp_out();
@@ -803,20 +781,20 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
   st_.mark(0);
 #pragma unroll
   for (int v = 0; v < BK_NB; ++v) S.binf[h][v][l] = 1u;
-  mflag_wait(&S.flag[BF_DIG]);
+  BFLAG_WAIT(BF_DIG);
   st_.mark(1);
   uint32_t avail = 0;  // points known published
 #pragma unroll 1
   for (int k = 0; k < BK_WIN; ++k) {
     if ((uint32_t)k >= avail) {
       st_.mark(2);
-      cnt_wait(&S.flag[BF_PUB], (uint32_t)(k + 1));
-      avail = cnt_get(&S.flag[BF_PUB]);
+      CNT_WAIT(BF_PUB, (uint32_t)(k + 1));
+      avail = ho_load(&S.flag[BF_PUB]);
       st_.mark(3);
     }
     gej P = lds_get_gej(S.ring[k % BK_RING], l);
     const int d = (int)S.dig[h][k][l];
-    cnt_set(&S.flag[BF_CON0 + h], (uint32_t)(k + 1));  // LDS reads of one wave complete in order
+    CNT_SET(BF_CON0 + h, (uint32_t)(k + 1));  // (the release fence orders this wave's ring reads first)
     const int a = d < 0 ? -d : d;
     const int v = a > 0 ? a - 1 : 0;
     P.y = fe_select(d < 0, fe_neg<1>(P.y), P.y);
@@ -832,42 +810,43 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
   // Q_h = B1 + 2 B2 + 3 B3 + 4 B4 = (B1 + B3) + 2 ((B2 + B3) + 2 B4): wave X joins B1 + B3
   // (its chain is done), this wave the rest: three joins and two doublings on this path
   static_assert(BK_NB == 4, "bucket sum written for 3-bit windows");
-  mflag_set(&S.flag[BF_FIN0 + h]);
+  BFLAG_SET(BF_FIN0 + h);
   bool ib, tinf;
   const bool i3 = S.binf[h][2][l] != 0;
   gej Jb = join_mid(lds_get_gej(S.bucket[h][1], l), S.binf[h][1][l] != 0, lds_get_gej(S.bucket[h][2], l), i3, ib, dg);
   Jb = join_mid(Jb, ib, gej_double(lds_get_gej(S.bucket[h][3], l)), S.binf[h][3][l] != 0, ib, dg);
   Jb = gej_double(Jb);
-  mflag_wait(&S.flag[BF_A0 + h]);
+  BFLAG_WAIT(BF_A0 + h);
   gej T = join_mid(lds_get_gej(S.ring[BK_ASLOT + h], l), S.ainf[h][l] != 0, Jb, ib, tinf, dg);
   st_.mark(4);
   if (h == 1) {
     T.x = fe_mul(T.x, fe_const(FE_BETA));  // lambda (X, Y, Z) = (beta X, Y, Z)
-    if (wire) mflag_wait(&S.flag[BF_STAGE_FREE]);  // part[1] shares LDS with the stage
+    if (wire) BFLAG_WAIT(BF_STAGE_FREE);  // part[1] shares LDS with the stage
     lds_put_gej(S.u.part[1], T, l);
     S.pinf[1][l] = tinf ? 1u : 0u;
-    mflag_set(&S.flag[BF_Q2]);
+    BFLAG_SET(BF_Q2);
     stamp_out();
     return;
   }
   // ---- Y1: the joins and the address
-  mflag_wait(&S.flag[BF_Q2]);
+  BFLAG_WAIT(BF_Q2);
   bool qinf, oinf;
   gej Q = join_mid(T, tinf, lds_get_gej(S.u.part[1], l), S.pinf[1][l] != 0, qinf, dg);
-  mflag_wait(&S.flag[BF_Y]);
+  BFLAG_WAIT(BF_Y);
   fe y;
   lds_get_fe<FE_LIMBS>(S.y, y.v, l);
   const bool yok = S.yok[l] != 0;
   Q.z = fe_mul(Q.z, y);  // E' -> E: (X, Y, Z) is (X, Y, Z y)
-  mflag_wait(&S.flag[BF_G]);
+  BFLAG_WAIT(BF_G);
   st_.mark(5);
   Q = join_mid(Q, qinf, lds_get_gej(S.u.part[0], l), S.pinf[0][l] != 0, oinf, dg);
   qinf = oinf;
   if (wire) {
-    mflag_wait(&S.flag[BF_PARSED]);
+    BFLAG_WAIT(BF_PARSED);
     q.meta = S.meta[l];
   }
-  const bool ok = (wire ? S.pok[l] != 0 : pok) && yok && !qinf;  // main_impl.h:120
+  const bool fault = ho_failed(&S.flag[BF_ERR], dg);  // after Y1's last wait
+  const bool ok = (wire ? S.pok[l] != 0 : pok) && yok && !qinf && !fault;  // main_impl.h:120
   if (__any(ok && fe_is_zero(Q.z))) diag_bump(dg, EGES_DIAG_MID_EXC);  // never (see above)
   st_.mark(5);
   const fe zq = fe_select(ok, Q.z, fe_one());
@@ -879,7 +858,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
   st_.mark(6);
   if (live) {
     const uint32_t pre_st = (q.meta >> 8) & 0xffu;
-    prm.status[idx] = (uint8_t)(pre_st != ST_OK ? pre_st : (ok ? ST_OK : ST_RECOVER_FAILED));
+    prm.status[idx] = (uint8_t)(fault ? ST_ENGINE_FAULT : pre_st != ST_OK ? pre_st : (ok ? ST_OK : ST_RECOVER_FAILED));
     if (prm.addr) {
       uint32_t a[5];
       pub_address(a, X, Y);

@@ -3,7 +3,8 @@
 // Knobs are read from the environment ONCE, at the first eges_init, and are otherwise changed
 // only through eges_test_set_knob (include/eges.h): no call path after init reads the
 // environment (getenv racing a host application's setenv is undefined behaviour in glibc).
-// The values are atomics, so a test may flip one between calls while other threads run.
+// The values are atomics, so a test may flip one while other threads run; a call snapshots the
+// routing knobs once at its start (capi.hip Route), so a change takes effect from the next call.
 #pragma once
 #include <stdint.h>
 
@@ -24,6 +25,8 @@ enum KnobId : int {
   KNOB_COALESCE_GATHER_US,  // single-item coalescer: a leader's gather window
   KNOB_COALESCE_SPIN_US,    //   a waiting caller spins this long before it blocks
   KNOB_COALESCE_SPINNERS,   //   at most this many callers spin at once
+  KNOB_TEST_SKIP_FLAG,    // tests: k > 0 makes the first workgroup's producer of hand-off flag k - 1
+                          //   skip publishing it (handoff.cuh), so its consumers time out
   KNOB_COUNT
 };
 

@@ -47,6 +47,9 @@ struct RecoverParams {
   uint32_t* diag = nullptr;
   // tests only (KNOB_FORCE_REDO): run every exact-redo pass as if an accumulator was poisoned
   uint32_t force_redo = 0;
+  // tests only (KNOB_TEST_SKIP_FLAG, handoff.cuh): workgroup test_skip_block's producer of hand-off
+  // flag test_skip_flag - 1 skips publishing it
+  uint32_t test_skip_flag = 0, test_skip_block = 0;
   // mid-size bucket form only: wire-format transactions instead of record rows (tx_rows_kernel
   // and prep_sender_kernel fused in): item i is wire_raw[wire_off[first + i] - wire_off[0],
   // wire_off[first + i + 1] - wire_off[0]); wire_raw 4-byte aligned. wire_sighash: n x 32 or null.
@@ -73,6 +76,7 @@ struct VerifyParams {
   uint32_t* counts;   // 2 counters for the order kernel
   uint32_t* diag = nullptr;   // as RecoverParams
   uint32_t force_redo = 0;
+  uint32_t test_skip_flag = 0, test_skip_block = 0;
 };
 // Verify scratch: slot rows (P affine, prefix product of s), the order, the two counters.
 constexpr int VERIFY_SLOT_ROWS = 7;

@@ -39,15 +39,24 @@ def all_gather_records(local, n, group=None):
     backend) or on the CPU (gloo). Every shard is padded to ceil(n / world) records so the
     collective is one fixed-size all-gather; the result is the [n, 21] batch in index order on
     every rank. It is outside the recovery path: bench.py's timed region never calls it.
+
+    The ranks first agree on whether every shard is well formed (one MIN all-reduce of a 0/1
+    flag), so a bad shard on one rank raises ValueError on every rank instead of leaving the
+    others blocked in the all-gather until the process-group timeout.
     """
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     lo, hi = shard_range(n, rank, world)
-    if local.dtype != torch.uint8 or local.dim() != 2 or local.shape != (hi - lo, RECORD):
+    good = local.dtype == torch.uint8 and local.dim() == 2 and tuple(local.shape) == (hi - lo, RECORD)
+    flag = torch.tensor([1 if good else 0], dtype=torch.int32, device=local.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    if not good:
         raise ValueError(f"rank {rank}: expected uint8 [{hi - lo}, {RECORD}] records, got "
                          f"{local.dtype} {tuple(local.shape)}")
+    if int(flag.item()) == 0:
+        raise ValueError(f"rank {rank}: another rank passed a malformed shard; no records exchanged")
     per = -(-n // world) if n else 0
     if per == 0:
         return local.new_zeros((0, RECORD))

@@ -41,8 +41,13 @@ typedef enum eges_status {
     EGES_INVALID_SIG_LEN = 4,     /* secp256k1.ErrInvalidSignatureLen  secp256.go:56 */
     EGES_INVALID_RECOVERY_ID = 5, /* secp256k1.ErrInvalidRecoveryID    secp256.go:57 */
     EGES_RECOVER_FAILED = 6,      /* secp256k1.ErrRecoverFailed        secp256.go:61 */
-    EGES_DECODE_FAILED = 7        /* rlp.DecodeBytes(raw, tx) error (transaction.go:157-165, rlp/decode.go):
+    EGES_DECODE_FAILED = 7,       /* rlp.DecodeBytes(raw, tx) error (transaction.go:157-165, rlp/decode.go):
                                      wire-format entries only; the reference never calls Sender */
+    EGES_ENGINE_FAULT = 255       /* not a reference error: an internal hand-off between the waves of a
+                                     kernel workgroup timed out, and the item got no result (no address
+                                     is written). Host-buffer entries then return EGES_E_HIP; *_dev
+                                     entries leave it in the status byte (and EGES_DIAG_HANDOFF counts
+                                     it). Never produced by a call that returns EGES_SUCCESS. */
 } eges_status;
 
 /* Call-level return codes. */
@@ -137,8 +142,10 @@ int eges_sender_raw_batch(const uint8_t *raw, const uint64_t *offsets, size_t n,
  * structure (or a selected transaction) would make rlp.DecodeBytes fail; header, uncle and
  * confirm-message field contents are not decoded; the transactions of unselected lists are
  * decoded (not recovered) on the GPU, as rlp.DecodeBytes decodes them too. Returns
- * EGES_E_INVALID_ARG when more than cap transactions are selected; *block_status and counts are
- * then still valid (a sizing call). */
+ * EGES_E_INVALID_ARG when more than cap transactions are selected (a sizing call): counts are
+ * then valid, and *block_status covers the block's list structure only (EGES_DECODE_FAILED for a
+ * structure error; EGES_OK does not yet mean that every transaction decodes, since none was
+ * decoded). */
 #define EGES_LIST_FAKE 0x1u
 #define EGES_LIST_GEEC 0x2u
 #define EGES_LIST_TXS 0x4u
@@ -215,6 +222,7 @@ int eges_synth_sign_msg_dev(int device, uint64_t first_index, size_t n, const ui
 #define EGES_DIAG_MID_REDO 7  /* mid-size kernel: exact redo of an R' Strauss part */
 #define EGES_DIAG_MID_EXC 8   /* mid-size kernel: checked addition met P == +-Q */
 #define EGES_DIAG_MID_JOIN 9  /* mid-size kernel: partial sums joined with a == +-b */
+#define EGES_DIAG_HANDOFF 10  /* a wave hand-off timed out: the workgroup's items got EGES_ENGINE_FAULT */
 #define EGES_DIAG_COUNT 16
 /* Copies min(n, EGES_DIAG_COUNT) counters of `device` (summed over the engine's instances of
  * it) into out; reset != 0 zeroes them afterwards. Synchronises the device. */
@@ -222,7 +230,8 @@ int eges_diag_counters(int device, uint64_t *out, size_t n, int reset);
 
 /* Engine knobs. Read from the environment once, at the first eges_init (EGES_LAT_MAX,
  * EGES_LAT_WIDE_MAX, EGES_MID_MAX, EGES_TXROWS_WAVE_MAX, EGES_TEST_ROOT_HELPERS, EGES_OVERLAP,
- * EGES_TEST_FORCE_REDO); no call path reads the environment after that. These two entries
+ * EGES_TEST_FORCE_REDO, EGES_TEST_SKIP_FLAG, ...); no call path reads the environment after that.
+ * A call reads the routing knobs once, at its start: a change takes effect from the next call. These two entries
  * change / read one by its environment name while the engine runs (tests and A/B tools; the
  * product defaults need neither). Return EGES_E_INVALID_ARG for an unknown name. */
 int eges_test_set_knob(const char *name, long long value);

@@ -96,6 +96,12 @@ def _rank_all_gather(rank, world, port, n, q):
         all_gather_records(torch.zeros((hi - lo + 1, 21), dtype=torch.uint8), n)
     except ValueError:
         bad = 1
+    # only rank 1's shard is malformed: both ranks must raise (no rank left in the all-gather)
+    shard = torch.from_numpy(_records(range(lo, hi + (1 if rank == 1 else 0))))
+    try:
+        all_gather_records(shard, n)
+    except ValueError:
+        bad += 1
     q.put((rank, got.numpy().copy(), bad))
     dist.barrier()
     dist.destroy_process_group()
@@ -119,7 +125,7 @@ def test_gloo_all_gather_records_every_rank(n):
     want = _records(range(n))
     for rank, got, bad in outs:
         assert got.shape == (n, 21) and np.array_equal(got, want), rank
-        assert bad == 1  # a shard of the wrong size is refused before the collective
+        assert bad == 2  # a shard of the wrong size (on every rank, or on one) is refused on every rank
 
 
 def _bench(args, env_extra=None, timeout=240):
