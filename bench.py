@@ -402,6 +402,9 @@ def run_throughput(c, strong):
         sec["c3_block_wire"] = measure_block(c, 1000, raw_mode=True, warmup=3, iters=50, cpu=False)
         sec["c1_transfers"] = measure_c1(c, 10000, warmup=3, iters=20, cpu=False)
         sec["c5_adversarial"] = measure_c5(c, B, msg, sig, exp_addr, steps=1, warmup=1)
+        # as many synchronous callers as the reference baseline's threads (the box's granted CPUs)
+        ref = cpu if cpu and cpu.get("kind") == "reference" else None
+        sec["single"] = measure_single(ref["cores"] if ref else 16, 2000, ref["value"] if ref else None)
         line["secondary"] = sec
         ok = ok and all(v.get("correct", True) for v in sec.values() if isinstance(v, dict))
         line["config"]["correct"] = ok
@@ -433,16 +436,30 @@ def measure_block(c, n, raw_mode, warmup, iters, cpu=True):
     sig_h, exp_h = sig_d.cpu().numpy(), exp_d.cpu().numpy()
     r, s, v = txs.sender_rows(sig_h, txs.GEEC_CHAIN_ID)
     if raw_mode:  # the block's transactions as the wire carries them (10-field Geec txdata RLP)
-        packed = c.eges.pack_raw(txs.geec_block_raw(0, sig_h, payload=100))
+        raw, offs = c.eges.pack_raw(txs.geec_block_raw(0, sig_h, payload=100))
+    # the C-ABI call itself on preallocated host buffers (what a cgo caller pays), not the numpy
+    # wrapper: every timed call's outputs are checked after it
+    from eges_amd._lib import check, lib
+    addr = np.zeros((n, 20), np.uint8)
+    st = np.zeros(n, np.uint8)
+    P = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+    vf = np.zeros(n, np.uint8)
+    if raw_mode:
+        args = (P(raw), P(offs), n, SIGNER_EIP155, txs.GEEC_CHAIN_ID, P(addr), P(st), None)
+        fn = lib.eges_sender_raw_batch
+    else:
+        sighash, r, s, v = (np.ascontiguousarray(x) for x in (sighash, r, s, v))
+        args = (P(sighash), P(r), P(s), P(v), P(vf), n, SIGNER_EIP155, txs.GEEC_CHAIN_ID, P(addr), P(st))
+        fn = lib.eges_sender_batch
     lat = []
     ok = True
     for i in range(warmup + iters):
+        addr.fill(0)
+        st.fill(0xEE)
         t0 = time.perf_counter()
-        if raw_mode:
-            addr, st, _ = c.eges.sender_raw_batch(packed, SIGNER_EIP155, txs.GEEC_CHAIN_ID)
-        else:
-            addr, st = c.eges.sender_batch(sighash, r, s, v, None, SIGNER_EIP155, txs.GEEC_CHAIN_ID)
+        rc = fn(*args)
         dt = time.perf_counter() - t0
+        check(rc)
         if i >= warmup:
             lat.append(dt)
         ok = ok and bool((st == 0).all()) and np.array_equal(addr, exp_h)
@@ -451,7 +468,7 @@ def measure_block(c, n, raw_mode, warmup, iters, cpu=True):
            "blocks": iters, "txs": n, "correct": ok,
            "path": ("wire-format txdata RLP through eges_sender_raw_batch (H2D + decode + sighash RLP/Keccak + "
                     "recovery kernels + D2H)" if raw_mode else "host buffers through eges_sender_batch (H2D + "
-                    "kernels + D2H)")}
+                    "kernels + D2H)") + "; timed around the C-ABI call (ctypes, preallocated outputs)"}
     if cpu:
         out["cpu"] = None
         try:
@@ -486,6 +503,33 @@ def run_block_latency(c):
             "config": {"workload": "configs[2]: Geec block import, 1000 txns/block (txnSize 100), EIP155Signer(930412), "
                                    + m["path"], "correct": m["correct"]}, "cpu_baseline": m.get("cpu")}
     c.finish(line, m["correct"])
+
+
+# ------------------------------------------------------------------ single-item seam
+def measure_single(callers=16, calls=2000, ref_rate=None):
+    """The per-call cgo seam (eges_ecdsa_recover, replacing ext.h:30-47 under
+    crypto.Ecrecover, signature_cgo.go:31-44): tools/single_bench (native threads, built by
+    build()) as a child process on the same GPU: one caller's p50 / p99, then `callers` synchronous
+    callers x `calls` calls, every result checked. ref_rate: the reference libsecp256k1 on the same
+    host with the same number of threads, each calling secp256k1_ext_ecdsa_recover once per item
+    (oracle/_ref eref_ecrecover_batch_mt = cpu_baseline)."""
+    exe = os.path.join(ROOT, "tools", "single_bench")
+    if not os.path.exists(exe):
+        return {"note": "tools/single_bench not built", "correct": True}
+    try:
+        cp = subprocess.run([exe, str(callers), str(calls)], capture_output=True, text=True, timeout=240)
+        m = json.loads(cp.stdout.strip().splitlines()[-1])
+    except Exception as e:  # noqa: BLE001
+        return {"note": f"single_bench failed: {e}", "correct": False}
+    out = {"p50_ms_one_caller": m["p50_ms_one_caller"], "p99_ms_one_caller": m["p99_ms_one_caller"],
+           "verify_p50_ms_one_caller": m["verify_p50_ms_one_caller"], "callers": callers,
+           "calls_per_caller": calls, "recoveries_per_s": m["recoveries_per_s"], "errors": m["errors"],
+           "correct": m["errors"] == 0 and cp.returncode == 0,
+           "path": "eges_ecdsa_recover (the per-call seam; concurrent callers coalesced into shared launches)"}
+    if ref_rate:
+        out["reference_same_threads_per_s"] = ref_rate
+        out["vs_reference"] = round(m["recoveries_per_s"] / ref_rate, 3)
+    return out
 
 
 # ------------------------------------------------------------------ c1: 10k EIP-155 transfers

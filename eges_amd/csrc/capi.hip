@@ -365,6 +365,20 @@ static hipError_t stamp_buf(size_t waves, hipStream_t st) {
 #endif
 
 size_t dev_ws_bytes(const Dev& d) { return ws_bytes_per_block() * (size_t)d.ws_blocks; }
+
+// Host-side phase stamps of the last host-buffer call (diagnostic build only, tools/block_bench):
+// 0 entry, 1 lane / device acquired, 2 inputs packed, 3 launches enqueued, 4 streams drained,
+// 5 outputs unpacked (steady_clock, ns).
+#ifdef EGES_PHASE_STAMPS
+static int64_t g_hstamp[6];
+#define HSTAMP(k) (g_hstamp[k] = std::chrono::steady_clock::now().time_since_epoch().count())
+extern "C" size_t eges_diag_host_stamps(int64_t* out, size_t n) {
+  for (size_t k = 0; k < n && k < 6; ++k) out[k] = g_hstamp[k];
+  return 6;
+}
+#else
+#define HSTAMP(k) ((void)0)
+#endif
 // batches (or chunks) the mid-size kernel takes: above LAT_MAX, up to MID_MAX and what the
 // device workspace holds
 // The bucket form (k_recover_mid.hip) holds 138 KB of LDS: one workgroup per CU. It is the
@@ -631,6 +645,7 @@ Region region_for(const HostJob& j, size_t base, size_t m) {
 // i-1's outputs (host order H2D(i+1), K(i+1), D2H(i): the pageable D2H blocks this thread
 // until K(i) is done, by which time K(i+1) is queued behind it). Synchronous overall.
 int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t cnt) {
+  HSTAMP(0);
   DevGuard g(d.id);
   // a shard big enough to pipeline runs as >= 2 chunks (each still a full resident grid)
   size_t c = std::min(CHUNK, cnt);
@@ -690,6 +705,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     HIPCHK(hipStreamWaitEvent(st, d.last, 0));
     HIPCHK(hipStreamWaitEvent(sx, d.last, 0));
   }
+  HSTAMP(1);
   // Input staging: each input array goes to its offset in the region, either by its own
   // (pageable) copy into device memory on the copy stream, or, for a pinned call, packed into
   // the pinned buffer at the same offset, where the kernels read it directly (zero-copy: no
@@ -714,6 +730,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   do {                              \
     int rc_ = flush_in(B);          \
     if (rc_) return rc_;            \
+    HSTAMP(2);                      \
   } while (0)
   // the kernels wait for their inputs' copies (a single chunk uses one stream: nothing to join)
 #define JOIN_IN(r)                                      \
@@ -866,6 +883,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       if (small || m <= rt.lat_max) HIPCHK(launch_verify_lat(p, p.n <= rt.wide_max, st));
       else HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
     }
+    HSTAMP(3);
     if (sx != st) HIPCHK(hipEventRecord(ev_k[r], st));
     // --- the previous chunk's outputs, while this chunk computes
     if (have_prev) {
@@ -882,8 +900,10 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   if (!small) HIPCHK(hipEventRecord(d.last, sx));
   HIPCHK(hipStreamSynchronize(sx));
   if (sx != st) HIPCHK(hipStreamSynchronize(st));  // (st's last work is already behind sx's events)
+  HSTAMP(4);
   drain.armed = false;
   if (pinned && have_prev) unpack(prev);
+  HSTAMP(5);
   // items a kernel marked EGES_ENGINE_FAULT (a wave hand-off timed out, handoff.cuh) have no
   // result: the call fails rather than return them
   if (j.status && !j.decode_only && std::memchr(j.status + off, EGES_ENGINE_FAULT, cnt))

@@ -11,3 +11,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 tail -1 $O/pytest_gpu.txt
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err
 cat $O/bench.json
+timeout -k 10 120 tools/block_bench 1000 300 > $O/block_bench.json 2>&1
+cat $O/block_bench.json
+timeout -k 10 120 tools/block_bench_diag 1000 300 > $O/block_bench_diag.json 2>&1
+cat $O/block_bench_diag.json
