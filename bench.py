@@ -55,16 +55,16 @@ METRIC = "secp256k1 ecrecover+address/sec at 1/8 MI355X; % of INT32 VALU peak"
 # algorithm = 80 x 3085.2 field ops + 128 x 301 scalar ops + 6,300 (Keccak-f) = 291,644.
 W_RECOVER = 291_644
 W_VERIFY65 = 242_216
-# INT32 VALU peak of one MI355X for the multiply/carry instruction class the kernel is made of
-# (256 CU x 64 lane-ops/clk x 2.4 GHz; tools/ubench_valu.hip measures
-# v_mad_u64_u32 / v_add_co / v_addc at 4.4-4.9 cyc per wave64 instruction per SIMD, i.e. this
-# rate; only v_add_u32/v_bitop3 issue at the 2x rate).
-PEAK_INT32_OPS = 256 * 64 * 2.4e9  # 3.93e13 lane-ops/s
-# The same achieved rate against two other named denominators (bench line "peaks_T"):
-#  - the guide (MI355X_MICROARCH.md): one wave64 VALU instruction per 2 cycles per SIMD,
-#    1024 SIMDs x 32 lane-ops/clk x 2.4 GHz = 7.86e13 (full-rate 32-bit ops);
+# The roofline's `peak` / `frac`: the guide's INT32 VALU peak (MI355X_MICROARCH.md "Wave
+# scheduling": one wave64 VALU instruction per 2 cycles per SIMD), 1024 SIMDs x 32 lane-ops/clk x
+# 2.4 GHz = 7.86e13 lane-ops/s. The same achieved rate is also given against two named ceilings
+# of the instruction class the kernel is made of (bench line "peaks_T"):
+#  - SURVEY.md §8(d)'s contract, 256 CU x 64 lane-ops/clk x 2.4 GHz = 3.93e13: the 64-bit MAD /
+#    carry class issues at half the full rate (tools/ubench_valu.hip: v_mad_u64_u32 / v_add_co /
+#    v_addc 4.4-4.9 cyc per wave64 instruction per SIMD; only v_add_u32 / v_bitop3 at ~2.5);
 #  - measured: v_mad_u64_u32 at 4 waves/SIMD, 31.6e12 lane-ops/s (profiles/r01/ubench_valu.txt).
 PEAK_GUIDE_VALU = 1024 * 32 * 2.4e9
+PEAK_INT32_OPS = 256 * 64 * 2.4e9  # SURVEY contract / MAD-class ceiling, 3.93e13 lane-ops/s
 PEAK_MEASURED_MAD = 31.61e12
 C4_TOTAL = 64 << 20
 
@@ -187,8 +187,9 @@ def kernel_src_hash():
 
 
 def read_pmc(kernel, batch):
-    """Counter summary of `kernel` at `batch` from profiles/pmc_traffic.json (tools/pmc.sh +
-    tools/pmc_summary.py), only when it was collected from the same kernel sources; else None."""
+    """Counter summary of `kernel` launched on `batch` items, from profiles/pmc_traffic.json
+    (tools/pmc.sh + tools/pmc_summary.py: one entry per (config, kernel), each with its own launch
+    size), only when it was collected from the same kernel sources; else None."""
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(tf) as f:
@@ -197,10 +198,10 @@ def read_pmc(kernel, batch):
         return None
     if tj.get("src_sha256") != kernel_src_hash():
         return None
-    ent = tj.get("kernels", {}).get(kernel)
-    if not ent or ent.get("batch") != batch:
-        return None
-    return ent
+    for ent in tj.get("entries", []):
+        if ent.get("kernel") == kernel and ent.get("batch") == batch:
+            return ent
+    return None
 
 
 class Ctx:
@@ -309,14 +310,18 @@ def roofline(per_gpu_rate, work, batch, kern_ms, kernel="eges::recover_kernel"):
     the measured v_mad_u64_u32 rate, each named. With a PMC summary of the same kernel sources:
     HBM-side traffic and the counter-derived VALU utilisation."""
     achieved = per_gpu_rate * work
-    r = {"bound": "valu", "achieved": round(achieved / 1e12, 3), "peak": round(PEAK_INT32_OPS / 1e12, 2),
-         "unit": "T INT32 lane-ops/s (reference-algorithm accounting, SURVEY.md 8(d))",
-         "frac": round(achieved / PEAK_INT32_OPS, 4),
-         "frac_vs_guide_valu_issue": round(achieved / PEAK_GUIDE_VALU, 4),
+    r = {"bound": "valu", "kernel": kernel, "batch": batch, "achieved": round(achieved / 1e12, 3),
+         "peak": round(PEAK_GUIDE_VALU / 1e12, 2),
+         "unit": "T INT32 lane-ops/s (reference-algorithm accounting, SURVEY.md 8(d); peak: MI355X_MICROARCH.md "
+                 "VALU issue, 1024 SIMDs x 32 lanes/clk x 2.4 GHz)",
+         "frac": round(achieved / PEAK_GUIDE_VALU, 4),
+         "frac_vs_survey_contract": round(achieved / PEAK_INT32_OPS, 4),
          "frac_vs_measured_mad_rate": round(achieved / PEAK_MEASURED_MAD, 4),
-         "peaks_T": {"contract": round(PEAK_INT32_OPS / 1e12, 2), "guide_valu_issue": round(PEAK_GUIDE_VALU / 1e12, 2),
+         "peaks_T": {"guide_valu_issue": round(PEAK_GUIDE_VALU / 1e12, 2),
+                     "survey_contract_mad_class": round(PEAK_INT32_OPS / 1e12, 2),
                      "measured_v_mad_u64_u32": round(PEAK_MEASURED_MAD / 1e12, 2)},
-         "traffic": None, "kernel_ms": round(kern_ms, 3)}
+         "traffic": None, "kernel_ms": round(kern_ms, 4),
+         "kernel_ms_source": "HIP events on the launch stream around each timed step"}
     pmc = read_pmc(kernel, batch)
     if pmc:
         # FETCH_SIZE (KB, x2: gfx950 correction) + WRITE_SIZE (KB): L2 <-> fabric (MALL / HBM) bytes
@@ -325,11 +330,14 @@ def roofline(per_gpu_rate, work, batch, kern_ms, kernel="eges::recover_kernel"):
         if insts and batch:
             lane_insts = insts * 64
             r["counters"] = {
-                "source": "profiles/pmc_traffic.json (PMC passes of the same kernel sources, src_sha256)",
+                "source": f"profiles/pmc_traffic.json entry {pmc.get('config')}/{kernel} (PMC passes of the same "
+                          "kernel sources, src_sha256), per launch of this batch size",
                 "valu_lane_insts_per_sig": round(lane_insts / batch),
+                "salu_insts_per_sig": round(pmc["SQ_INSTS_SALU"] / batch, 1) if pmc.get("SQ_INSTS_SALU") else None,
                 "int64_class_share": round(pmc.get("SQ_INSTS_VALU_INT64", 0) / insts, 4),
-                "valu_util_vs_contract": round(lane_insts / (kern_ms / 1e3) / PEAK_INT32_OPS, 4),
-                "valu_util_vs_guide": round(lane_insts / (kern_ms / 1e3) / PEAK_GUIDE_VALU, 4)}
+                "waves_per_launch": pmc.get("SQ_WAVES"),
+                "valu_util_vs_guide": round(lane_insts / (kern_ms / 1e3) / PEAK_GUIDE_VALU, 4),
+                "valu_util_vs_survey_contract": round(lane_insts / (kern_ms / 1e3) / PEAK_INT32_OPS, 4)}
     return r
 
 
@@ -423,6 +431,22 @@ def run_stub(c, B):
 
 
 # ------------------------------------------------------------------ c3: Geec block latency
+def dev_kernel_ms(c, step, reps=20, warmup=3):
+    """Mean span of one device-resident launch of `step` (everything on the bench stream c.sp),
+    from HIP events around each launch: the dominant kernel's duration for a one-kernel step."""
+    torch = c.torch
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for e0, e1 in evs:
+        e0.record(c.stream)
+        step()
+        e1.record(c.stream)
+    torch.cuda.synchronize()
+    return sum(a.elapsed_time(b) for a, b in evs) / reps
+
+
 def measure_block(c, n, raw_mode, warmup, iters, cpu=True):
     """A Geec block of n EIP-155 transactions (100-byte payload) through eges_sender_batch (host
     buffers) or, raw_mode, as wire bytes through eges_sender_raw_batch: per-block latency."""
@@ -464,8 +488,23 @@ def measure_block(c, n, raw_mode, warmup, iters, cpu=True):
             lat.append(dt)
         ok = ok and bool((st == 0).all()) and np.array_equal(addr, exp_h)
     lat = np.array(lat) * 1e3
+    # the dominant kernel's roofline: the same block device-resident through the *_dev entry (one
+    # launch with the sender rows / wire bytes classified in-kernel), HIP events on the bench stream
+    if raw_mode:
+        rd, od = torch.from_numpy(raw).to(c.dev), torch.from_numpy(offs.astype(np.int64)).to(c.dev)
+        ad, sd = torch.empty((n, 20), dtype=torch.uint8, device=c.dev), torch.empty(n, dtype=torch.uint8, device=c.dev)
+        kms = dev_kernel_ms(c, lambda: c.eges.sender_raw_batch_dev(rd, od, SIGNER_EIP155, txs.GEEC_CHAIN_ID, addr=ad,
+                                                                   status=sd, stream=c.sp))
+    else:
+        hd, rr, sr, vr, vd = (torch.from_numpy(np.ascontiguousarray(x)).to(c.dev) for x in (sighash, r, s, v, vf))
+        ad, sd = torch.empty((n, 20), dtype=torch.uint8, device=c.dev), torch.empty(n, dtype=torch.uint8, device=c.dev)
+        kms = dev_kernel_ms(c, lambda: c.eges.sender_batch_dev(hd, rr, sr, vr, vd, SIGNER_EIP155, txs.GEEC_CHAIN_ID,
+                                                               addr=ad, status=sd, stream=c.sp))
+    torch.cuda.synchronize()
+    ok = ok and bool((sd == 0).all().item()) and np.array_equal(ad.cpu().numpy(), exp_h)
     out = {"median_ms": round(float(np.median(lat)), 3), "p99_ms": round(float(np.percentile(lat, 99)), 3),
            "blocks": iters, "txs": n, "correct": ok,
+           "roofline": roofline(n / (kms / 1e3), W_RECOVER, n, kms, kernel="eges::recover_lat_kernel"),
            "path": ("wire-format txdata RLP through eges_sender_raw_batch (H2D + decode + sighash RLP/Keccak + "
                     "recovery kernels + D2H)" if raw_mode else "host buffers through eges_sender_batch (H2D + "
                     "kernels + D2H)") + "; timed around the C-ABI call (ctypes, preallocated outputs)"}
@@ -555,9 +594,20 @@ def measure_c1(c, n, warmup, iters, cpu=True):
             lat.append(dt)
         ok = ok and bool((st == 0).all()) and np.array_equal(addr, exp_h)
     med = float(np.median(lat))
+    # the dominant kernel's roofline: the batch device-resident through eges_sender_raw_batch_dev
+    # (one launch of the bucket form with decode + sighash fused in), HIP events on the bench stream
+    raw, offs = packed
+    rd, od = torch.from_numpy(raw).to(c.dev), torch.from_numpy(offs.astype(np.int64)).to(c.dev)
+    ad, sd = torch.empty((n, 20), dtype=torch.uint8, device=c.dev), torch.empty(n, dtype=torch.uint8, device=c.dev)
+    kms = dev_kernel_ms(c, lambda: c.eges.sender_raw_batch_dev(rd, od, SIGNER_EIP155, txs.GEEC_CHAIN_ID, addr=ad,
+                                                               status=sd, stream=c.sp))
+    torch.cuda.synchronize()
+    ok = ok and bool((sd == 0).all().item()) and np.array_equal(ad.cpu().numpy(), exp_h)
     out = {"txs_per_s": round(n / med, 1), "median_ms": round(med * 1e3, 3),
            "p99_ms": round(float(np.percentile(np.array(lat) * 1e3, 99)), 3), "txs": n, "batches": iters,
-           "correct": ok}
+           "correct": ok,
+           "roofline": dict(roofline(n / (kms / 1e3), W_RECOVER, n, kms, kernel="eges::recover_bkt_kernel"),
+                            note="W excludes the fused RLP decode and signing-hash Keccak (conservative)")}
     if cpu:
         out["cpu"] = None
         try:

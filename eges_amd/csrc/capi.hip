@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <memory>
 #include <atomic>
 #include <mutex>
@@ -141,6 +142,7 @@ const KnobDef KNOB_DEFS[KNOB_COUNT] = {
     {"EGES_COALESCE_GATHER_US", 20},
     {"EGES_COALESCE_SPIN_US", 2000},
     {"EGES_COALESCE_SPINNERS", 8},
+    {"EGES_SENDER_FUSED", 1},
     {"EGES_TEST_SKIP_FLAG", 0},
 };
 std::atomic<long long> g_knob[KNOB_COUNT];
@@ -167,7 +169,7 @@ int knob_index(const char* name) {
 struct Route {
   size_t lat_max = 0, mid_max = 0;
   uint32_t wide_max = 0;
-  long long mid_form = 1, wire_fused = 1, overlap = -1;
+  long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1;
   uint32_t force_redo = 0, skip_flag = 0;
   static Route now() {
     Route r;
@@ -177,6 +179,7 @@ struct Route {
     r.mid_form = knob(KNOB_MID_FORM);
     r.wire_fused = knob(KNOB_WIRE_FUSED);
     r.overlap = knob(KNOB_OVERLAP);
+    r.sender_fused = knob(KNOB_SENDER_FUSED);
     r.force_redo = knob(KNOB_FORCE_REDO) != 0 ? 1u : 0u;
     r.skip_flag = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TEST_SKIP_FLAG), 64));
     return r;
@@ -396,6 +399,23 @@ bool use_mid(const Dev& d, const Route& rt, size_t n) {
 }
 // the recover kernels that parse msg / sig bytes themselves (no prep launch)
 bool fused_parse(const Dev& d, const Route& rt, size_t n) { return n <= rt.lat_max || use_mid(d, rt, n); }
+// ... and classify types.Sender rows themselves (no prep_sender launch): 4-byte aligned rows only
+bool sender_fused(const Dev& d, const Route& rt, size_t n, std::initializer_list<const void*> rows) {
+  if (rt.sender_fused == 0 || !fused_parse(d, rt, n)) return false;
+  for (const void* q : rows)
+    if (((uintptr_t)q & 3u) != 0) return false;
+  return true;
+}
+void bind_sender_rows(RecoverParams& p, const uint8_t* h, const uint8_t* r, const uint8_t* s, const uint8_t* v,
+                      const uint8_t* f, int signer, uint64_t chain_id) {
+  p.snd_h = h;
+  p.snd_r = r;
+  p.snd_s = s;
+  p.snd_v = v;
+  p.snd_f = f;
+  p.snd_signer = signer;
+  p.snd_chain_id = chain_id;
+}
 
 hipError_t launch_recover_pass(Dev& d, const Route& rt, const RecoverParams& p0, hipStream_t st) {
   RecoverParams p = with_diag(d, p0, rt);
@@ -403,6 +423,7 @@ hipError_t launch_recover_pass(Dev& d, const Route& rt, const RecoverParams& p0,
   p.wide = p.n <= rt.wide_max ? 1u : 0u;
   const bool mid = use_mid(d, rt, p.n);
   if (p.wire_raw && !(mid ? mid_bucket(d, rt, p.n) : p.n <= rt.lat_max)) return hipErrorInvalidValue;  // wire_fused() decides
+  if (p.snd_r && !(mid || p.n <= rt.lat_max)) return hipErrorInvalidValue;  // sender_fused() decides
 #ifdef EGES_PHASE_STAMPS
   if (mid) {
     hipError_t e = stamp_buf((p.n + 63) / 64 * 4, st);  // one row per wave
@@ -507,9 +528,13 @@ int run_sender_dev(Dev& d, const Route& rt, const uint8_t* sighash, const uint8_
   Serial ser(d, st);
   for (size_t off = 0; off < n; off += CHUNK) {
     const uint32_t m = (uint32_t)std::min(CHUNK, n - off);
-    HIPCHK(launch_prep_sender(sighash + off * 32, r + off * 32, s + off * 32, v + off * 32, vflags ? vflags + off : nullptr,
-                              m, (uint32_t)n_pad, signer, chain_id, rec, st));
     RecoverParams p{rec, m, (uint32_t)n_pad, status + off, addr + off * 20, nullptr, d.gtab, d.ws};
+    const uint8_t *h_ = sighash + off * 32, *r_ = r + off * 32, *s_ = s + off * 32, *v_ = v + off * 32;
+    const uint8_t* f_ = vflags ? vflags + off : nullptr;
+    if (sender_fused(d, rt, m, {h_, r_, s_, v_}))
+      bind_sender_rows(p, h_, r_, s_, v_, f_, signer, chain_id);
+    else
+      HIPCHK(launch_prep_sender(h_, r_, s_, v_, f_, m, (uint32_t)n_pad, signer, chain_id, rec, st));
     HIPCHK(launch_recover_pass(d, rt, p, st));
   }
   return EGES_SUCCESS;
@@ -818,9 +843,12 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       if (j.e) H2D(B, df, j.e + base, m);
       FLUSH_IN(B);
       JOIN_IN(r);
-      HIPCHK(launch_prep_sender(dh, dr, dsv, dv, j.e ? df : nullptr, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id,
-                                rec, st));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
+      if (sender_fused(d, rt, m, {dh, dr, dsv, dv}))  // the recover kernel reads the rows itself
+        bind_sender_rows(p, dh, dr, dsv, dv, j.e ? df : nullptr, j.signer, j.chain_id);
+      else
+        HIPCHK(launch_prep_sender(dh, dr, dsv, dv, j.e ? df : nullptr, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id,
+                                  rec, st));
       HIPCHK(launch_recover_pass(d, rt, p, st));
     } else if (j.kind == HostJob::PRECOMPILE) {
       uint8_t* din = I;

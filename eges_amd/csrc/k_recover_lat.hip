@@ -691,7 +691,7 @@ DEV void root_helper(const RecoverParams& prm) {
     Payload m;
     wire_item(prm.wire_raw + ra, len, sp, prm.wire_signer, prm.wire_chain_id, q, m);
   } else {
-    q = lat_parse(prm, j);
+    q = prm.snd_r ? sender_parse_lane(prm, j) : lat_parse(prm, j);
   }
   const ge G = gen_point();
   const fe x = q.ok ? fe_from_u256(q.xr) : G.x;  // the row-form waves use the same substitute
@@ -786,7 +786,7 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
     decoded = wire_item(p, wlen, wspan, prm.wire_signer, prm.wire_chain_id, q, m);
     q.Z = sc_zero();  // (wave 1 hashes m for z)
   } else {
-    q = lat_parse(prm, idx);
+    q = prm.snd_r ? sender_parse_wave(prm, idx) : lat_parse(prm, idx);  // (fused prep_sender / prep)
   }
   const uint32_t meta = q.meta, recid = q.recid;
   bool ok = q.ok;

@@ -281,7 +281,8 @@ DEV void recover_mid_body(const RecoverParams& prm, uint64_t* stamps) {
   const bool live = idx < prm.n;
   if (threadIdx.x < MF_N) S.flag[threadIdx.x] = 0u;
   __syncthreads();  // the only barrier
-  const LatParse q = lat_parse(prm, live ? idx : prm.n - 1);
+  const uint32_t pidx = live ? idx : prm.n - 1;
+  const LatParse q = prm.snd_r ? sender_parse_lane(prm, pidx) : lat_parse(prm, pidx);
   // diagnostic build: per-wave phase ticks, row blockIdx * 4 + wave (tools/phases_mid.py)
   auto stamp_out = [&] {
     if constexpr (!std::is_same<ST, NoStamp>::value) {
@@ -646,7 +647,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
   LatParse q;
   Payload m;
   if (!wire) {
-    q = lat_parse(prm, live ? idx : prm.n - 1);
+    q = prm.snd_r ? sender_parse_lane(prm, live ? idx : prm.n - 1) : lat_parse(prm, live ? idx : prm.n - 1);
   } else if (wv == 1) {
     wire_parse(S, prm, live ? idx : prm.n - 1, stage_a0, stage_end, q, m);
     S.meta[l] = q.meta;

@@ -25,6 +25,8 @@ enum KnobId : int {
   KNOB_COALESCE_GATHER_US,  // single-item coalescer: a leader's gather window
   KNOB_COALESCE_SPIN_US,    //   a waiting caller spins this long before it blocks
   KNOB_COALESCE_SPINNERS,   //   at most this many callers spin at once
+  KNOB_SENDER_FUSED,      // 1: sender rows of latency / mid-size batches are classified inside the
+                          //   recover kernel (no prep_sender launch); 0: prep_sender_kernel first
   KNOB_TEST_SKIP_FLAG,    // tests: k > 0 makes the first workgroup's producer of hand-off flag k - 1
                           //   skip publishing it (handoff.cuh), so its consumers time out
   KNOB_COUNT

@@ -50,6 +50,12 @@ struct RecoverParams {
   // tests only (KNOB_TEST_SKIP_FLAG, handoff.cuh): workgroup test_skip_block's producer of hand-off
   // flag test_skip_flag - 1 skips publishing it
   uint32_t test_skip_flag = 0, test_skip_block = 0;
+  // latency / mid-size kernels: types.Sender rows straight from the caller's SoA rows (n x 32
+  // big-endian sighash, r, s, v, 4-byte aligned; vflags n bytes, nullable) instead of record rows:
+  // prep_sender_kernel's classification (sender.cuh sender_meta) fused in (sender_parse_*)
+  const uint8_t *snd_h = nullptr, *snd_r = nullptr, *snd_s = nullptr, *snd_v = nullptr, *snd_f = nullptr;
+  int snd_signer = 0;
+  uint64_t snd_chain_id = 0;
   // mid-size bucket form only: wire-format transactions instead of record rows (tx_rows_kernel
   // and prep_sender_kernel fused in): item i is wire_raw[wire_off[first + i] - wire_off[0],
   // wire_off[first + i + 1] - wire_off[0]); wire_raw 4-byte aligned. wire_sighash: n x 32 or null.

@@ -52,10 +52,13 @@ DEV bool s30_ge(const s30& a, const s30& b) {
   return true;
 }
 
+#ifndef EGES_DIVSTEPS_ASM
+#define EGES_DIVSTEPS_ASM 1
+#endif
 // divsteps_30_var (modinv.cuh) for wave-uniform f, g: the same steps, kept on the scalar ALU (the
 // two-sided min of the lookahead limit would otherwise become a v_min3 and a v_readfirstlane
-// round trip through the VALU in every inner iteration).
-DEV int32_t divsteps_30_var_s(int32_t eta, uint32_t f0, uint32_t g0, trans2x2& t) {
+// round trip through the VALU in every inner iteration). C version: EGES_DIVSTEPS_ASM=0.
+DEV int32_t divsteps_30_var_c(int32_t eta, uint32_t f0, uint32_t g0, trans2x2& t) {
   uint32_t u = 1, v = 0, q = 0, r = 1;
   uint32_t f = f0, g = g0;
   int i = 30;
@@ -101,6 +104,116 @@ DEV int32_t divsteps_30_var_s(int32_t eta, uint32_t f0, uint32_t g0, trans2x2& t
   t.q = (int32_t)q;
   t.r = (int32_t)r;
   return eta;
+}
+
+// The same 30 divsteps as scalar-ALU assembly (one wave alone issues ~1 instruction per 6-8
+// cycles, tools/ubench_lat.hip, so the loop is priced by its instruction count):
+//  - a swap happens in ~97 % of the iterations (the eta rule), so the loop is written twice with
+//    the registers' roles exchanged (copy A: f = A, g = B, (u, v) = (uA, vA), (q, r) = (uB, vB);
+//    copy B the other way round): a swap is three negations and a fall-through into the other
+//    copy's tail, instead of six moves;
+//  - the bits of g cancelled per iteration are capped at 6 (libsecp256k1's formula
+//    w = f g (f^2 - 2) mod 2^6, f^-1 by one Newton step from f^-1 = f mod 8) instead of a 12-bit
+//    inverse recomputed at every swap: a capped iteration is simply continued by the next one, so
+//    the sequence of divsteps, and the (u, v, q, r) after 30 of them, are unchanged (the same
+//    argument as libsecp256k1 modinv32_impl.h's variable-time divsteps);
+//  - the remaining count i is kept as the sentinel mask sm = -1 << i (shifted arithmetically with
+//    g), which gives ctz's sentinel, the end test (sm == -1) and the limit mask (~sm) directly.
+// ~30 instructions per iteration (swap path) against ~41 for the compiled C version.
+DEV int32_t divsteps_30_var_asm(int32_t eta, uint32_t f0, uint32_t g0, trans2x2& t) {
+  uint32_t A = f0, B = g0, uA = 1, vA = 0, uB = 0, vB = 1, sm = 0xC0000000u;  // -1 << 30
+  uint32_t tmp, z, m, w;
+  asm volatile(
+      "LA_head_%=:\n"
+      "  s_or_b32 %[tmp], %[B], %[sm]\n"
+      "  s_ff1_i32_b32 %[z], %[tmp]\n"
+      "  s_lshr_b32 %[B], %[B], %[z]\n"
+      "  s_lshl_b32 %[uA], %[uA], %[z]\n"
+      "  s_lshl_b32 %[vA], %[vA], %[z]\n"
+      "  s_sub_i32 %[eta], %[eta], %[z]\n"
+      "  s_ashr_i32 %[sm], %[sm], %[z]\n"
+      "  s_cmp_eq_u32 %[sm], -1\n"
+      "  s_cbranch_scc1 LA_done_%=\n"
+      "  s_cmp_lt_i32 %[eta], 0\n"
+      "  s_cbranch_scc0 LA_tail_%=\n"
+      // swap: (f, g) = (g, -f), (u, v, q, r) = (q, r, -u, -v), eta = -eta: copy B's roles
+      "  s_sub_i32 %[eta], 0, %[eta]\n"
+      "  s_sub_i32 %[A], 0, %[A]\n"
+      "  s_sub_i32 %[uA], 0, %[uA]\n"
+      "  s_sub_i32 %[vA], 0, %[vA]\n"
+      "LB_tail_%=:\n"  // f = B, g = A, f-row (uB, vB), g-row (uA, vA); eta >= 0
+      "  s_add_i32 %[tmp], %[eta], 1\n"
+      "  s_min_u32 %[tmp], %[tmp], 6\n"
+      "  s_bfm_b32 %[m], %[tmp], 0\n"
+      "  s_andn2_b32 %[m], %[m], %[sm]\n"
+      "  s_mul_i32 %[tmp], %[B], %[B]\n"
+      "  s_add_i32 %[tmp], %[tmp], -2\n"
+      "  s_mul_i32 %[tmp], %[tmp], %[B]\n"
+      "  s_mul_i32 %[tmp], %[tmp], %[A]\n"
+      "  s_and_b32 %[w], %[tmp], %[m]\n"
+      "  s_mul_i32 %[tmp], %[B], %[w]\n"
+      "  s_add_i32 %[A], %[A], %[tmp]\n"
+      "  s_mul_i32 %[tmp], %[uB], %[w]\n"
+      "  s_add_i32 %[uA], %[uA], %[tmp]\n"
+      "  s_mul_i32 %[tmp], %[vB], %[w]\n"
+      "  s_add_i32 %[vA], %[vA], %[tmp]\n"
+      "LB_head_%=:\n"
+      "  s_or_b32 %[tmp], %[A], %[sm]\n"
+      "  s_ff1_i32_b32 %[z], %[tmp]\n"
+      "  s_lshr_b32 %[A], %[A], %[z]\n"
+      "  s_lshl_b32 %[uB], %[uB], %[z]\n"
+      "  s_lshl_b32 %[vB], %[vB], %[z]\n"
+      "  s_sub_i32 %[eta], %[eta], %[z]\n"
+      "  s_ashr_i32 %[sm], %[sm], %[z]\n"
+      "  s_cmp_eq_u32 %[sm], -1\n"
+      "  s_cbranch_scc1 LB_done_%=\n"
+      "  s_cmp_lt_i32 %[eta], 0\n"
+      "  s_cbranch_scc0 LB_tail_%=\n"
+      "  s_sub_i32 %[eta], 0, %[eta]\n"
+      "  s_sub_i32 %[B], 0, %[B]\n"
+      "  s_sub_i32 %[uB], 0, %[uB]\n"
+      "  s_sub_i32 %[vB], 0, %[vB]\n"
+      "LA_tail_%=:\n"  // f = A, g = B, f-row (uA, vA), g-row (uB, vB); eta >= 0
+      "  s_add_i32 %[tmp], %[eta], 1\n"
+      "  s_min_u32 %[tmp], %[tmp], 6\n"
+      "  s_bfm_b32 %[m], %[tmp], 0\n"
+      "  s_andn2_b32 %[m], %[m], %[sm]\n"
+      "  s_mul_i32 %[tmp], %[A], %[A]\n"
+      "  s_add_i32 %[tmp], %[tmp], -2\n"
+      "  s_mul_i32 %[tmp], %[tmp], %[A]\n"
+      "  s_mul_i32 %[tmp], %[tmp], %[B]\n"
+      "  s_and_b32 %[w], %[tmp], %[m]\n"
+      "  s_mul_i32 %[tmp], %[A], %[w]\n"
+      "  s_add_i32 %[B], %[B], %[tmp]\n"
+      "  s_mul_i32 %[tmp], %[uA], %[w]\n"
+      "  s_add_i32 %[uB], %[uB], %[tmp]\n"
+      "  s_mul_i32 %[tmp], %[vA], %[w]\n"
+      "  s_add_i32 %[vB], %[vB], %[tmp]\n"
+      "  s_branch LA_head_%=\n"
+      "LB_done_%=:\n"  // copy B's roles back to (u, v) = (uA, vA), (q, r) = (uB, vB)
+      "  s_mov_b32 %[tmp], %[uA]\n"
+      "  s_mov_b32 %[uA], %[uB]\n"
+      "  s_mov_b32 %[uB], %[tmp]\n"
+      "  s_mov_b32 %[tmp], %[vA]\n"
+      "  s_mov_b32 %[vA], %[vB]\n"
+      "  s_mov_b32 %[vB], %[tmp]\n"
+      "LA_done_%=:\n"
+      : [A] "+s"(A), [B] "+s"(B), [uA] "+s"(uA), [vA] "+s"(vA), [uB] "+s"(uB), [vB] "+s"(vB), [sm] "+s"(sm),
+        [eta] "+s"(eta), [tmp] "=&s"(tmp), [z] "=&s"(z), [m] "=&s"(m), [w] "=&s"(w)
+      :
+      : "scc");
+  t.u = (int32_t)uA;
+  t.v = (int32_t)vA;
+  t.q = (int32_t)uB;
+  t.r = (int32_t)vB;
+  return eta;
+}
+DEV int32_t divsteps_30_var_s(int32_t eta, uint32_t f0, uint32_t g0, trans2x2& t) {
+#if EGES_DIVSTEPS_ASM
+  return divsteps_30_var_asm(eta, f0, g0, t);
+#else
+  return divsteps_30_var_c(eta, f0, g0, t);
+#endif
 }
 
 // x^-1 mod M for x in [0, M), x wave-uniform (0 maps to 0)

@@ -3,6 +3,8 @@
 // integers as 8 little-endian 32-bit words; the Python side checks against big integers.
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "core.cuh"
 
 namespace eges {
@@ -305,6 +307,7 @@ enum : int {
   FR_QUAD2 = 8,    // fr_mul2 (a*b, c*c): out = ab + 2c^2
   FR_INV = 9,      // fr_inv_var (row-parallel safegcd): out = a^-1
   FR_GADD = 10,    // gejq_add of lift(a, even) on Z = c and lift(b, parity of c) on Z = c^2: x of the sum
+  FR_SCINV = 11,   // sc_inv_row_var (row-parallel safegcd mod n) of a < n: out = a^-1 mod n
 };
 __global__ void fr_selftest_kernel(int op, uint32_t n, const uint32_t* A, const uint32_t* B, const uint32_t* C,
                                    uint32_t* out) {
@@ -372,13 +375,50 @@ __global__ void fr_selftest_kernel(int op, uint32_t n, const uint32_t* A, const 
     }
     default: r = a;
   }
-  const fe o = fe_normalize(fr_to_fe_row(r));
   uint32_t x[8];
-  fe_to_u256(x, o);
+  if (op == FR_SCINV) {  // a scalar in, a scalar out (the raw words, not reduced mod p)
+    uint32_t w[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = A[(size_t)i * 8 + k];
+    bool ov;
+    const sc si = sc_inv_row_var(sc_from_limbs(w, ov));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = si.v[k];
+  } else {
+    fe_to_u256(x, fe_normalize(fr_to_fe_row(r)));
+  }
   if (in && (threadIdx.x & (op >= FR_QUAD ? 63 : 15)) == 0) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) out[(size_t)i * 8 + k] = x[k];
   }
+}
+
+// Inversion latency: one wave per CU, `reps` dependent row-form inversions (mode 0: fr_inv_var mod
+// p, 1: sc_inv_row_var mod n) on a chain x -> (x + 1)^-1; mean s_memtime cycles per inversion.
+__global__ void __launch_bounds__(64) inv_latency_kernel(int mode, int reps, uint64_t* cyc, uint32_t* sink) {
+  uint32_t w[8];
+  for (int k = 0; k < 8; ++k) w[k] = (blockIdx.x + 1) * 2654435761u + k * 40503u;
+  w[7] &= 0x7FFFFFFFu;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  uint32_t acc = 0;
+  if (mode == 0) {
+    fr x = fe_to_fr(fe_from_u256(w));
+#pragma unroll 1
+    for (int r = 0; r < reps; ++r) x = fr_inv_var(fr_add(x, fr_one()));
+    acc = x.v;
+  } else {
+    bool ov;
+    sc x = sc_from_limbs(w, ov);
+#pragma unroll 1
+    for (int r = 0; r < reps; ++r) {
+      x.v[0] += 1;  // (no carry: the chain only needs distinct nonzero values)
+      x = sc_inv_row_var(x);
+    }
+    acc = x.v[0];
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  sink[blockIdx.x * 64 + threadIdx.x] = acc;
+  if (threadIdx.x == 0) cyc[blockIdx.x] = (t1 - t0) / (uint64_t)reps;
 }
 
 // Latency microbenchmark: one wave per CU, each runs a chain of `reps` dependent squarings in
@@ -416,6 +456,26 @@ extern "C" int eges_fr_selftest(int op, uint32_t n, const uint32_t* a, const uin
   (void)hipMemcpy(out, dout, B, hipMemcpyDeviceToHost);
   (void)hipFree(da); (void)hipFree(db); (void)hipFree(dc); (void)hipFree(dout);
   return e == hipSuccess ? 0 : -2;
+}
+
+// mean s_memtime cycles per dependent row-form inversion at one wave per CU (mode 0 mod p, 1 mod n)
+extern "C" double eges_inv_latency(int mode, int reps) {
+  hipDeviceProp_t prop;
+  (void)hipGetDeviceProperties(&prop, 0);
+  const int blocks = prop.multiProcessorCount;
+  uint32_t* sink;
+  uint64_t* cyc;
+  if (hipMalloc(&sink, (size_t)blocks * 64 * 4) != hipSuccess || hipMalloc(&cyc, (size_t)blocks * 8) != hipSuccess)
+    return -1;
+  hipLaunchKernelGGL(eges::inv_latency_kernel, dim3(blocks), dim3(64), 0, 0, mode, reps, cyc, sink);
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  std::vector<uint64_t> h(blocks);
+  (void)hipMemcpy(h.data(), cyc, (size_t)blocks * 8, hipMemcpyDeviceToHost);
+  (void)hipFree(sink);
+  (void)hipFree(cyc);
+  double s = 0;
+  for (uint64_t v : h) s += (double)v;
+  return s / blocks;
 }
 
 // ns per dependent squaring at one wave per CU (mode 0 lane-serial fe, 1 row-form fr)

@@ -98,6 +98,62 @@ DEV uint32_t sender_meta(const uint32_t r[8], const uint32_t s[8], const uint32_
   return recid | (status << 8);
 }
 
+// The record lat_parse builds, from a sender row's little-endian limbs (z = the signing hash,
+// r, s, v) and its vflags: prep_sender_kernel's classification and prep's range checks.
+DEV LatParse sender_record(const uint32_t z[8], const uint32_t r[8], const uint32_t s[8], const uint32_t v[8],
+                           uint32_t fl, int signer, uint64_t chain_id) {
+  LatParse q;
+  q.meta = sender_meta(r, s, v, fl, signer, chain_id);
+  q.recid = q.meta & 3u;
+  q.ok = ((q.meta >> 8) & 0xffu) == ST_OK;
+  bool ovr, ovs, ovz;
+  q.R = sc_from_limbs(r, ovr);
+  q.Sv = sc_from_limbs(s, ovs);
+  q.Z = sc_from_limbs(z, ovz);  // msg mod n (main_impl.h:183)
+  q.ok = q.ok && !ovr && !ovs && !sc_is_zero(q.R) && !sc_is_zero(q.Sv);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q.xr[i] = q.R.v[i];  // recid < 2 on this path: x = r
+  return q;
+}
+
+// Sender rows (RecoverParams::snd_*, 4-byte aligned) of item idx, one lane (root helpers, the
+// mid-size kernel): eight dword loads per row, limb i = byte-swapped dword 7 - i.
+DEV void row_limbs(uint32_t out[8], const uint8_t* row, uint32_t idx) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(row + (size_t)idx * 32);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) out[i] = __builtin_bswap32(w[7 - i]);
+}
+DEV LatParse sender_parse_lane(const RecoverParams& prm, uint32_t idx) {
+  uint32_t z[8], r[8], s[8], v[8];
+  row_limbs(z, prm.snd_h, idx);
+  row_limbs(r, prm.snd_r, idx);
+  row_limbs(s, prm.snd_s, idx);
+  row_limbs(v, prm.snd_v, idx);
+  const uint32_t fl = prm.snd_f ? prm.snd_f[idx] : 0u;
+  return sender_record(z, r, s, v, fl, prm.snd_signer, prm.snd_chain_id);
+}
+// The same for a whole wave working on one item (the latency kernels' row-form waves): one load
+// instruction fetches the item's four rows (lane 8 k + j: dword j of row k) and its flags byte
+// (lane 32); the limbs come back wave-uniform through readlane.
+DEV LatParse sender_parse_wave(const RecoverParams& prm, uint32_t idx) {
+  const uint32_t lane = (uint32_t)__lane_id();
+  const uint32_t k = lane >> 3, j = lane & 7u;
+  const uint8_t* row = k == 0 ? prm.snd_h : k == 1 ? prm.snd_r : k == 2 ? prm.snd_s : prm.snd_v;
+  uint32_t w = 0;
+  if (lane < 32) w = reinterpret_cast<const uint32_t*>(row + (size_t)idx * 32)[j];
+  else if (lane == 32 && prm.snd_f) w = prm.snd_f[idx];
+  uint32_t z[8], r[8], s[8], v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    z[i] = __builtin_bswap32((uint32_t)__builtin_amdgcn_readlane((int)w, 7 - i));
+    r[i] = __builtin_bswap32((uint32_t)__builtin_amdgcn_readlane((int)w, 15 - i));
+    s[i] = __builtin_bswap32((uint32_t)__builtin_amdgcn_readlane((int)w, 23 - i));
+    v[i] = __builtin_bswap32((uint32_t)__builtin_amdgcn_readlane((int)w, 31 - i));
+  }
+  const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)w, 32);
+  return sender_record(z, r, s, v, fl, prm.snd_signer, prm.snd_chain_id);
+}
+
 // One wire-format transaction p[0, len) (span_ok: its offsets were consistent) -> the record
 // lat_parse builds from rows (R, S, meta = recid | status << 8, R's x; z is left to the caller,
 // who hashes m, the signing payload) — tx_rows_kernel's decode and prep_sender_kernel's
@@ -122,15 +178,8 @@ DEV bool wire_item(const uint8_t* p, uint64_t len, bool span_ok, int signer, uin
 #pragma unroll
     for (int k = 0; k < 8; ++k) r[k] = s[k] = v[k] = 0;
   }
-  q.meta = sender_meta(r, s, v, fl, signer, chain_id);
-  q.recid = q.meta & 3u;
-  q.ok = ((q.meta >> 8) & 0xffu) == ST_OK;
-  bool ovr, ovs;
-  q.R = sc_from_limbs(r, ovr);
-  q.Sv = sc_from_limbs(s, ovs);
-  q.ok = q.ok && !ovr && !ovs && !sc_is_zero(q.R) && !sc_is_zero(q.Sv);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) q.xr[i] = q.R.v[i];  // recid < 2 on this path: x = r
+  const uint32_t z0[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // z: the caller hashes m
+  q = sender_record(z0, r, s, v, fl, signer, chain_id);
   return ok;
 }
 

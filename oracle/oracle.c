@@ -514,9 +514,14 @@ static int bitlen_be(const unsigned char *b) {
 
 /* recoverPlain (transaction_signing.go:222-247) with V already reduced to {27,28,...}
  * given as a 256-bit BE value vb (+ wide flag). */
-static int recover_plain(unsigned char addr20[20], const unsigned char sighash[32], const unsigned char r32[32],
-                         const unsigned char s32[32], const unsigned char vb[32], int v_wide, int r_wide, int s_wide,
-                         int homestead) {
+/* The recovery recoverPlain ends in (crypto.Ecrecover): this restatement's own by default;
+ * oracle_sender_with lets a caller put the reference libsecp256k1's in its place (ref_shim.c),
+ * so that the Go-layer rules here are checked with the reference's recovery underneath. */
+typedef int (*recover_fn)(unsigned char pub65[65], const unsigned char sig65[65], const unsigned char msg32[32]);
+
+static int recover_plain(recover_fn rec, unsigned char addr20[20], const unsigned char sighash[32],
+                         const unsigned char r32[32], const unsigned char s32[32], const unsigned char vb[32],
+                         int v_wide, int r_wide, int s_wide, int homestead) {
     if (v_wide || bitlen_be(vb) > 8) return ST_INVALID_SIG;
     unsigned char V = (unsigned char)(vb[31] - 27); /* byte(Vb.Uint64() - 27) */
     /* ValidateSignatureValues (crypto.go:181-192) */
@@ -532,7 +537,7 @@ static int recover_plain(unsigned char addr20[20], const unsigned char sighash[3
     memcpy(sig, r32, 32);
     memcpy(sig + 32, s32, 32);
     sig[64] = V;
-    int st = oracle_recover_pubkey(pub, sig, sighash);
+    int st = rec(pub, sig, sighash);
     if (st) return st;
     oracle_keccak256(pub + 1, 64, h);
     memcpy(addr20, h + 12, 20);
@@ -551,21 +556,23 @@ static void be_sub_u64(unsigned char *r, const unsigned char *a, u64 x) {
 }
 
 /* Signer.Sender for the three signers. v32 = V as 256-bit BE (VF_V_WIDE if V > 2^256).
- * chain_id is the EIP155 signer's chain id (uint64). Returns a status. */
-int oracle_sender(unsigned char addr20[20], int signer, u64 chain_id, const unsigned char sighash[32],
-                  const unsigned char r32[32], const unsigned char s32[32], const unsigned char v32[32], int vflags) {
+ * chain_id is the EIP155 signer's chain id (uint64). Returns a status. `rec` recovers the key
+ * (oracle_recover_pubkey's contract: 0 ok, else the status). */
+int oracle_sender_with(recover_fn rec, unsigned char addr20[20], int signer, u64 chain_id,
+                       const unsigned char sighash[32], const unsigned char r32[32], const unsigned char s32[32],
+                       const unsigned char v32[32], int vflags) {
     int v_wide = vflags & VF_V_WIDE, r_wide = vflags & VF_R_WIDE, s_wide = vflags & VF_S_WIDE;
     memset(addr20, 0, 20);
     if (signer == SIGNER_FRONTIER) /* :218-220 */
-        return recover_plain(addr20, sighash, r32, s32, v32, v_wide, r_wide, s_wide, 0);
+        return recover_plain(rec, addr20, sighash, r32, s32, v32, v_wide, r_wide, s_wide, 0);
     if (signer == SIGNER_HOMESTEAD) /* :182-184 */
-        return recover_plain(addr20, sighash, r32, s32, v32, v_wide, r_wide, s_wide, 1);
+        return recover_plain(rec, addr20, sighash, r32, s32, v32, v_wide, r_wide, s_wide, 1);
     /* EIP155Signer.Sender :127-137 */
     int bl = v_wide ? 1000 : bitlen_be(v32);
     int prot; /* isProtectedV, transaction.go:142-149 */
     if (bl <= 8) prot = !(v32[31] == 27 || v32[31] == 28);
     else prot = 1;
-    if (!prot) return recover_plain(addr20, sighash, r32, s32, v32, v_wide, r_wide, s_wide, 1);
+    if (!prot) return recover_plain(rec, addr20, sighash, r32, s32, v32, v_wide, r_wide, s_wide, 1);
     /* deriveChainId (:250-260) compared with chain_id */
     int match;
     if (bl <= 64) {
@@ -604,7 +611,12 @@ int oracle_sender(unsigned char addr20[20], int signer, u64 chain_id, const unsi
         }
         (void)borrow; /* V >= 2c+35 here, no underflow */
     }
-    return recover_plain(addr20, sighash, r32, s32, vp, 0, r_wide, s_wide, 1);
+    return recover_plain(rec, addr20, sighash, r32, s32, vp, 0, r_wide, s_wide, 1);
+}
+
+int oracle_sender(unsigned char addr20[20], int signer, u64 chain_id, const unsigned char sighash[32],
+                  const unsigned char r32[32], const unsigned char s32[32], const unsigned char v32[32], int vflags) {
+    return oracle_sender_with(oracle_recover_pubkey, addr20, signer, chain_id, sighash, r32, s32, v32, vflags);
 }
 
 /* Address from uncompressed pubkey (crypto.go:194-197 PubkeyToAddress / recoverPlain :245). */

@@ -126,6 +126,7 @@ class RefLib:
         L.eref_sign.argtypes = [P, P, P]
         L.eref_pubkey.argtypes = [P, P]
         L.eref_ecrecover_batch_mt.argtypes = [SZ, P, P, P, P, P, I]
+        L.eref_sender_batch_mt.argtypes = [SZ, I, ctypes.c_ulonglong, P, P, P, P, P, P, P, I]
         self.L = L
 
     def ecrecover(self, msg: bytes, sig: bytes):
@@ -146,3 +147,14 @@ class RefLib:
         self.L.eref_ecrecover_batch_mt(n, _p(msg), _p(sig), _p(pub), _p(addr), _p(ret), int(nthreads))
         _rec("eref_batch_mt", n, msg, sig, int(nthreads), pub, addr, ret)
         return pub, addr, ret
+
+    def sender_batch_mt(self, signer, chain_id, sighash, r, s, v, vflags, nthreads):
+        """types.Sender: oracle.c's Go-layer rules over the reference's recovery -> (addr, status)."""
+        sighash, r, s, v = (np.ascontiguousarray(x, np.uint8) for x in (sighash, r, s, v))
+        n = sighash.shape[0]
+        vflags = np.zeros(n, np.uint8) if vflags is None else np.ascontiguousarray(vflags, np.uint8)
+        addr = np.zeros((n, 20), np.uint8)
+        st = np.zeros(n, np.uint8)
+        self.L.eref_sender_batch_mt(n, int(signer), int(chain_id), _p(sighash), _p(r), _p(s), _p(v), _p(vflags), _p(addr),
+                                    _p(st), int(nthreads))
+        return addr, st

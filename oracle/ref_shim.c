@@ -148,3 +148,56 @@ void eref_ecrecover_batch_mt(size_t n, const unsigned char *msg, const unsigned 
     }
     for (t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
 }
+
+/* ---- types.Sender over the reference libsecp256k1 (TEST INFRASTRUCTURE) ----
+ * The Go-layer rules (EIP155Signer / HomesteadSigner / FrontierSigner.Sender, recoverPlain,
+ * ValidateSignatureValues) are oracle.c's restatement (oracle_sender_with); the recovery under
+ * them is the reference's secp256k1_ext_ecdsa_recover (eref_ecrecover), one pthread per worker.
+ * Used by the GPU tests to check the engine's Sender statuses and addresses item for item at
+ * configs[4]'s full size. */
+int oracle_sender_with(int (*rec)(unsigned char *, const unsigned char *, const unsigned char *), unsigned char *addr20,
+                       int signer, unsigned long long chain_id, const unsigned char *sighash, const unsigned char *r32,
+                       const unsigned char *s32, const unsigned char *v32, int vflags);
+
+static int eref_recover_status(unsigned char *pub65, const unsigned char *sig65, const unsigned char *msg32) {
+    const int r = eref_ecrecover(pub65, sig65, msg32);
+    return r == 1 ? 0 : r == -2 ? 5 /* EGES_INVALID_RECOVERY_ID */ : 6 /* EGES_RECOVER_FAILED */;
+}
+
+typedef struct {
+    size_t lo, hi;
+    int signer;
+    unsigned long long chain_id;
+    const unsigned char *h, *r, *s, *v, *f;
+    unsigned char *addr, *status;
+} eref_sender_job;
+
+static void *eref_sender_worker(void *p) {
+    eref_sender_job *j = (eref_sender_job *)p;
+    for (size_t i = j->lo; i < j->hi; ++i)
+        j->status[i] = (unsigned char)oracle_sender_with(eref_recover_status, j->addr + 20 * i, j->signer, j->chain_id,
+                                                         j->h + 32 * i, j->r + 32 * i, j->s + 32 * i, j->v + 32 * i,
+                                                         j->f ? j->f[i] : 0);
+    return NULL;
+}
+
+void eref_sender_batch_mt(size_t n, int signer, unsigned long long chain_id, const unsigned char *sighash,
+                          const unsigned char *r, const unsigned char *s, const unsigned char *v,
+                          const unsigned char *vflags, unsigned char *addr_out, unsigned char *status_out, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 1024) nthreads = 1024;
+    ctx_get();
+    pthread_t th[1024];
+    eref_sender_job jobs[1024];
+    size_t per = (n + (size_t)nthreads - 1) / (size_t)nthreads;
+    int t;
+    for (t = 0; t < nthreads; ++t) {
+        size_t lo = (size_t)t * per, hi = lo + per;
+        if (lo > n) lo = n;
+        if (hi > n) hi = n;
+        eref_sender_job jb = {lo, hi, signer, chain_id, sighash, r, s, v, vflags, addr_out, status_out};
+        jobs[t] = jb;
+        pthread_create(&th[t], NULL, eref_sender_worker, &jobs[t]);
+    }
+    for (t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+}

@@ -1,5 +1,6 @@
 """configs[3] (C4) on the GPU: the full 64M-signature batch through the device entry, every
-address checked against the synthetic signer, plus an oracle sample across every pass boundary;
+address checked against the synthetic signer, an oracle sample across every pass boundary and a
+1M random-index sample against the reference libsecp256k1 (oracle/_ref);
 and the in-library multi-device split (capi.hip run_host with ndev > 1) and a small-grid device
 run in child processes with the engine's test-only knobs (tests/gpu_child.py)."""
 import json
@@ -37,6 +38,19 @@ def test_c4_full_64m_batch(engine, oracle):
     for j in range(len(idx)):
         ost, opub = oracle.recover_pubkey(m[j].tobytes(), s[j].tobytes())
         assert ost == 0 and oracle.pub_to_addr(opub) == a[j].tobytes(), int(idx[j])
+    # a 1M random-index sample of the 64M batch against the reference libsecp256k1 itself
+    # (oracle/_ref, its recovery + the address, on the host cores): independent of the GPU signer
+    from oracle import RefLib, have_ref
+    if have_ref():
+        rng = np.random.default_rng(64)
+        ridx = np.unique(rng.integers(0, n, size=(1 << 20) + (1 << 16)))[: 1 << 20].astype(np.int64)
+        sel = torch.from_numpy(ridx).to(msg.device)
+        m, s, a = msg[sel].cpu().numpy(), sig[sel].cpu().numpy(), addr[sel].cpu().numpy()
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        _, raddr, ret = RefLib().ecrecover_batch_mt(m, s, threads)
+        assert (ret == 1).all()
+        bad = np.nonzero((raddr != a).any(axis=1))[0]
+        assert bad.size == 0, ridx[bad[:10]].tolist()
     del msg, sig, exp, addr, st
     torch.cuda.empty_cache()
 

@@ -14,7 +14,8 @@ from conftest import ROOT
 from test_gpu_field import P, dec, enc, samples
 
 pytestmark = pytest.mark.gpu
-FR = dict(MUL=0, SQR=1, MULSUB=2, SUB=3, LAZY=4, NORMW=5, CHAIN=6, QUAD=7, QUAD2=8, INV=9, GADD=10)
+FR = dict(MUL=0, SQR=1, MULSUB=2, SUB=3, LAZY=4, NORMW=5, CHAIN=6, QUAD=7, QUAD2=8, INV=9, GADD=10, SCINV=11)
+N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
 
 
 @pytest.fixture(scope="module")
@@ -107,7 +108,7 @@ def test_fr_general_add(st):
         assert got[i] == exp, (i, i % 3)
 
 
-@pytest.mark.parametrize("op", [o for o in FR if o != "GADD"])
+@pytest.mark.parametrize("op", [o for o in FR if o not in ("GADD", "SCINV")])
 def test_fr_ops(st, op):
     rnd = random.Random(1234 + FR[op])
     n = 1500
@@ -125,6 +126,26 @@ def test_fr_inv_edges(st):
     got = run(st, "INV", vals, vals, vals)
     bad = [(hex(v), hex(g)) for v, g in zip(vals, got) if g != expect("INV", v, 0, 0)]
     assert not bad, bad[:5]
+
+
+def test_sc_inv_row(st):
+    """sc_inv_row_var (r^-1 / s^-1 of the latency kernels: scalar-ALU divsteps, limb-parallel
+    updates) against pow(a, n - 2, n): random scalars and edges (0 -> 0, 1, n - 1, powers of two,
+    values with long runs of zero bits)"""
+    rnd = random.Random(99)
+    vals = [0, 1, 2, 3, N - 1, N - 2, (N + 1) // 2, 2**255 % N] + [2**k for k in range(0, 256, 13)]
+    vals += [(2**k - 1) % N for k in range(1, 256, 19)] + [rnd.randrange(1, N) for _ in range(1500)]
+    got = run(st, "SCINV", vals, vals, vals)
+    bad = [(hex(v), hex(g)) for v, g in zip(vals, got) if g != (pow(v, N - 2, N) if v else 0)]
+    assert not bad, bad[:5]
+
+
+def test_inv_latency_record(st):
+    st.eges_inv_latency.argtypes = [ctypes.c_int, ctypes.c_int]
+    st.eges_inv_latency.restype = ctypes.c_double
+    p, n = st.eges_inv_latency(0, 64), st.eges_inv_latency(1, 64)
+    print(f"\nrow-form inversion at one wave per CU: mod p {p:.0f} cycles, mod n {n:.0f} cycles")
+    assert p > 0 and n > 0
 
 
 def test_fr_latency_record(st):

@@ -86,6 +86,39 @@ def test_adversarial_mix_1m_vs_reference(engine):
     assert (st != 0).sum() > n // 20
 
 
+def test_adversarial_mix_1m_sender_vs_reference(engine):
+    """configs[4]'s Sender mode at its full size, item for item: 1,048,576 EIP-155 sender rows,
+    10 % invalid over seven classes (high-s, bad V / foreign chain id, r >= n, s >= n,
+    non-residue R, zero r / s), through eges_sender_batch_dev against the Go-layer rules of
+    oracle.c (EIP155Signer.Sender, recoverPlain, ValidateSignatureValues) over the reference
+    libsecp256k1's recovery (oracle/_ref eref_sender_batch_mt, host cores): every status and
+    every address equal."""
+    import torch
+    from eges_amd import txs, workloads
+    from eges_amd._lib import SIGNER_EIP155
+    from oracle import RefLib, have_ref
+    if not have_ref():
+        pytest.skip("oracle/_ref not built")
+    n = 1 << 20
+    msg, sig, exp = engine.synth_sign_dev(9 << 40, n, 0)
+    torch.cuda.synchronize()
+    sig_h, msg_h = sig.cpu().numpy(), msg.cpu().numpy()
+    kind = workloads.adversarial_mix(sig_h, frac=0.10, seed=8)
+    r, s, v = workloads.sender_rows_mixed(sig_h, kind, txs.GEEC_CHAIN_ID)
+    addr, st = engine.sender_batch_dev(msg, *(torch.from_numpy(x).cuda() for x in (r, s, v)),
+                                       torch.zeros(n, dtype=torch.uint8, device="cuda"), SIGNER_EIP155,
+                                       txs.GEEC_CHAIN_ID)
+    torch.cuda.synchronize()
+    addr, st = addr.cpu().numpy(), st.cpu().numpy()
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    raddr, rst = RefLib().sender_batch_mt(SIGNER_EIP155, txs.GEEC_CHAIN_ID, msg_h, r, s, v, None, threads)
+    bad = np.nonzero(st != rst)[0]
+    assert bad.size == 0, [(int(i), int(st[i]), int(rst[i]), int(kind[i])) for i in bad[:10]]
+    assert np.array_equal(addr, raddr)
+    assert np.array_equal(st, workloads.expected_status(kind, "sender"))
+    assert (st != 0).sum() > n // 20
+
+
 def test_verify_mode_mix(engine, oracle):
     import torch
     from eges_amd import workloads

@@ -160,3 +160,22 @@ def test_validate_signature_values_table(oracle):  # crypto/crypto_test.go:148-1
         st, _ = oracle.sender(0, 0, h, r, s, (27 + v).to_bytes(32, "big"), 0)
         # valid range => passes ValidateSignatureValues; recovery itself may still fail (6)
         assert (st != 2) == valid, (v, valid, st)
+
+
+def test_ref_backed_sender_reproduces_golden():
+    """oracle/_ref eref_sender_batch_mt (oracle.c's Go-layer Sender rules over the reference
+    libsecp256k1's recovery; the 1M Sender-mode GPU check uses it) reproduces every golden sender
+    item: status and address, every signer and chain id."""
+    import numpy as np
+    from oracle import RefLib, have_ref
+    if not have_ref():
+        pytest.skip("oracle/_ref not built")
+    from conftest import load_golden
+    g = load_golden("sender.npz")
+    ref = RefLib()
+    for signer, cid in sorted(set(zip(g["signer"].tolist(), g["chain_id"].tolist()))):
+        sel = np.nonzero((g["signer"] == signer) & (g["chain_id"] == cid))[0]
+        a, st = ref.sender_batch_mt(signer, cid, g["sighash"][sel], g["r"][sel], g["s"][sel], g["v"][sel],
+                                    g["vflags"][sel], 4)
+        assert np.array_equal(st, g["status"][sel]), (signer, cid)
+        assert np.array_equal(a, g["addr"][sel]), (signer, cid)
