@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <initializer_list>
 #include <memory>
 #include <atomic>
@@ -102,6 +103,11 @@ struct Dev {
   hipStream_t aux = nullptr;
   uint32_t* ws2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // pipelined host-buffer calls (run_host_pipe): H2D / D2H streams, two pinned staging slots
+  hipStream_t hin = nullptr, hout = nullptr;
+  hipEvent_t ev_out[2] = {nullptr, nullptr};
+  uint8_t* ring[2] = {nullptr, nullptr};
+  size_t ring_cap = 0;
   std::mutex mu;
   Lane lanes[NLANES];
   ~Dev();
@@ -143,6 +149,9 @@ const KnobDef KNOB_DEFS[KNOB_COUNT] = {
     {"EGES_COALESCE_SPIN_US", 2000},
     {"EGES_COALESCE_SPINNERS", 8},
     {"EGES_SENDER_FUSED", 1},
+    {"EGES_HOST_PIPE", 1},
+    {"EGES_PIPE_CHUNK", 262144},
+    {"EGES_PIPE_FIRST", 131072},
     {"EGES_TEST_SKIP_FLAG", 0},
 };
 std::atomic<long long> g_knob[KNOB_COUNT];
@@ -169,7 +178,8 @@ int knob_index(const char* name) {
 struct Route {
   size_t lat_max = 0, mid_max = 0;
   uint32_t wide_max = 0;
-  long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1;
+  long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, host_pipe = 1;
+  size_t pipe_chunk = 262144, pipe_first = 131072;
   uint32_t force_redo = 0, skip_flag = 0;
   static Route now() {
     Route r;
@@ -180,6 +190,9 @@ struct Route {
     r.wire_fused = knob(KNOB_WIRE_FUSED);
     r.overlap = knob(KNOB_OVERLAP);
     r.sender_fused = knob(KNOB_SENDER_FUSED);
+    r.host_pipe = knob(KNOB_HOST_PIPE);
+    r.pipe_chunk = (size_t)std::max<long long>(64, knob(KNOB_PIPE_CHUNK));
+    r.pipe_first = (size_t)std::max<long long>(64, knob(KNOB_PIPE_FIRST));
     r.force_redo = knob(KNOB_FORCE_REDO) != 0 ? 1u : 0u;
     r.skip_flag = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TEST_SKIP_FLAG), 64));
     return r;
@@ -296,10 +309,17 @@ Dev::~Dev() {
   }
   if (copy) (void)hipStreamDestroy(copy);
   if (aux) {
+    (void)hipStreamSynchronize(aux);
     (void)hipStreamDestroy(aux);
     (void)hipEventDestroy(ev_fork);
     (void)hipEventDestroy(ev_join);
     (void)hipFree(ws2);
+  }
+  if (hin) (void)hipStreamSynchronize(hin), (void)hipStreamDestroy(hin);
+  if (hout) (void)hipStreamSynchronize(hout), (void)hipStreamDestroy(hout);
+  for (int r = 0; r < 2; ++r) {
+    if (ev_out[r]) (void)hipEventDestroy(ev_out[r]);
+    if (ring[r]) (void)hipHostFree(ring[r]);
   }
   for (Lane& l : lanes) {
     if (l.stream) (void)hipStreamSynchronize(l.stream);
@@ -669,8 +689,13 @@ Region region_for(const HostJob& j, size_t base, size_t m) {
 // compute stream runs chunk i, the copy stream stages chunk i+1's inputs and returns chunk
 // i-1's outputs (host order H2D(i+1), K(i+1), D2H(i): the pageable D2H blocks this thread
 // until K(i) is done, by which time K(i+1) is queued behind it). Synchronous overall.
+int run_host_pipe(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t cnt);
 int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t cnt) {
   HSTAMP(0);
+  // (EGES_HOST_PIPE = 2: tests force the pipeline for any batch larger than its first chunk)
+  if (j.kind != HostJob::SENDER_RAW &&
+      ((rt.host_pipe == 1 && cnt >= 2 * PIPE_MIN) || (rt.host_pipe == 2 && cnt > rt.pipe_first)))
+    return run_host_pipe(d, rt, j, off, cnt);
   DevGuard g(d.id);
   // a shard big enough to pipeline runs as >= 2 chunks (each still a full resident grid)
   size_t c = std::min(CHUNK, cnt);
@@ -940,6 +965,282 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
 #undef H2D
 #undef FLUSH_IN
 #undef JOIN_IN
+}
+
+// ------------------------------------------------------------------ pipelined host-buffer calls
+// Host memcpy workers (a process-wide pool, created on first use): the caller's pageable buffers
+// are copied into pinned staging by several threads at once, so that the DMA engines then move
+// them at the link's rate (tools/memcpy_probe.cpp). The calling thread takes a share too.
+class CopyPool {
+ public:
+  struct Task {
+    uint8_t* dst;
+    const uint8_t* src;
+    size_t n;
+  };
+  static CopyPool& get() {
+    static CopyPool* p = new CopyPool(4);  // never destroyed: detached workers live to process exit
+    return *p;
+  }
+  void run(const std::vector<Task>& tasks) {
+    std::vector<Task> pieces;
+    for (const Task& t : tasks)
+      for (size_t o = 0; o < t.n; o += PIECE) pieces.push_back({t.dst + o, t.src + o, std::min(PIECE, t.n - o)});
+    if (pieces.empty()) return;
+    std::lock_guard<std::mutex> one(run_mu_);  // one job at a time (several devices' threads may call)
+    std::atomic<size_t> next{0}, left{pieces.size()};
+    auto work = [&] {
+      for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
+        std::memcpy(pieces[k].dst, pieces[k].src, pieces[k].n);
+        left.fetch_sub(1, std::memory_order_release);
+      }
+    };
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = work;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    while (left.load(std::memory_order_acquire) != 0) cpu_relax();
+    {
+      std::lock_guard<std::mutex> lk(mu_);  // workers that wake late find no job ...
+      job_ = nullptr;
+    }
+    // ... and none still inside this one touches its (stack) state after we return
+    while (active_.load(std::memory_order_acquire) != 0) cpu_relax();
+  }
+
+ private:
+  static constexpr size_t PIECE = size_t(1) << 20;
+  explicit CopyPool(int n) {
+    for (int i = 0; i < n; ++i) std::thread([this] { loop(); }).detach();
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      std::function<void()> job;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        job = job_;
+        if (job) active_.fetch_add(1, std::memory_order_relaxed);
+      }
+      if (job) {
+        job();
+        active_.fetch_sub(1, std::memory_order_release);
+      }
+    }
+  }
+  std::mutex mu_, run_mu_;
+  std::condition_variable cv_;
+  std::function<void()> job_;
+  uint64_t gen_ = 0;
+  std::atomic<int> active_{0};
+};
+
+// A multi-chunk host-buffer call (RECOVER / SENDER / VERIFY / PRECOMPILE) as a four-stage
+// pipeline over chunks: host copy into a pinned slot (CopyPool) -> DMA to the device (stream
+// hin) -> kernels (two compute streams alternating, each with its own workspace, so one chunk's
+// launch starts while the previous one's last waves drain) -> DMA back into the pinned slot
+// (stream hout) -> host copy into the caller's outputs. Two slots alternate. The first chunk is
+// smaller (EGES_PIPE_FIRST), so the GPU starts after a short copy. Synchronous overall.
+struct PipeArr {
+  const uint8_t* src;
+  uint8_t* dst;
+  size_t w;  // bytes per item
+};
+int run_host_pipe(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t cnt) {
+  DevGuard g(d.id);
+  std::unique_lock<std::mutex> lk(d.mu);
+  // chunk schedule: a smaller first chunk, then near-equal chunks of at most rt.pipe_chunk
+  std::vector<std::pair<size_t, size_t>> ch;
+  {
+    const size_t C = std::max<size_t>(64, std::min(rt.pipe_chunk, CHUNK));
+    const size_t f = std::min(cnt, std::max<size_t>(64, std::min(rt.pipe_first, C)));
+    ch.push_back({off, f});
+    const size_t rem = cnt - f;
+    const size_t parts = (rem + C - 1) / C;
+    for (size_t k = 0, b = off + f; k < parts; ++k) {
+      const size_t m = rem / parts + (k < rem % parts ? 1 : 0);
+      ch.push_back({b, m});
+      b += m;
+    }
+  }
+  size_t cmax = 0;
+  for (auto& c : ch) cmax = std::max(cmax, c.second);
+  // per-item inputs and outputs of the kind (in the order the kernels read them from the region)
+  std::vector<PipeArr> in, out;
+  const size_t astride = j.kind == HostJob::PRECOMPILE ? 32 : 20;
+  switch (j.kind) {
+    case HostJob::RECOVER:
+      in = {{j.a, nullptr, 32}, {j.b, nullptr, 65}};
+      break;
+    case HostJob::SENDER:
+      in = {{j.a, nullptr, 32}, {j.b, nullptr, 32}, {j.c, nullptr, 32}, {j.d, nullptr, 32}};
+      if (j.e) in.push_back({j.e, nullptr, 1});
+      break;
+    case HostJob::VERIFY:
+      in = {{j.a, nullptr, 65}, {j.b, nullptr, 1}, {j.c, nullptr, 32}, {j.d, nullptr, 64}};
+      break;
+    case HostJob::PRECOMPILE:
+      in = {{j.a, nullptr, 128}};
+      if (j.inlen) in.push_back({reinterpret_cast<const uint8_t*>(j.inlen), nullptr, 4});
+      break;
+    default:
+      return set_err(EGES_E_INVALID_ARG, "run_host_pipe: unsupported kind");
+  }
+  if (j.pub) out.push_back({nullptr, j.pub, 65});
+  if (j.addr) out.push_back({nullptr, j.addr, astride});
+  out.push_back({nullptr, j.status, 1});
+  size_t in_w = 0, out_w = 0;
+  for (auto& a : in) in_w += a.w;
+  for (auto& a : out) out_w += a.w;
+  // device region per slot: inputs | record / verify scratch | outputs
+  const size_t cpad = align_up(cmax, 64);
+  const size_t rec_bytes = j.kind == HostJob::VERIFY ? verify_scratch_bytes(cpad) : recover_scratch_bytes(cpad);
+  const size_t o_rec = align_up(cmax * in_w + 256 * in.size(), 256);
+  const size_t o_out = o_rec + align_up(rec_bytes, 256);
+  const size_t R = align_up(o_out + cmax * out_w + 256 * out.size(), 256);
+  int rc = dev_ensure_buf(d, 2 * R);
+  if (rc) return rc;
+  if (!d.aux) {
+    HIPCHK(hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&d.ev_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&d.ev_join, hipEventDisableTiming));
+    HIPCHK(hipMalloc(&d.ws2, ws_bytes_per_block() * (size_t)d.ws_blocks));
+  }
+  if (!d.hin) {
+    HIPCHK(hipStreamCreateWithFlags(&d.hin, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&d.hout, hipStreamNonBlocking));
+    for (int r = 0; r < 2; ++r) HIPCHK(hipEventCreateWithFlags(&d.ev_out[r], hipEventDisableTiming));
+  }
+  const size_t slot = align_up(cmax * in_w + 256 * in.size(), 256) + align_up(cmax * out_w + 256 * out.size(), 256);
+  if (slot > d.ring_cap) {
+    for (int r = 0; r < 2; ++r) {
+      if (d.ring[r]) HIPCHK(hipHostFree(d.ring[r]));
+      d.ring[r] = nullptr;
+    }
+    d.ring_cap = 0;
+    for (int r = 0; r < 2; ++r)
+      if (hipHostMalloc(&d.ring[r], slot, hipHostMallocDefault) != hipSuccess)
+        return set_err(EGES_E_NOMEM, "hipHostMalloc(%zu) failed", slot);
+    d.ring_cap = slot;
+  }
+  const size_t pin_out = align_up(cmax * in_w + 256 * in.size(), 256);
+  hipStream_t cs[2] = {d.stream, d.aux};
+  uint32_t* wsr[2] = {d.ws, d.ws2};
+  struct Drain {
+    hipStream_t s[4];
+    bool armed;
+    ~Drain() {
+      if (!armed) return;
+      for (hipStream_t x : s) (void)hipStreamSynchronize(x);
+    }
+  } drain{{d.hin, cs[0], cs[1], d.hout}, true};
+  for (hipStream_t x : {d.hin, cs[0], cs[1], d.hout}) HIPCHK(hipStreamWaitEvent(x, d.last, 0));
+  // offsets of each array inside a slot's input / output block, for a chunk of m items
+  auto offs = [](const std::vector<PipeArr>& v, size_t m) {
+    std::vector<size_t> o;
+    size_t x = 0;
+    for (const PipeArr& a : v) {
+      o.push_back(x);
+      x = align_up(x + m * a.w, 256);
+    }
+    o.push_back(x);  // total
+    return o;
+  };
+  auto copy_out = [&](size_t ci) {
+    const size_t base = ch[ci].first, m = ch[ci].second;
+    const auto oo = offs(out, m);
+    std::vector<CopyPool::Task> t;
+    for (size_t k = 0; k < out.size(); ++k)
+      t.push_back({out[k].dst + base * out[k].w, d.ring[ci & 1] + pin_out + oo[k], m * out[k].w});
+    CopyPool::get().run(t);
+  };
+  for (size_t ci = 0; ci < ch.size(); ++ci) {
+    const int r = (int)(ci & 1);
+    const size_t base = ch[ci].first, m = ch[ci].second, m_pad = align_up(m, 64);
+    uint8_t* B = d.buf + (size_t)r * R;
+    uint8_t* P = d.ring[r];
+    const auto io = offs(in, m), oo = offs(out, m);
+    // 1. host copy into the pinned slot (free: chunk ci - 2 was copied out in iteration ci - 1)
+    {
+      std::vector<CopyPool::Task> t;
+      for (size_t k = 0; k < in.size(); ++k) t.push_back({P + io[k], in[k].src + base * in[k].w, m * in[k].w});
+      CopyPool::get().run(t);
+    }
+    // 2. DMA in, after the kernels of chunk ci - 2 (same device region) are done
+    if (ci >= 2) HIPCHK(hipStreamWaitEvent(d.hin, d.ev_k[r], 0));
+    HIPCHK(hipMemcpyAsync(B, P, io.back(), hipMemcpyHostToDevice, d.hin));
+    HIPCHK(hipEventRecord(d.ev_in[r], d.hin));
+    // 3. kernels on this slot's compute stream and workspace
+    hipStream_t st = cs[r];
+    HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
+    uint32_t* rec = reinterpret_cast<uint32_t*>(B + o_rec);
+    uint8_t* O = B + o_out;
+    uint8_t* o_pub = nullptr;
+    uint8_t* o_addr = nullptr;
+    uint8_t* o_st = nullptr;
+    {
+      size_t k = 0;
+      if (j.pub) o_pub = O + oo[k++];
+      if (j.addr) o_addr = O + oo[k++];
+      o_st = O + oo[k];
+    }
+    const uint8_t* I[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    for (size_t k = 0; k < in.size(); ++k) I[k] = B + io[k];
+    if (j.kind == HostJob::RECOVER) {
+      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, o_pub, d.gtab, wsr[r]};
+      if (fused_parse(d, rt, m)) {
+        p.raw_msg = I[0];
+        p.raw_sig = I[1];
+      } else {
+        HIPCHK(launch_prep_ecrecover(I[0], I[1], (uint32_t)m, (uint32_t)m_pad, rec, st));
+      }
+      HIPCHK(launch_recover_pass(d, rt, p, st));
+    } else if (j.kind == HostJob::SENDER) {
+      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, wsr[r]};
+      const uint8_t* vf = j.e ? I[4] : nullptr;
+      if (sender_fused(d, rt, m, {I[0], I[1], I[2], I[3]}))
+        bind_sender_rows(p, I[0], I[1], I[2], I[3], vf, j.signer, j.chain_id);
+      else
+        HIPCHK(launch_prep_sender(I[0], I[1], I[2], I[3], vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, st));
+      HIPCHK(launch_recover_pass(d, rt, p, st));
+    } else if (j.kind == HostJob::PRECOMPILE) {
+      HIPCHK(hipMemsetAsync(o_addr, 0, m * 32, st));
+      HIPCHK(launch_prep_precompile(I[0], j.inlen ? reinterpret_cast<const uint32_t*>(I[1]) : nullptr, (uint32_t)m,
+                                    (uint32_t)m_pad, rec, st));
+      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr + 12, nullptr, d.gtab, wsr[r], 32};
+      HIPCHK(launch_recover_pass(d, rt, p, st));
+    } else {
+      VerifyParams p{I[0], I[1], I[2], I[3], (uint32_t)m, o_st, d.gtab, wsr[r]};
+      verify_scratch_bind(p, B + o_rec, m_pad);
+      p = with_diag(d, p, rt);
+      if (m <= rt.lat_max) HIPCHK(launch_verify_lat(p, p.n <= rt.wide_max, st));
+      else HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
+    }
+    HIPCHK(hipEventRecord(d.ev_k[r], st));
+    // 4. DMA out into the pinned slot
+    HIPCHK(hipStreamWaitEvent(d.hout, d.ev_k[r], 0));
+    HIPCHK(hipMemcpyAsync(P + pin_out, O, oo.back(), hipMemcpyDeviceToHost, d.hout));
+    HIPCHK(hipEventRecord(d.ev_out[r], d.hout));
+    // 5. the previous chunk's outputs into the caller's buffers, while this chunk computes
+    if (ci >= 1) {
+      HIPCHK(hipEventSynchronize(d.ev_out[r ^ 1]));
+      copy_out(ci - 1);
+    }
+  }
+  const size_t last = ch.size() - 1;
+  HIPCHK(hipEventSynchronize(d.ev_out[last & 1]));
+  copy_out(last);
+  for (hipStream_t x : {d.hin, cs[0], cs[1], d.hout}) HIPCHK(hipStreamSynchronize(x));
+  drain.armed = false;
+  HIPCHK(hipEventRecord(d.last, d.hout));
+  if (j.status && std::memchr(j.status + off, EGES_ENGINE_FAULT, cnt))
+    return set_err(EGES_E_HIP, "a kernel hand-off timed out (EGES_ENGINE_FAULT items; EGES_DIAG_HANDOFF)");
+  return EGES_SUCCESS;
 }
 
 // Contiguous index shards across the engine's devices.

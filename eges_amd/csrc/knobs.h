@@ -27,6 +27,10 @@ enum KnobId : int {
   KNOB_COALESCE_SPINNERS,   //   at most this many callers spin at once
   KNOB_SENDER_FUSED,      // 1: sender rows of latency / mid-size batches are classified inside the
                           //   recover kernel (no prep_sender launch); 0: prep_sender_kernel first
+  KNOB_HOST_PIPE,         // 1: multi-chunk host-buffer calls run the pinned-slot pipeline (run_host_pipe);
+                          //   0: the older pageable-copy path; 2 (tests): any batch above PIPE_FIRST
+  KNOB_PIPE_CHUNK,        //   its chunk size (signatures)
+  KNOB_PIPE_FIRST,        //   and its first, smaller chunk
   KNOB_TEST_SKIP_FLAG,    // tests: k > 0 makes the first workgroup's producer of hand-off flag k - 1
                           //   skip publishing it (handoff.cuh), so its consumers time out
   KNOB_COUNT

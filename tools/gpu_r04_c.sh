@@ -22,3 +22,12 @@ for i in 1 2; do
   LD_LIBRARY_PATH=$PWD/tools/abbase timeout -k 10 120 tools/single_bench 1 300 > $O/single_c_$i.json 2>&1
   cat $O/single_asm_$i.json $O/single_c_$i.json
 done
+timeout -k 10 120 tools/memcpy_probe > $O/memcpy_probe.txt 2>&1
+cat $O/memcpy_probe.txt
+timeout -k 10 200 python bench.py --config c2host --steps 5 --warmup 2 > $O/c2host.json 2> $O/c2host.err
+cat $O/c2host.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c2host -o run --output-format csv -- python3 bench.py --config c2host --steps 3 --warmup 1 > $O/prof_c2host.log 2>&1
+for b in 65536 131072 262144 524288 1048576; do
+  timeout -k 10 120 python bench.py --batch $b --steps 5 --warmup 2 --no-secondary --no-cpu-baseline > $O/c2_b$b.json 2> $O/c2_b$b.err
+  python -c "import json,sys; d=json.load(open('$O/c2_b$b.json')); print($b, d['roofline']['kernel_ms'], d['value'])"
+done
