@@ -417,6 +417,17 @@ bool use_mid(const Dev& d, const Route& rt, size_t n) {
   if (n <= rt.lat_max || n > rt.mid_max) return false;
   return mid_bucket(d, rt, n) || (n + 63) / 64 * mid_ws_bytes_per_block() <= dev_ws_bytes(d);
 }
+// VerifySignature batches above LAT_MAX that the bucket form's verify mode takes (one generation of
+// workgroups: n <= 64 x CUs), instead of the lane-serial verify kernel's fixed chain
+bool verify_mid(const Dev& d, const Route& rt, size_t n) {
+  return rt.mid_form != 0 && n > rt.lat_max && n <= rt.mid_max &&
+         (n + MID_SIGS_PER_BLOCK - 1) / MID_SIGS_PER_BLOCK <= (size_t)d.cus;
+}
+hipError_t launch_verify_any(Dev& d, const Route& rt, const VerifyParams& p, bool small, hipStream_t st) {
+  if (small || p.n <= rt.lat_max) return launch_verify_lat(p, p.n <= rt.wide_max, st);
+  if (verify_mid(d, rt, p.n)) return launch_verify_mid(p, st);
+  return launch_verify(p, d.mb_verify, d.ws_blocks, st);
+}
 // the recover kernels that parse msg / sig bytes themselves (no prep launch)
 bool fused_parse(const Dev& d, const Route& rt, size_t n) { return n <= rt.lat_max || use_mid(d, rt, n); }
 // ... and classify types.Sender rows themselves (no prep_sender launch): 4-byte aligned rows only
@@ -638,8 +649,7 @@ int run_verify_dev(Dev& d, const Route& rt, const uint8_t* pub, const uint8_t* p
     VerifyParams p{pub + off * 65, publen + off, msg + off * 32, sig + off * 64, m, ok + off, d.gtab, d.ws};
     verify_scratch_bind(p, d.buf, n_pad);
     p = with_diag(d, p, rt);
-    if (m <= rt.lat_max) HIPCHK(launch_verify_lat(p, p.n <= rt.wide_max, st));
-    else HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
+    HIPCHK(launch_verify_any(d, rt, p, false, st));
   }
   return EGES_SUCCESS;
 }
@@ -933,8 +943,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       verify_scratch_bind(p, B + rg.o_rec, m_pad);
       p = with_diag(d, p, rt);
       // small (lane) calls must not touch the device's shared workspace: latency kernel
-      if (small || m <= rt.lat_max) HIPCHK(launch_verify_lat(p, p.n <= rt.wide_max, st));
-      else HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
+      HIPCHK(launch_verify_any(d, rt, p, small, st));
     }
     HSTAMP(3);
     if (sx != st) HIPCHK(hipEventRecord(ev_k[r], st));
@@ -1218,8 +1227,7 @@ int run_host_pipe(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t 
       VerifyParams p{I[0], I[1], I[2], I[3], (uint32_t)m, o_st, d.gtab, wsr[r]};
       verify_scratch_bind(p, B + o_rec, m_pad);
       p = with_diag(d, p, rt);
-      if (m <= rt.lat_max) HIPCHK(launch_verify_lat(p, p.n <= rt.wide_max, st));
-      else HIPCHK(launch_verify(p, d.mb_verify, d.ws_blocks, st));
+      HIPCHK(launch_verify_any(d, rt, p, false, st));
     }
     HIPCHK(hipEventRecord(d.ev_k[r], st));
     // 4. DMA out into the pinned slot

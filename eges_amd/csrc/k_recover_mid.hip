@@ -631,7 +631,41 @@ __device__ __attribute__((noinline)) bool wire_r_only(const BktLds& S, const Rec
   return ok;
 }
 
-template <class ST>
+// VerifySignature mode (VERIFY): item idx's signature, message and public key as the lane-serial
+// verify kernel parses them (k_verify.hip verify_parse; eckey_impl.h:17-34, secp256k1.c:293-308):
+// q.R = r, q.Sv = s, q.Z = z, q.xr = the key's x, q.ok = the signature and key checks that need
+// no field arithmetic; py / c65 / odd for wave S's y (given, or the root of a 33-byte key).
+DEV void verify_parse_lane(const RecoverParams& prm, uint32_t idx, LatParse& q, uint32_t py[8], bool& c65, bool& odd) {
+  uint32_t l[8];
+  bool ovr, ovs, ovz;
+  limbs_from_be32(l, prm.v_sig + (size_t)idx * 64);
+  q.R = sc_from_limbs(l, ovr);
+  limbs_from_be32(l, prm.v_sig + (size_t)idx * 64 + 32);
+  q.Sv = sc_from_limbs(l, ovs);
+  limbs_from_be32(l, prm.v_msg + (size_t)idx * 32);
+  q.Z = sc_from_limbs(l, ovz);  // the message reduced mod n
+  const bool sig_ok = !ovr && !ovs && !sc_is_high(q.Sv) && !sc_is_zero(q.R) && !sc_is_zero(q.Sv);
+  const uint32_t plen = prm.v_publen[idx];
+  const uint8_t* pk = prm.v_pub + (size_t)idx * 65;
+  const uint32_t pfx = pk[0];
+  limbs_from_be32(q.xr, pk + 1);
+  if (plen == 65) {
+    limbs_from_be32(py, pk + 33);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) py[k] = 0;
+  }
+  const bool x_ok = !u256_ge(q.xr, FE_P), y_ok = !u256_ge(py, FE_P);
+  const bool c33 = plen == 33 && (pfx == 2 || pfx == 3);
+  c65 = plen == 65 && (pfx == 4 || pfx == 6 || pfx == 7);
+  const bool hybrid_bad = (pfx == 6 || pfx == 7) && ((py[0] & 1u) != (pfx == 7 ? 1u : 0u));
+  q.ok = sig_ok && ((c33 && x_ok) || (c65 && x_ok && y_ok && !hybrid_bad));
+  odd = pfx == 3;
+  q.meta = 0;
+  q.recid = 0;
+}
+
+template <class ST, bool VERIFY = false>
 DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
   __shared__ BktLds S;
   ST st_;
@@ -639,14 +673,18 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
   const uint32_t l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t idx = blockIdx.x * MID_L + l;
   const bool live = idx < prm.n;
-  const bool wire = prm.wire_raw != nullptr;  // kernel-uniform
+  const bool wire = !VERIFY && prm.wire_raw != nullptr;  // kernel-uniform
   uint64_t stage_a0 = 0, stage_end = 0;
   if (threadIdx.x < BF_N) S.flag[threadIdx.x] = 0u;
   if (wire) wire_stage(S, prm, stage_a0, stage_end);
   __syncthreads();  // the only barrier
   LatParse q;
   Payload m;
-  if (!wire) {
+  uint32_t vpy[8];
+  bool vc65 = false, vodd = false;
+  if (VERIFY) {
+    verify_parse_lane(prm, live ? idx : prm.n - 1, q, vpy, vc65, vodd);
+  } else if (!wire) {
     q = prm.snd_r ? sender_parse_lane(prm, live ? idx : prm.n - 1) : lat_parse(prm, live ? idx : prm.n - 1);
   } else if (wv == 1) {
     wire_parse(S, prm, live ? idx : prm.n - 1, stage_a0, stage_end, q, m);
@@ -671,9 +709,11 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
   const fe x = fe_select(pok, fe_from_u256(q.xr), G.x);
   if (wv == 1) {  // ---- S: scalars, digits, y, u1 G
     st_.mark(0);
-    const sc R = sc_select(pok, q.R, sc_one());
+    // recovery: r^-1, u2 = s / r, u1 = -z / r (main_impl.h:114-117); verification: s^-1,
+    // u2 = r / s, u1 = z / s (ecdsa_impl.h:203-271)
+    const sc R = sc_select(pok, VERIFY ? q.Sv : q.R, sc_one());
     const sc rinv = EGES_BK_VARINV ? sc_inv_var(R) : sc_inv(R);
-    const sc u2 = sc_select(pok, sc_mul(rinv, q.Sv), sc_one());
+    const sc u2 = sc_select(pok, sc_mul(rinv, VERIFY ? q.R : q.Sv), sc_one());
     st_.mark(1);
     glv_half h1, h2;
     glv_split(h1, h2, u2);
@@ -705,9 +745,21 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
       q.Z = sc_from_limbs(zl, ovz);  // msg mod n (main_impl.h:183)
       st_.mark(5);
     }
-    const sc u1 = sc_neg(sc_mul(rinv, q.Z));  // main_impl.h:114-117
+    const sc u1 = VERIFY ? sc_mul(rinv, q.Z) : sc_neg(sc_mul(rinv, q.Z));  // main_impl.h:114-117
     ge Rp;
-    const bool yok = ge_set_xo(Rp, x, pok && (q.recid & 1u) != 0);  // ge_set_xo_var, group_impl.h:216-237
+    bool yok;
+    if (VERIFY && __all(vc65 || !pok)) {  // every key of the wave uncompressed: no root (wave-uniform)
+      Rp.y = fe_from_u256(vpy);
+      yok = true;
+    } else {
+      yok = ge_set_xo(Rp, x, VERIFY ? vodd : pok && (q.recid & 1u) != 0);  // ge_set_xo_var, group_impl.h:216-237
+    }
+    if (VERIFY && vc65) {  // a 65-byte key: its own y, on the curve (eckey_impl.h:17-34)
+      const fe yk = fe_from_u256(vpy);
+      const fe cx = fe_add(fe_mul(fe_sqr(x), x), fe_from_u32(7));
+      yok = fe_equal(cx, fe_sqr(yk));
+      Rp.y = yk;
+    }
     lds_put_fe<FE_LIMBS>(S.y, Rp.y.v, l);
     S.yok[l] = yok ? 1u : 0u;
     BFLAG_SET(BF_Y);
@@ -848,6 +900,24 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
   }
   const bool fault = ho_failed(&S.flag[BF_ERR], dg);  // after Y1's last wait
   const bool ok = (wire ? S.pok[l] != 0 : pok) && yok && !qinf && !fault;  // main_impl.h:120
+  if constexpr (VERIFY) {
+    // x(Q) mod n == r  <=>  r Z^2 == X  or  (r < p - n and (r + n) Z^2 == X)  (ecdsa_impl.h:246-270)
+    const fe z2 = fe_sqr(Q.z);
+    bool eq = fe_equal(Q.x, fe_mul(fe_from_u256(q.R.v), z2));
+    uint32_t rn[8];
+    uint64_t cy = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      cy += (uint64_t)q.R.v[k] + SC_N[k];
+      rn[k] = (uint32_t)cy;
+      cy >>= 32;
+    }
+    eq = eq || (!u256_ge(q.R.v, P_MINUS_N) && fe_equal(Q.x, fe_mul(fe_from_u256(rn), z2)));
+    if (live) prm.v_ok[idx] = fault ? (uint8_t)ST_ENGINE_FAULT : (ok && eq) ? 1 : 0;
+    st_.mark(7);
+    stamp_out();
+    return;
+  }
   if (__any(ok && fe_is_zero(Q.z))) diag_bump(dg, EGES_DIAG_MID_EXC);  // never (see above)
   st_.mark(5);
   const fe zq = fe_select(ok, Q.z, fe_one());
@@ -886,11 +956,31 @@ __global__ void __launch_bounds__(MID_WG, 1) recover_bkt_kernel(RecoverParams pr
   recover_bkt_body<NoStamp>(prm, nullptr);
 }
 
+__global__ void __launch_bounds__(MID_WG, 1) verify_bkt_kernel(RecoverParams prm) {
+  recover_bkt_body<NoStamp, true>(prm, nullptr);
+}
+
 __global__ void __launch_bounds__(MID_WG, 2) recover_mid_kernel(RecoverParams prm) {
   recover_mid_body<NoStamp>(prm, nullptr);
 }
 
 size_t mid_ws_bytes_per_block() { return MID_WS_WORDS * sizeof(uint32_t); }
+
+hipError_t launch_verify_mid(const VerifyParams& v, hipStream_t st) {
+  if (v.n == 0) return hipSuccess;
+  RecoverParams p{nullptr, v.n, v.n, nullptr, nullptr, nullptr, v.gtab, nullptr};
+  p.diag = v.diag;
+  p.force_redo = v.force_redo;
+  p.test_skip_flag = v.test_skip_flag;
+  p.test_skip_block = v.test_skip_block;
+  p.v_pub = v.pub;
+  p.v_publen = v.publen;
+  p.v_msg = v.msg;
+  p.v_sig = v.sig;
+  p.v_ok = v.ok;
+  hipLaunchKernelGGL(verify_bkt_kernel, dim3((v.n + MID_L - 1) / MID_L), dim3(MID_WG), 0, st, p);
+  return hipGetLastError();
+}
 
 // ws must hold ceil(n / 64) blocks of mid_ws_bytes_per_block(); the caller checks
 hipError_t launch_recover_mid(const RecoverParams& p, bool bucket, size_t ws_bytes, hipStream_t st) {

@@ -56,6 +56,10 @@ struct RecoverParams {
   const uint8_t *snd_h = nullptr, *snd_r = nullptr, *snd_s = nullptr, *snd_v = nullptr, *snd_f = nullptr;
   int snd_signer = 0;
   uint64_t snd_chain_id = 0;
+  // mid-size bucket form, crypto.VerifySignature mode (launch_verify_mid): the verify inputs
+  // (VerifyParams' pub n x 65, publen, msg n x 32, sig n x 64) and its 0/1 output instead
+  const uint8_t *v_pub = nullptr, *v_publen = nullptr, *v_msg = nullptr, *v_sig = nullptr;
+  uint8_t* v_ok = nullptr;
   // mid-size bucket form only: wire-format transactions instead of record rows (tx_rows_kernel
   // and prep_sender_kernel fused in): item i is wire_raw[wire_off[first + i] - wire_off[0],
   // wire_off[first + i + 1] - wire_off[0]); wire_raw 4-byte aligned. wire_sighash: n x 32 or null.
@@ -136,6 +140,9 @@ hipError_t launch_recover_mid(const RecoverParams& p, bool bucket, size_t ws_byt
 size_t mid_ws_bytes_per_block();
 constexpr uint32_t MID_SIGS_PER_BLOCK = 64;
 hipError_t launch_verify(const VerifyParams& p, int max_blocks, int ws_blocks, hipStream_t st);
+// VerifySignature on the mid-size kernel's bucket form (64 items per 4-wave workgroup, one per CU
+// at most: n <= 64 x CUs; no workspace)
+hipError_t launch_verify_mid(const VerifyParams& p, hipStream_t st);
 // one item per 128-thread workgroup (k_recover_lat.hip; wide: 192 threads, three partial sums);
 // uses pub/publen/msg/sig/n/ok/gtab only
 hipError_t launch_verify_lat(const VerifyParams& p, bool wide, hipStream_t st);

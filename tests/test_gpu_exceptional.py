@@ -182,8 +182,10 @@ def test_verify_exceptional_sums_every_form(engine, oracle):
         assert np.array_equal(ok, exp), (form, np.nonzero(ok != exp)[0])
         if form == "lane_serial":
             assert d["ls_redo"] > 0 and d["ls_exc"] > 0, d
-        elif form in ("mid", "mid_bucket"):  # (verification has no mid-size form: lane-serial runs)
+        elif form == "mid":  # (verification has no windowed mid-size form: lane-serial runs)
             assert d["ls_redo"] > 0 and d["ls_exc"] > 0, d
+        elif form == "mid_bucket":  # the bucket form's verify mode: the exact final join
+            assert d["mid_join"] > 0 and d["mid_exc"] == 0, d
         else:
             assert d["join_dbl"] > 0 and d["join_inf"] > 0, (form, d)
     for i in range(n):
@@ -206,7 +208,9 @@ def test_forced_redo_every_form_golden(engine):
         assert np.array_equal(ok, gv["ok"]), form
         if form == "lane_serial":
             assert d["ls_redo"] > 0, d
-        elif form in ("mid", "mid_bucket"):
+        elif form == "mid":
             assert d["mid_redo"] > 0 and d["ls_redo"] > 0, d  # recovery: mid-size; verification: lane-serial
+        elif form == "mid_bucket":
+            assert d["mid_redo"] > 0, d  # recovery and verification both on the bucket form
         else:
             assert d["lat_redo"] > 0 and d["comb_redo"] > 0, (form, d)

@@ -131,3 +131,19 @@ def test_verify_split_form_skipped_flag_faults_one_item(engine):
     with knobs(engine, SPLIT):
         assert np.array_equal(engine.verify_batch(pub, publen, msg, sig), g["ok"][:n])
     engine.diag_counters(reset=True)
+
+
+def test_verify_bucket_form_skipped_flag_faults_one_workgroup(engine):
+    """the bucket form's VerifySignature mode: a skipped digit flag faults workgroup 0's items"""
+    g = load_golden("verify.npz")
+    n = 300
+    rep = -(-n // len(g["pub"]))
+    pub, publen, msg, sig, exp = (np.ascontiguousarray(np.concatenate([g[k]] * rep)[:n])
+                                  for k in ("pub", "publen", "msg", "sig", "ok"))
+    ok = np.full(n, 0xEE, np.uint8)
+    with knobs(engine, dict(BUCKET, EGES_TEST_SKIP_FLAG=1)):
+        rc = _lib.lib.eges_verify_batch(_p(pub), _p(publen), _p(msg), _p(sig), n, _p(ok))
+    assert rc == -3
+    assert (ok[:64] == _lib.ENGINE_FAULT).all()
+    assert np.array_equal(ok[64:], exp[64:])
+    engine.diag_counters(reset=True)
