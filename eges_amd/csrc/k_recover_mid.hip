@@ -27,12 +27,16 @@
 
 #include "core.cuh"
 #include "handoff.cuh"
+#include "modinv_row.cuh"
 #include "sender.cuh"
 
 namespace eges {
 
 constexpr int MID_WG = 256;  // four waves
 constexpr int MID_L = 64;    // signatures per workgroup (one per lane)
+#ifndef EGES_MID_BATCHINV
+#define EGES_MID_BATCHINV 1  // final Z^-1 by Montgomery's trick across the wave (fe_inv_wave); 0: per lane
+#endif
 #ifndef EGES_MID_W0
 #define EGES_MID_W0 15
 #endif
@@ -401,7 +405,10 @@ DEV void recover_mid_body(const RecoverParams& prm, uint64_t* stamps) {
   const bool fault = ho_failed(&S.flag[MF_ERR], dg);  // after A's last wait
   const bool ok = pok && yok && !qinf && !fault;  // main_impl.h:120
   // affine, serialize, address
-  const fe zi = fe_inv(fe_select(ok, Q.z, fe_one()));
+  // (a zero factor would zero the whole wave's batch inversion: such a lane, which the exceptional-sum
+  // argument excludes, takes 1 and keeps its own wrong value to itself)
+  const fe zq = fe_select(ok && !fe_is_zero(Q.z), Q.z, fe_one());
+  const fe zi = EGES_MID_BATCHINV ? fe_inv_wave(zq) : fe_inv(zq);
   const fe zi2 = fe_sqr(zi);
   uint32_t X[8], Y[8];
   fe_to_u256(X, fe_normalize(fe_mul(Q.x, zi2)));
@@ -920,8 +927,8 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
   }
   if (__any(ok && fe_is_zero(Q.z))) diag_bump(dg, EGES_DIAG_MID_EXC);  // never (see above)
   st_.mark(5);
-  const fe zq = fe_select(ok, Q.z, fe_one());
-  const fe zi = EGES_BK_VARINV ? fe_inv_var(zq) : fe_inv(zq);
+  const fe zq = fe_select(ok && !fe_is_zero(Q.z), Q.z, fe_one());  // (see recover_mid_body)
+  const fe zi = EGES_BK_VARINV ? fe_inv_var(zq) : EGES_MID_BATCHINV ? fe_inv_wave(zq) : fe_inv(zq);
   const fe zi2 = fe_sqr(zi);
   uint32_t X[8], Y[8];
   fe_to_u256(X, fe_normalize(fe_mul(Q.x, zi2)));

@@ -2,8 +2,9 @@
 per wave) against the fixtures, the oracle and the other two recover forms.
 
 Forms are selected with engine knobs (eges_test_set_knob): EGES_LAT_MAX = 0 and EGES_MID_MAX
-large send every batch through the mid-size kernel, in its bucket form (EGES_MID_FORM = 1, the
-default) or its windowed form (0); EGES_MID_MAX = 0 sends it through the lane-serial kernel.
+large send every batch through the mid-size kernel, in its bucket form (EGES_MID_FORM = 2; the
+default 1 is auto: bucket while the grid fits one workgroup per CU) or its windowed form (0);
+EGES_MID_MAX = 0 sends it through the lane-serial kernel.
 Every output byte must agree across forms and with the reference-generated fixtures."""
 import numpy as np
 import pytest

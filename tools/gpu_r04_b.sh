@@ -42,3 +42,10 @@ for b in 65536 131072 262144 524288 1048576; do
   timeout -k 10 120 python bench.py --batch $b --steps 5 --warmup 2 --no-secondary --no-cpu-baseline > $O/c2_b$b.json 2> $O/c2_b$b.err
   python -c "import json; d=json.load(open('$O/c2_b$b.json')); print('lane-serial batch', $b, 'kernel_ms', d['roofline']['kernel_ms'], 'sigs/s', d['value'])"
 done
+timeout -k 10 300 python tools/formcurve_verify.py > $O/formcurve_verify.jsonl 2> $O/formcurve_verify.err
+tail -1 $O/formcurve_verify.jsonl
+for i in 1 2 3; do
+  timeout -k 10 200 python bench.py --config c1 --steps 5 --no-cpu-baseline > $O/c1_binv_$i.json 2> $O/c1_binv_$i.err
+  EGES_AB_LIB=$PWD/tools/abmid/libeges.so timeout -k 10 200 python bench.py --config c1 --steps 5 --no-cpu-baseline > $O/c1_lane_$i.json 2> $O/c1_lane_$i.err
+  python -c "import json; a=json.load(open('$O/c1_binv_$i.json')); b=json.load(open('$O/c1_lane_$i.json')); print('c1 batchinv', a['ms_per_batch'], a['roofline']['kernel_ms'], 'per-lane inv', b['ms_per_batch'], b['roofline']['kernel_ms'], a['config']['correct'], b['config']['correct'])"
+done
