@@ -540,7 +540,8 @@ def run_block_latency(c):
             "sigs_per_s": round(n / (m["median_ms"] / 1e3), 1), "n_gpus": 1, "steps": iters, "warmup": a.warmup,
             "higher_is_better": False, "dtype": "u32", "data": "synthetic",
             "config": {"workload": "configs[2]: Geec block import, 1000 txns/block (txnSize 100), EIP155Signer(930412), "
-                                   + m["path"], "correct": m["correct"]}, "cpu_baseline": m.get("cpu")}
+                                   + m["path"], "correct": m["correct"]}, "roofline": m.get("roofline"),
+            "cpu_baseline": m.get("cpu")}
     c.finish(line, m["correct"])
 
 
@@ -645,7 +646,7 @@ def run_c1(c):
             "config": {"workload": f"configs[0]: {n} EIP-155 transfers (nonce i, gasPrice 1, gas 21000, value 1, "
                                    "empty data, chainId 930412) as 10-field txdata RLP through eges_sender_raw_batch "
                                    "(pageable host buffers: H2D + GPU decode + sighash RLP/Keccak + recovery + D2H)",
-                       "correct": m["correct"]}, "cpu_baseline": m.get("cpu")}
+                       "correct": m["correct"]}, "roofline": m.get("roofline"), "cpu_baseline": m.get("cpu")}
     if m.get("cpu"):
         line["vs_cpu"] = round(m["txs_per_s"] / m["cpu"]["value"], 1)
     c.finish(line, m["correct"])
