@@ -338,6 +338,41 @@ DEV fe fe_inv_wave(const fe& z) {
   return fe_mul(fe_from_u256(y), fe_mul(pex, sex));
 }
 
+// The same for scalars mod n (the lane-serial kernels' batched r^-1 / s^-1): every lane's a^-1,
+// every a nonzero mod n, one row-form inversion for the wave.
+DEV sc sc_inv_wave(const sc& a) {
+  const int lane = (int)lane_id();
+  sc P = a;
+#pragma unroll 1
+  for (int d = 1; d < 64; d <<= 1) {
+    const sc y = shfl_up_t(P, d);
+    const sc m = sc_mul(P, y);
+    P = sc_select(lane >= d, m, P);
+  }
+  sc Q = a;
+#pragma unroll 1
+  for (int d = 1; d < 64; d <<= 1) {
+    const sc y = shfl_down_t(Q, d);
+    const sc m = sc_mul(Q, y);
+    Q = sc_select(lane + d < 64, m, Q);
+  }
+  const sc pex = sc_select(lane == 0, sc_one(), shfl_up_t(P, 1));
+  const sc sex = sc_select(lane == 63, sc_one(), shfl_down_t(Q, 1));
+  sc tot;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) tot.v[i] = (uint32_t)__builtin_amdgcn_readlane((int)P.v[i], 63);
+  sc inv;
+  modinv256_row_var<ModN>(inv.v, tot.v);
+  return sc_mul(inv, sc_mul(pex, sex));
+}
+// fe_inv_wave for values that may be zero (the lane-serial kernel's Z products): a zero lane gets
+// 0 (as fe_inv(0)) without zeroing the rest of the wave's batch
+DEV fe fe_inv_wave_z(const fe& z) {
+  const bool zero = fe_is_zero(z);
+  const fe r = fe_inv_wave(fe_select(zero, fe_one(), z));
+  return fe_select(zero, fe_zero(), r);
+}
+
 // Z^-1 in the latency kernel: value replicated over the rows in, same out (row form)
 DEV fr fr_inv_var(fr a, uint64_t* prof = nullptr) {
   uint32_t x[8], y[8];

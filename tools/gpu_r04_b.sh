@@ -49,3 +49,8 @@ for i in 1 2 3; do
   EGES_AB_LIB=$PWD/tools/abmid/libeges.so timeout -k 10 200 python bench.py --config c1 --steps 5 --no-cpu-baseline > $O/c1_lane_$i.json 2> $O/c1_lane_$i.err
   python -c "import json; a=json.load(open('$O/c1_binv_$i.json')); b=json.load(open('$O/c1_lane_$i.json')); print('c1 batchinv', a['ms_per_batch'], a['roofline']['kernel_ms'], 'per-lane inv', b['ms_per_batch'], b['roofline']['kernel_ms'], a['config']['correct'], b['config']['correct'])"
 done
+for i in 1 2 3; do
+  timeout -k 10 200 python bench.py --steps 10 --no-secondary --no-cpu-baseline > $O/c2_binv_$i.json 2> $O/c2_binv_$i.err
+  EGES_AB_LIB=$PWD/tools/abmid/libeges.so timeout -k 10 200 python bench.py --steps 10 --no-secondary --no-cpu-baseline > $O/c2_lane_$i.json 2> $O/c2_lane_$i.err
+  python -c "import json; a=json.load(open('$O/c2_binv_$i.json')); b=json.load(open('$O/c2_lane_$i.json')); print('c2 wave-batch inv', a['value'], a['roofline']['kernel_ms'], 'per-thread inv', b['value'], b['roofline']['kernel_ms'], a['config']['correct'], b['config']['correct'])"
+done
