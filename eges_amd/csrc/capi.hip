@@ -150,8 +150,9 @@ const KnobDef KNOB_DEFS[KNOB_COUNT] = {
     {"EGES_COALESCE_SPINNERS", 8},
     {"EGES_SENDER_FUSED", 1},
     {"EGES_HOST_PIPE", 1},
-    {"EGES_PIPE_CHUNK", 262144},
-    {"EGES_PIPE_FIRST", 131072},
+    {"EGES_PIPE_CHUNK", 786432},
+    {"EGES_PIPE_FIRST", 262144},
+    {"EGES_PIPE_STREAMS", 1},
     {"EGES_TEST_SKIP_FLAG", 0},
 };
 std::atomic<long long> g_knob[KNOB_COUNT];
@@ -179,7 +180,8 @@ struct Route {
   size_t lat_max = 0, mid_max = 0;
   uint32_t wide_max = 0;
   long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, host_pipe = 1;
-  size_t pipe_chunk = 262144, pipe_first = 131072;
+  size_t pipe_chunk = 786432, pipe_first = 262144;
+  long long pipe_streams = 1;
   uint32_t force_redo = 0, skip_flag = 0;
   static Route now() {
     Route r;
@@ -193,6 +195,7 @@ struct Route {
     r.host_pipe = knob(KNOB_HOST_PIPE);
     r.pipe_chunk = (size_t)std::max<long long>(64, knob(KNOB_PIPE_CHUNK));
     r.pipe_first = (size_t)std::max<long long>(64, knob(KNOB_PIPE_FIRST));
+    r.pipe_streams = knob(KNOB_PIPE_STREAMS);
     r.force_redo = knob(KNOB_FORCE_REDO) != 0 ? 1u : 0u;
     r.skip_flag = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TEST_SKIP_FLAG), 64));
     return r;
@@ -1138,8 +1141,12 @@ int run_host_pipe(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t 
     d.ring_cap = slot;
   }
   const size_t pin_out = align_up(cmax * in_w + 256 * in.size(), 256);
-  hipStream_t cs[2] = {d.stream, d.aux};
-  uint32_t* wsr[2] = {d.ws, d.ws2};
+  // One compute stream by default: two lane-serial launches running concurrently double the
+  // per-lane R-table working set past the Infinity Cache (profiles/r04: 78-81 vs 84 M sigs/s);
+  // EGES_PIPE_STREAMS = 2 alternates d.stream / d.aux with their own workspaces (A/B).
+  const bool two = rt.pipe_streams >= 2;
+  hipStream_t cs[2] = {d.stream, two ? d.aux : d.stream};
+  uint32_t* wsr[2] = {d.ws, two ? d.ws2 : d.ws};
   struct Drain {
     hipStream_t s[4];
     bool armed;
@@ -1147,7 +1154,7 @@ int run_host_pipe(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t 
       if (!armed) return;
       for (hipStream_t x : s) (void)hipStreamSynchronize(x);
     }
-  } drain{{d.hin, cs[0], cs[1], d.hout}, true};
+  } drain{{d.hin, cs[0], cs[1], d.hout}, true};  // (cs[1] may equal cs[0]: synchronising twice is harmless)
   for (hipStream_t x : {d.hin, cs[0], cs[1], d.hout}) HIPCHK(hipStreamWaitEvent(x, d.last, 0));
   // offsets of each array inside a slot's input / output block, for a chunk of m items
   auto offs = [](const std::vector<PipeArr>& v, size_t m) {

@@ -31,6 +31,7 @@ enum KnobId : int {
                           //   0: the older pageable-copy path; 2 (tests): any batch above PIPE_FIRST
   KNOB_PIPE_CHUNK,        //   its chunk size (signatures)
   KNOB_PIPE_FIRST,        //   and its first, smaller chunk
+  KNOB_PIPE_STREAMS,      //   compute streams the chunks alternate on (1 default, 2 for A/B)
   KNOB_TEST_SKIP_FLAG,    // tests: k > 0 makes the first workgroup's producer of hand-off flag k - 1
                           //   skip publishing it (handoff.cuh), so its consumers time out
   KNOB_COUNT

@@ -29,8 +29,8 @@ class knobs:
             self.engine.set_knob(k, v)
 
 
-def _pipe(first, chunk):
-    return {"EGES_HOST_PIPE": 2, "EGES_PIPE_FIRST": first, "EGES_PIPE_CHUNK": chunk}
+def _pipe(first, chunk, streams=1):
+    return {"EGES_HOST_PIPE": 2, "EGES_PIPE_FIRST": first, "EGES_PIPE_CHUNK": chunk, "EGES_PIPE_STREAMS": streams}
 
 
 def _tile(a, n):
@@ -38,12 +38,13 @@ def _tile(a, n):
     return np.ascontiguousarray(np.concatenate([a] * rep)[:n])
 
 
+@pytest.mark.parametrize("streams", [1, 2])
 @pytest.mark.parametrize("sched", SCHEDULES)
-def test_pipe_ecrecover_golden_tiled(engine, sched):
+def test_pipe_ecrecover_golden_tiled(engine, sched, streams):
     g = load_golden("recover.npz")
     n = 30011
     msg, sig = _tile(g["msg"], n), _tile(g["sig"], n)
-    with knobs(engine, _pipe(*sched)):
+    with knobs(engine, _pipe(*sched, streams)):
         pub, addr, st = engine.ecrecover_batch(msg, sig)
     assert np.array_equal(st, _tile(g["status"], n))
     assert np.array_equal(pub, _tile(g["pub"], n))

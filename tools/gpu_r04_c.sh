@@ -1,33 +1,33 @@
-# Round-4 pass c: scalar-ALU divsteps in assembly. Row-form field/inverse tests, the inversion
-# latency A/B (asm vs compiled C, same box, alternating), latency-kernel and exceptional tests,
-# then C3 native block call and single-call latency A/B (tools/abbase = the C divsteps build).
+# Round-4 pass c: host-buffer pipeline on one compute stream (chunk schedules, old path, 2-stream
+# A/B), the lane-serial kernel by batch and grid generations, then the host-pipe tests and the
+# host-code ASan harness on the GPU.
 set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/r04_c
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_fr.py -x -v -s --timeout 200 --timeout-method thread > $O/pytest_fr.txt 2>&1 || { tail -30 $O/pytest_fr.txt; exit 1; }
-grep -E "inversion|passed|failed" $O/pytest_fr.txt
-timeout -k 10 120 python tools/ab_inv.py 3 > $O/ab_inv.json 2>&1
-cat $O/ab_inv.json
-timeout -k 10 600 python -u -m pytest tests/test_gpu_lat.py tests/test_gpu_exceptional.py tests/test_gpu_parity.py tests/test_gpu_concurrency.py -x -v --timeout 300 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
-tail -1 $O/pytest.txt
-for i in 1 2 3; do
-  timeout -k 10 120 tools/block_bench 1000 300 > $O/bb_asm_$i.json 2>&1
-  LD_LIBRARY_PATH=$PWD/tools/abbase timeout -k 10 120 tools/block_bench 1000 300 > $O/bb_c_$i.json 2>&1
-  cat $O/bb_asm_$i.json $O/bb_c_$i.json
-done
+timeout -k 10 300 python -u -m pytest tests/test_gpu_host_pipe.py -x -v --timeout 200 --timeout-method thread > $O/pytest_pipe.txt 2>&1 || { tail -30 $O/pytest_pipe.txt; exit 1; }
+tail -1 $O/pytest_pipe.txt
+c2h() {  # name env...
+  local name=$1; shift
+  env "$@" timeout -k 10 200 python bench.py --config c2host --steps 6 --warmup 2 > $O/c2host_$name.json 2> $O/c2host_$name.err
+  python -c "import json; a=json.load(open('$O/c2host_$name.json')); print('c2host $name', a['value'], a['ms_per_step'], a['config']['correct'])"
+}
 for i in 1 2; do
-  timeout -k 10 120 tools/single_bench 1 300 > $O/single_asm_$i.json 2>&1
-  LD_LIBRARY_PATH=$PWD/tools/abbase timeout -k 10 120 tools/single_bench 1 300 > $O/single_c_$i.json 2>&1
-  cat $O/single_asm_$i.json $O/single_c_$i.json
+  c2h default_$i EGES_HOST_PIPE=1
+  c2h old_$i EGES_HOST_PIPE=0
+  c2h f196_$i EGES_PIPE_FIRST=196608 EGES_PIPE_CHUNK=851968
+  c2h f131_$i EGES_PIPE_FIRST=131072 EGES_PIPE_CHUNK=917504
+  c2h f393_$i EGES_PIPE_FIRST=393216 EGES_PIPE_CHUNK=655360
+  c2h f262x3_$i EGES_PIPE_FIRST=262144 EGES_PIPE_CHUNK=393216
+  c2h two_$i EGES_PIPE_STREAMS=2
 done
-timeout -k 10 120 tools/memcpy_probe > $O/memcpy_probe.txt 2>&1
-cat $O/memcpy_probe.txt
-timeout -k 10 200 python bench.py --config c2host --steps 5 --warmup 2 > $O/c2host.json 2> $O/c2host.err
-cat $O/c2host.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c2host -o run --output-format csv -- python3 bench.py --config c2host --steps 3 --warmup 1 > $O/prof_c2host.log 2>&1
-for b in 65536 131072 262144 524288 1048576; do
-  timeout -k 10 120 python bench.py --batch $b --steps 5 --warmup 2 --no-secondary --no-cpu-baseline > $O/c2_b$b.json 2> $O/c2_b$b.err
-  python -c "import json,sys; d=json.load(open('$O/c2_b$b.json')); print($b, d['roofline']['kernel_ms'], d['value'])"
+for gm in 1 2; do
+  for b in 262144 393216 524288 786432 1048576; do
+    EGES_GRID_MULT=$gm timeout -k 10 120 python bench.py --batch $b --steps 5 --warmup 2 --no-secondary --no-cpu-baseline > $O/gm${gm}_b$b.json 2> $O/gm${gm}_b$b.err
+    python -c "import json; d=json.load(open('$O/gm${gm}_b$b.json')); print('grid_mult $gm batch $b kernel_ms', d['roofline']['kernel_ms'], d['config']['correct'])"
+  done
 done
+ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 timeout -k 10 300 tools/asan/sanitize_host 3000 > $O/sanitize_gpu.log 2>&1
+tail -1 $O/sanitize_gpu.log

@@ -382,8 +382,11 @@ int main(int argc, char** argv) {
     batch_recover(20011);
     signed_block(5003);
     eges_test_set_knob("EGES_HOST_PIPE", 1);
-    eges_test_set_knob("EGES_PIPE_FIRST", 131072);
-    eges_test_set_knob("EGES_PIPE_CHUNK", 262144);
+    eges_test_set_knob("EGES_PIPE_STREAMS", 2);
+    batch_recover(20011);
+    eges_test_set_knob("EGES_PIPE_STREAMS", 1);
+    eges_test_set_knob("EGES_PIPE_FIRST", 262144);
+    eges_test_set_knob("EGES_PIPE_CHUNK", 786432);
     block_structure(2000);
     eges_shutdown();
   }
