@@ -788,9 +788,13 @@ def run_host_throughput(c):
     torch.cuda.synchronize()
     msg_h, sig_h, exp_h = msg.cpu().numpy(), sig.cpu().numpy(), exp_addr.cpu().numpy()
     out = {}
+    # the caller's output arrays are reused across calls (a buffer pool): fresh arrays cost their
+    # first-touch page faults inside the call, reported beside the line as fresh_outputs_sigs_per_s
+    oa, os_ = np.zeros((B, 20), np.uint8), np.zeros(B, np.uint8)
 
-    def step():
-        out["r"] = c.eges.ecrecover_batch(msg_h, sig_h, want_pub=False)
+    def step(fresh=False):
+        out["r"] = c.eges.ecrecover_batch(msg_h, sig_h, want_pub=False, out_addr=None if fresh else oa,
+                                          out_status=None if fresh else os_)
 
     for _ in range(a.warmup):
         step()
@@ -800,13 +804,21 @@ def run_host_throughput(c):
     elapsed = time.perf_counter() - t0
     _, addr, st = out["r"]
     ok = bool((st == 0).all()) and np.array_equal(addr, exp_h)
+    tf = time.perf_counter()
+    for _ in range(3):
+        step(fresh=True)
+    fresh = B * 3 / (time.perf_counter() - tf)
+    _, addr, st = out["r"]
+    ok = ok and bool((st == 0).all()) and np.array_equal(addr, exp_h)
     line = {"metric": "secp256k1 ecrecover+address/sec, host buffers (PCIe-inclusive)", "value": round(B * a.steps / elapsed, 1),
             "unit": "sigs/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed * 1e3 / a.steps, 3), "higher_is_better": True, "dtype": "u32",
             "data": "synthetic",
             "config": {"workload": "configs[1] batch through eges_ecrecover_batch: pageable host msg/sig in, host "
-                                   "addresses + statuses out (H2D + prep + recover + D2H, synchronous call)",
-                       "batch": B, "correct": ok}}
+                                   "addresses + statuses out (H2D + prep + recover + D2H, synchronous call) into "
+                                   "reused output arrays",
+                       "batch": B, "correct": ok},
+            "fresh_outputs_sigs_per_s": round(fresh, 1)}
     c.finish(line, ok)
 
 

@@ -63,16 +63,28 @@ def diag_counters(device=0, reset=False):
     return {n: int(out[i]) for i, n in enumerate(_lib.DIAG_NAMES)}
 
 
-def ecrecover_batch(msg, sig, want_pub=True, want_addr=True):
-    """crypto.Ecrecover over n items: msg (n,32), sig (n,65) -> (pub (n,65)|None, addr (n,20)|None, status (n,))."""
+def _out(buf, n, w, name):
+    """a caller-supplied output array (reused across calls, e.g. a buffer pool) or a fresh one"""
+    shape = (n, w) if w else (n,)
+    if buf is None:
+        return np.zeros(shape, np.uint8)
+    if not (isinstance(buf, np.ndarray) and buf.dtype == np.uint8 and buf.shape == shape and buf.flags.c_contiguous
+            and buf.flags.writeable):
+        raise ValueError(f"{name}: expected a writable C-contiguous uint8 array of shape {shape}")
+    return buf
+
+
+def ecrecover_batch(msg, sig, want_pub=True, want_addr=True, out_pub=None, out_addr=None, out_status=None):
+    """crypto.Ecrecover over n items: msg (n,32), sig (n,65) -> (pub (n,65)|None, addr (n,20)|None, status (n,)).
+    out_* optionally supply the output arrays (written in place and returned)."""
     msg = _u8(msg, (32,), "msg")
     sig = _u8(sig, (65,), "sig")
     n = msg.shape[0]
     if sig.shape[0] != n:
         raise ValueError("msg/sig length mismatch")
-    pub = np.zeros((n, 65), np.uint8) if want_pub else None
-    addr = np.zeros((n, 20), np.uint8) if want_addr else None
-    status = np.zeros(n, np.uint8)
+    pub = _out(out_pub, n, 65, "out_pub") if want_pub else None
+    addr = _out(out_addr, n, 20, "out_addr") if want_addr else None
+    status = _out(out_status, n, 0, "out_status")
     if n:
         check(lib.eges_ecrecover_batch(_p(msg), _p(sig), n, _p(pub), _p(addr), _p(status)))
     return pub, addr, status
