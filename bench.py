@@ -27,8 +27,9 @@ Metric (BASELINE.json): "secp256k1 ecrecover+address/sec at 1/8 MI355X; % of INT
   eges_ecrecover_batch — the PCIe-inclusive rate a Go caller sees (never `value` of the c2 line).
 
 The c2 line also carries a `secondary` object (N = 1, outside the timed region): C3's block
-latency (median / p99 over 50 blocks), C1's 10k transfers from wire bytes, and C5 over the same
-1M batch (ecrecover and sender statuses, mismatch counts).
+latency (median / p99 over 50 blocks, from sender rows and from wire bytes), C1's 10k transfers
+from wire bytes, C5 over the same 1M batch (ecrecover and sender statuses, mismatch counts), the
+same 1M batch as host buffers (c2_host) and the single-item seam under concurrent callers.
 
 Multi-GPU: `--gpus N` without a launcher starts `torch.distributed.run --nproc-per-node N` on this
 script as a child process (no exec) and exits with its code; under a launcher WORLD_SIZE must
@@ -410,6 +411,9 @@ def run_throughput(c, strong):
         sec["c3_block_wire"] = measure_block(c, 1000, raw_mode=True, warmup=3, iters=50, cpu=False)
         sec["c1_transfers"] = measure_c1(c, 10000, warmup=3, iters=20, cpu=False)
         sec["c5_adversarial"] = measure_c5(c, B, msg, sig, exp_addr, steps=1, warmup=1)
+        # the same 1M batch handed over as host buffers
+        sec["c2_host"] = measure_host(c, msg.cpu().numpy(), sig.cpu().numpy(), exp_addr.cpu().numpy(), steps=6,
+                                      warmup=2)
         # as many synchronous callers as the reference baseline's threads (the box's granted CPUs)
         ref = cpu if cpu and cpu.get("kind") == "reference" else None
         sec["single"] = measure_single(ref["cores"] if ref else 16, 2000, ref["value"] if ref else None)
@@ -585,12 +589,22 @@ def measure_c1(c, n, warmup, iters, cpu=True):
     torch.cuda.synchronize()
     sig_h, exp_h = sig_d.cpu().numpy(), exp_d.cpu().numpy()
     packed = c.eges.pack_raw(txs.c1_raw(0, sig_h))
+    # the C-ABI call itself on preallocated host buffers (what a cgo caller pays), as in
+    # measure_block: every timed call's outputs are checked after it
+    from eges_amd._lib import check, lib
+    P = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+    addr = np.zeros((n, 20), np.uint8)
+    st = np.zeros(n, np.uint8)
+    args = (P(packed[0]), P(packed[1]), n, SIGNER_EIP155, txs.GEEC_CHAIN_ID, P(addr), P(st), None)
     lat = []
     ok = True
     for i in range(warmup + iters):
+        addr.fill(0)
+        st.fill(0xEE)
         t0 = time.perf_counter()
-        addr, st, _ = c.eges.sender_raw_batch(packed, SIGNER_EIP155, txs.GEEC_CHAIN_ID)
+        rc = lib.eges_sender_raw_batch(*args)
         dt = time.perf_counter() - t0
+        check(rc)
         if i >= warmup:
             lat.append(dt)
         ok = ok and bool((st == 0).all()) and np.array_equal(addr, exp_h)
@@ -606,7 +620,8 @@ def measure_c1(c, n, warmup, iters, cpu=True):
     ok = ok and bool((sd == 0).all().item()) and np.array_equal(ad.cpu().numpy(), exp_h)
     out = {"txs_per_s": round(n / med, 1), "median_ms": round(med * 1e3, 3),
            "p99_ms": round(float(np.percentile(np.array(lat) * 1e3, 99)), 3), "txs": n, "batches": iters,
-           "correct": ok,
+           "correct": ok, "path": "wire-format txdata RLP through eges_sender_raw_batch; timed around the C-ABI "
+                                   "call (ctypes, preallocated outputs)",
            "roofline": dict(roofline(n / (kms / 1e3), W_RECOVER, n, kms, kernel="eges::recover_bkt_kernel"),
                             note="W excludes the fused RLP decode and signing-hash Keccak (conservative)")}
     if cpu:
@@ -780,26 +795,26 @@ def run_verify(c):
 
 
 # ------------------------------------------------------------------ c2host: host buffers
-def run_host_throughput(c):
+def measure_host(c, msg_h, sig_h, exp_h, steps, warmup):
+    """configs[1]'s batch as host (pageable) buffers through eges_ecrecover_batch (the cgo path of
+    signature_cgo.go:31): H2D + prep + recover + D2H in one synchronous call. The caller's output
+    arrays are reused across calls (a buffer pool); fresh arrays cost their first-touch page faults
+    inside the call, reported beside it as fresh_outputs_sigs_per_s."""
     import numpy as np
-    torch, a = c.torch, c.args
-    B = a.batch or (1 << 20)
-    msg, sig, exp_addr = c.eges.synth_sign_dev(0, B, c.local)
-    torch.cuda.synchronize()
-    msg_h, sig_h, exp_h = msg.cpu().numpy(), sig.cpu().numpy(), exp_addr.cpu().numpy()
+    B = msg_h.shape[0]
     out = {}
-    # the caller's output arrays are reused across calls (a buffer pool): fresh arrays cost their
-    # first-touch page faults inside the call, reported beside the line as fresh_outputs_sigs_per_s
     oa, os_ = np.zeros((B, 20), np.uint8), np.zeros(B, np.uint8)
 
     def step(fresh=False):
         out["r"] = c.eges.ecrecover_batch(msg_h, sig_h, want_pub=False, out_addr=None if fresh else oa,
                                           out_status=None if fresh else os_)
 
-    for _ in range(a.warmup):
+    for _ in range(warmup):
         step()
+    os_.fill(0xFF)
+    oa.fill(0)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for _ in range(steps):
         step()
     elapsed = time.perf_counter() - t0
     _, addr, st = out["r"]
@@ -810,15 +825,26 @@ def run_host_throughput(c):
     fresh = B * 3 / (time.perf_counter() - tf)
     _, addr, st = out["r"]
     ok = ok and bool((st == 0).all()) and np.array_equal(addr, exp_h)
-    line = {"metric": "secp256k1 ecrecover+address/sec, host buffers (PCIe-inclusive)", "value": round(B * a.steps / elapsed, 1),
+    return {"batch": B, "sigs_per_s": round(B * steps / elapsed, 1), "ms_per_call": round(elapsed * 1e3 / steps, 3),
+            "steps": steps, "fresh_outputs_sigs_per_s": round(fresh, 1), "correct": ok}
+
+
+def run_host_throughput(c):
+    torch, a = c.torch, c.args
+    B = a.batch or (1 << 20)
+    msg, sig, exp_addr = c.eges.synth_sign_dev(0, B, c.local)
+    torch.cuda.synchronize()
+    r = measure_host(c, msg.cpu().numpy(), sig.cpu().numpy(), exp_addr.cpu().numpy(), a.steps, a.warmup)
+    ok = r["correct"]
+    line = {"metric": "secp256k1 ecrecover+address/sec, host buffers (PCIe-inclusive)", "value": r["sigs_per_s"],
             "unit": "sigs/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(elapsed * 1e3 / a.steps, 3), "higher_is_better": True, "dtype": "u32",
+            "ms_per_step": r["ms_per_call"], "higher_is_better": True, "dtype": "u32",
             "data": "synthetic",
             "config": {"workload": "configs[1] batch through eges_ecrecover_batch: pageable host msg/sig in, host "
                                    "addresses + statuses out (H2D + prep + recover + D2H, synchronous call) into "
                                    "reused output arrays",
                        "batch": B, "correct": ok},
-            "fresh_outputs_sigs_per_s": round(fresh, 1)}
+            "fresh_outputs_sigs_per_s": r["fresh_outputs_sigs_per_s"]}
     c.finish(line, ok)
 
 

@@ -153,6 +153,8 @@ const KnobDef KNOB_DEFS[KNOB_COUNT] = {
     {"EGES_PIPE_CHUNK", 786432},
     {"EGES_PIPE_FIRST", 262144},
     {"EGES_PIPE_STREAMS", 1},
+    {"EGES_LAT_TRI_MAX", 0},
+    {"EGES_HOST_PARTS", EGES_PIPE_PARTS},
     {"EGES_TEST_SKIP_FLAG", 0},
 };
 std::atomic<long long> g_knob[KNOB_COUNT];
@@ -178,10 +180,11 @@ int knob_index(const char* name) {
 // windowed form's shared workspace).
 struct Route {
   size_t lat_max = 0, mid_max = 0;
-  uint32_t wide_max = 0;
+  uint32_t wide_max = 0, tri_max = 0;
   long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, host_pipe = 1;
   size_t pipe_chunk = 786432, pipe_first = 262144;
   long long pipe_streams = 1;
+  size_t host_parts = EGES_PIPE_PARTS;
   uint32_t force_redo = 0, skip_flag = 0;
   static Route now() {
     Route r;
@@ -196,6 +199,8 @@ struct Route {
     r.pipe_chunk = (size_t)std::max<long long>(64, knob(KNOB_PIPE_CHUNK));
     r.pipe_first = (size_t)std::max<long long>(64, knob(KNOB_PIPE_FIRST));
     r.pipe_streams = knob(KNOB_PIPE_STREAMS);
+    r.tri_max = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_LAT_TRI_MAX), 1u << 30));
+    r.host_parts = (size_t)std::max<long long>(2, std::min<long long>(knob(KNOB_HOST_PARTS), 64));
     r.force_redo = knob(KNOB_FORCE_REDO) != 0 ? 1u : 0u;
     r.skip_flag = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TEST_SKIP_FLAG), 64));
     return r;
@@ -453,8 +458,12 @@ void bind_sender_rows(RecoverParams& p, const uint8_t* h, const uint8_t* r, cons
 
 hipError_t launch_recover_pass(Dev& d, const Route& rt, const RecoverParams& p0, hipStream_t st) {
   RecoverParams p = with_diag(d, p0, rt);
-  // the split form (four waves per signature) while the batch leaves SIMDs idle
-  p.wide = p.n <= rt.wide_max ? 1u : 0u;
+  // the split form (four waves per signature) while the batch leaves SIMDs idle, then the
+  // three-wave form, then the narrow form (k_recover_lat.hip FORM_*)
+  // (the three-wave form only while its workgroups and the root helpers fit one generation at
+  // its occupancy of 3 waves per SIMD)
+  const bool tri = p.n <= rt.tri_max && 3 * (size_t)p.n + 2 * ((p.n + 127) / 128) <= (size_t)d.cus * 4 * 3;
+  p.wide = p.n <= rt.wide_max ? 1u : tri ? 2u : 0u;
   const bool mid = use_mid(d, rt, p.n);
   if (p.wire_raw && !(mid ? mid_bucket(d, rt, p.n) : p.n <= rt.lat_max)) return hipErrorInvalidValue;  // wire_fused() decides
   if (p.snd_r && !(mid || p.n <= rt.lat_max)) return hipErrorInvalidValue;  // sender_fused() decides
@@ -712,7 +721,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   DevGuard g(d.id);
   // a shard big enough to pipeline runs as >= 2 chunks (each still a full resident grid)
   size_t c = std::min(CHUNK, cnt);
-  if (cnt >= 2 * PIPE_MIN && c > cnt / 2) c = align_up((cnt + EGES_PIPE_PARTS - 1) / EGES_PIPE_PARTS, 64);
+  if (cnt >= 2 * PIPE_MIN && c > cnt / 2) c = std::min(CHUNK, align_up((cnt + rt.host_parts - 1) / rt.host_parts, 64));
   size_t worst = 0;  // region size: SENDER_RAW depends on the bytes of each chunk
   for (size_t base = off; base < off + cnt; base += c) worst = std::max(worst, region_for(j, base, std::min(c, off + cnt - base)).total);
   const int nreg = cnt > c ? 2 : 1;

@@ -20,9 +20,11 @@
 //                                            split form: wave 1
 //   back to E: (X, Y, Z) -> (X, Y, Z y); + u1 G; Z^-1 (limb-parallel safegcd), affine,
 //   serialize, Keccak address across the wave's lanes (keccak_wave.cuh); lane 0 stores.
-// Forms: narrow (two waves per signature, batches above EGES_LAT_WIDE_MAX) and split (four
-// waves: the doubling chain cut at window SPLIT_W0, its high part on waves 2 / 3 against tables
-// of D = 2^75 R'; batches up to EGES_LAT_WIDE_MAX = 256). DESIGN.md §3.3.
+// Forms: narrow (two waves per signature), split (four waves: the doubling chain cut at window
+// SPLIT_W0, its high part on waves 2 / 3 against tables of D = 2^75 R'; batches up to
+// EGES_LAT_WIDE_MAX = 256) and three-wave (the chain cut at TRI_W0, the high part of both GLV
+// halves on wave 2, the roots from the helper workgroups; batches up to EGES_LAT_TRI_MAX).
+// DESIGN.md §3.3.
 #include <atomic>
 #include <cstdlib>
 #include <type_traits>
@@ -55,8 +57,21 @@ static_assert(SPLIT_W0 > 0 && SPLIT_W0 < RWIN, "split point");
 constexpr int HBITS = 4;
 constexpr int HTAB = 1 << (HBITS - 1);
 constexpr int HWIN = (130 - RBITS * SPLIT_W0 + HBITS) / HBITS;
+// Three-wave form: windows [0, TRI_W0) of both halves on wave 0, the rest of both halves on
+// wave 2 against one table of D = 2^(RBITS TRI_W0) R' (and its beta x), so the two chains
+// (table + TRI_W0 windows / RBITS TRI_W0 doublings + D's table + TRI_HWIN windows) are about even.
+#ifndef EGES_TRI_W0
+#define EGES_TRI_W0 20
+#endif
+constexpr int TRI_W0 = EGES_TRI_W0;
+static_assert(TRI_W0 > 0 && TRI_W0 < RWIN, "three-wave split point");
+constexpr int TRI_HWIN = (130 - RBITS * TRI_W0 + HBITS) / HBITS;
+static_assert(TRI_HWIN <= HWIN, "the high digits fit LatLds::hdig");
+// forms of the latency kernels (RecoverParams::wide)
+enum { FORM_NARROW = 0, FORM_SPLIT = 1, FORM_TRI = 2 };
 
-// LDS flags of the split form (set once by their producer wave, polled by the consumers)
+// LDS flags of the split and three-wave forms (set once by their producer wave, polled by the
+// consumers; the three-wave form uses F_DIG, F_G and F_HI)
 enum { F_DIG = 0, F_Y, F_G, F_LHI, F_HI, F_ERR, NFLAGS };
 
 struct LatLds {
@@ -175,26 +190,30 @@ DEV void recode_step(uint32_t m[5], int& carry, bool neg, int8_t& out) {
   for (int i = 0; i < 4; ++i) m[i] = (m[i] >> W) | (m[i + 1] << (32 - W));
   m[4] >>= W;
 }
+template <int W0, int NH>
 DEV void recode_split(const glv_half& h, int8_t* lo, int8_t* hi) {
   uint32_t m[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) m[i] = h.mag[i];
   int carry = 0;
 #pragma unroll 1
-  for (int w = 0; w < SPLIT_W0; ++w) recode_step<RBITS>(m, carry, h.neg, lo[w]);
+  for (int w = 0; w < W0; ++w) recode_step<RBITS>(m, carry, h.neg, lo[w]);
 #pragma unroll 1
-  for (int w = 0; w < HWIN; ++w) recode_step<HBITS>(m, carry, h.neg, hi[w]);
+  for (int w = 0; w < NH; ++w) recode_step<HBITS>(m, carry, h.neg, hi[w]);
 }
 
-// GLV split of u_r into signed 5-bit windows (core.cuh ecmult_core's digits; the split form's
-// high part in 4-bit ones), u_g for the comb
-template <bool SPLIT>
+// GLV split of u_r into signed 5-bit windows (core.cuh ecmult_core's digits; the split and
+// three-wave forms' high parts in 4-bit ones), u_g for the comb
+template <int FORM>
 DEV void recode_r(const sc& u_r, LatLds& S) {
   glv_half h1, h2;
   glv_split(h1, h2, u_r);
-  if (SPLIT) {
-    recode_split(h1, S.rdig[0], S.hdig[0]);
-    recode_split(h2, S.rdig[1], S.hdig[1]);
+  if (FORM == FORM_SPLIT) {
+    recode_split<SPLIT_W0, HWIN>(h1, S.rdig[0], S.hdig[0]);
+    recode_split<SPLIT_W0, HWIN>(h2, S.rdig[1], S.hdig[1]);
+  } else if (FORM == FORM_TRI) {
+    recode_split<TRI_W0, TRI_HWIN>(h1, S.rdig[0], S.hdig[0]);
+    recode_split<TRI_W0, TRI_HWIN>(h2, S.rdig[1], S.hdig[1]);
   } else {
     recode_row<RBITS, RWIN, int8_t>(h1, S.rdig[0]);
     recode_row<RBITS, RWIN, int8_t>(h2, S.rdig[1]);
@@ -622,6 +641,37 @@ DEV void high_wave(LatLds& S, const fr& x, const fr& c, int j, const Diag& dg) {
   put_part(S, 3, A, ainf);
   flag_set(S, F_HI);
 }
+// Three-wave form, wave 1 after its scalar work: u_g G (y comes from the root helpers)
+DEV void helper_tri(LatLds& S, const uint32_t* gcomb, const Diag& dg) {
+  gejr A;
+  bool ainf;
+  gcomb_exact(A, ainf, S, gcomb, dg);
+  put_part(S, 2, A, ainf);
+  flag_set(S, F_G);
+}
+// Three-wave form, wave 2: D = 2^(RBITS TRI_W0) R', D's table and its beta x, the high windows
+// of both GLV halves jointly; the sum is published as the E' point (X, Y, Z zeta_D Z_D) (wave 0
+// joins it on E' and maps the total to E with y once).
+DEV void high_wave_tri(LatLds& S, const fr& x, const fr& c, const Diag& dg) {
+  gejr D;
+  fr_mul2(D.x, D.y, c, x, c, c);  // R' = (c x, c^2)
+  D.z = fr_one();
+#pragma unroll 1
+  for (int k = 0; k < RBITS * TRI_W0; ++k) D = gejq_double(D);  // R' has odd order: never exceptional
+  ger Dp;
+  Dp.x = D.x;
+  Dp.y = D.y;
+  const fr zd = build_table_wave<HTAB>(Dp, S.dtab[0], S.dzr[0], S.dzq[0]);
+  build_btab<HTAB>(S.dtab[0], S.dbtab);
+  const fr scale = fr_mul(zd, D.z);
+  flag_wait(S, F_DIG);
+  gejr A;
+  bool ainf;
+  strauss_win_exact<HBITS, HTAB>(A, ainf, S.dtab[0], S.dbtab, S.hdig[0], S.hdig[1], 3, 0, TRI_HWIN, dg);
+  A.z = fr_mul(A.z, scale);
+  put_part(S, 3, A, ainf);
+  flag_set(S, F_HI);
+}
 
 // Wave 0: u_r * (x, y) + u_g G with y deferred. R' = (c x, c^2) on E', its table, the digits,
 // the R' Strauss sum(s), then back to the true curve: an E' Jacobian point (X, Y, Z) is (X, Y, Z y)
@@ -634,20 +684,39 @@ struct RootSrc {  // narrow recover form: where wave 0 finds R's y (root_fetch)
   uint32_t idx;
   bool odd;
 };
-template <class ST, bool SPLIT>
+template <class ST, int FORM>
 DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& S, ST* st, const Diag& dg,
                          const RootSrc* root = nullptr) {
+  constexpr bool SPLIT = FORM == FORM_SPLIT;
   ger Rp;
   fr_mul2(Rp.x, Rp.y, c, x, c, c);  // (c x, c^2)
   const fr zeta = build_table_wave<PTAB>(Rp, S.tab, S.zr, S.zq);
   build_btab<PTAB>(S.tab, S.btab);
   st->mark(3);
-  if (SPLIT) flag_wait(S, F_DIG);
+  if (FORM != FORM_NARROW) flag_wait(S, F_DIG);
   else __syncthreads();  // digits ready
   st->mark(1);
   gejr A;
   bool ainf;
-  strauss_win_exact<RBITS, PTAB>(A, ainf, S.tab, S.btab, S.rdig[0], S.rdig[1], 3, 0, SPLIT ? SPLIT_W0 : RWIN, dg);
+  strauss_win_exact<RBITS, PTAB>(A, ainf, S.tab, S.btab, S.rdig[0], S.rdig[1], 3, 0,
+                                 SPLIT ? SPLIT_W0 : FORM == FORM_TRI ? TRI_W0 : RWIN, dg);
+  if constexpr (FORM == FORM_TRI) {
+    // the low and high sums joined on E' (the addition formulas do not involve b), then to E
+    // with y (from the root helpers) once, then + u_g G
+    A.z = fr_mul(A.z, zeta);
+    flag_wait(S, F_HI);
+    bool hinf;
+    const gejr Hp = get_part(S, 3, hinf);
+    A = join_parts(A, ainf, Hp, hinf, ainf, dg);
+    root_fetch(*root->prm, root->idx, c, root->odd, S);
+    A.z = fr_mul(A.z, fr{S.ylift[row_lane()]});
+    flag_wait(S, F_G);
+    bool ginf;
+    const gejr Gp = get_part(S, 2, ginf);
+    Q = join_parts(A, ainf, Gp, ginf, qinf, dg);
+    st->mark(4);
+    return;
+  }
   if (SPLIT) flag_wait(S, F_Y);
   else __syncthreads();  // partial sums (and y) ready
   if (root) root_fetch(*root->prm, root->idx, c, root->odd, S);  // (this wave's own LDS words)
@@ -752,13 +821,15 @@ DEV uint32_t hw_place() {
 // square root and the u1 G comb part. SPLIT (small batches, four waves): wave 1 the scalar work,
 // y and u1 G; waves 2 and 3 the high windows of the two GLV halves against their own table of
 // D = 2^75 R'; wave 0 the low windows of both halves, then joins the three partial sums.
-template <class ST, bool SPLIT>
+template <class ST, int FORM>
 DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
+  constexpr bool SPLIT = FORM == FORM_SPLIT;   // four waves, wave 1 computes y
+  constexpr bool FLAGS = FORM != FORM_NARROW;  // LDS flag hand-offs instead of barriers
   __shared__ LatLds S;
   ST st_;
   ST* st = &st_;
   const Diag dg = diag_of(prm);
-  if (!SPLIT && blockIdx.x < prm.n_helpers) {  // narrow form: the lane-serial roots
+  if (!SPLIT && blockIdx.x < prm.n_helpers) {  // narrow / three-wave forms: the lane-serial roots
     root_helper(prm);
     return;
   }
@@ -774,9 +845,9 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
     if (wlen <= LAT_STAGE)
       for (uint32_t j = threadIdx.x; j < wlen; j += blockDim.x) S.stage[j] = prm.wire_raw[wra + j];
   }
-  if (SPLIT && threadIdx.x < NFLAGS) S.flag[threadIdx.x] = 0u;
-  if (SPLIT && threadIdx.x == 0) S.skip = blockIdx.x == prm.test_skip_block ? prm.test_skip_flag : 0u;
-  if (SPLIT || wire) __syncthreads();  // (split form: the only barrier besides; narrow: the stage)
+  if (FLAGS && threadIdx.x < NFLAGS) S.flag[threadIdx.x] = 0u;
+  if (FLAGS && threadIdx.x == 0) S.skip = idx == prm.test_skip_block ? prm.test_skip_flag : 0u;  // (item index)
+  if (FLAGS || wire) __syncthreads();  // (split / three-wave: the only barrier; narrow: the stage)
   // --- parse (every lane reads the same record; wire form: every lane decodes the same item)
   LatParse q;
   Payload m;
@@ -813,14 +884,14 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
     const sc u2 = sc_select(ok, sc_mul(rinv, Sv), sc_one());
     if (wire) {
       // the R digits first (wave 0 is waiting for them), then the signing hash for z and u1
-      recode_r<SPLIT>(u2, S);
-      if (SPLIT) flag_set(S, F_DIG);
+      recode_r<FORM>(u2, S);
+      if (FLAGS) flag_set(S, F_DIG);
       else __syncthreads();  // digits ready (and the table)
       uint8_t* hs = prm.wire_sighash ? prm.wire_sighash + (size_t)idx * 32 : nullptr;
       recode_g(sc_neg(sc_mul(rinv, wire_sighash_wave(m, decoded, hs))), S);
     } else {
-      recode_r<SPLIT>(u2, S);  // the R digits first: wave 0 is waiting for them
-      if (SPLIT) flag_set(S, F_DIG);
+      recode_r<FORM>(u2, S);  // the R digits first: wave 0 is waiting for them
+      if (FLAGS) flag_set(S, F_DIG);
       else __syncthreads();  // digits ready (and the table)
       recode_g(sc_neg(sc_mul(rinv, Z)), S);  // u1 = -z / r, for this wave's comb
     }
@@ -829,11 +900,17 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
       S.w1t[1] = __builtin_amdgcn_s_memtime() - t1;
     }
     if (SPLIT) helper_split(S, gcomb, true, c, odd, fr_zero(), dg);
-    else helper_wave(S, gcomb, false, c, odd, fr_zero(), dg);  // y: the helper workgroups (root_fetch)
+    else if (FORM == FORM_TRI) helper_tri(S, gcomb, dg);  // y: the helper workgroups (root_fetch)
+    else helper_wave(S, gcomb, false, c, odd, fr_zero(), dg);
     return;
   }
   if (SPLIT && (wv == 2 || wv == 3)) {
     high_wave(S, x, c, (int)wv - 2, dg);
+    return;
+  }
+  if (FORM == FORM_TRI && wv == 2) {
+    if (idx == 0) diag_bump(dg, EGES_DIAG_LAT_TRI);  // (once per launch: tests see the form ran)
+    high_wave_tri(S, x, c, dg);
     return;
   }
   st->mark(0);
@@ -841,8 +918,8 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   gejr Q;
   bool qinf;
   const RootSrc root{&prm, idx, odd};
-  ecmult_deferred<ST, SPLIT>(Q, qinf, x, c, S, st, dg, SPLIT ? nullptr : &root);
-  const bool fault = SPLIT && ho_failed(&S.flag[F_ERR], dg);  // after wave 0's last wait (F_HI)
+  ecmult_deferred<ST, FORM>(Q, qinf, x, c, S, st, dg, SPLIT ? nullptr : &root);
+  const bool fault = FLAGS && ho_failed(&S.flag[F_ERR], dg);  // after wave 0's last wait
   ok = ok && S.yok != 0 && !qinf && !fault;  // ge_set_xo_var failure, main_impl.h:120
   // --- affine, serialize, address
   const fr zq = fr_select(ok, Q.z, fr_one());
@@ -954,7 +1031,7 @@ DEV void verify_lat_body(const VerifyParams& prm) {
   if (wv == 1) {
     const sc sinv = sc_inv_row_var(sc_select(sig_ok, Sv, sc_one()));
     const sc u2 = sc_select(sig_ok, sc_mul(sinv, R), sc_one());
-    recode_r<SPLIT>(u2, S);  // the key's digits first: wave 0 is waiting for them
+    recode_r<SPLIT ? FORM_SPLIT : FORM_NARROW>(u2, S);  // the key's digits first: wave 0 is waiting for them
     if (SPLIT) flag_set(S, F_DIG);
     else __syncthreads();  // digits ready (and the table)
     recode_g(sc_mul(sinv, Z), S);  // u1 = z / s
@@ -970,7 +1047,7 @@ DEV void verify_lat_body(const VerifyParams& prm) {
   const bool on = fr_equal(c, fr_sqr(Y));  // 65-byte keys: on the curve
   gejr Q;
   bool qinf;
-  ecmult_deferred<NoStamp, SPLIT>(Q, qinf, x, c, S, &st_, dg);
+  ecmult_deferred<NoStamp, SPLIT ? FORM_SPLIT : FORM_NARROW>(Q, qinf, x, c, S, &st_, dg);
   const bool fault = SPLIT && ho_failed(&S.flag[F_ERR], dg);  // after wave 0's last wait (F_HI)
   const bool pk_ok = c33 ? (x_ok && S.yok != 0) : (c65 && x_ok && y_ok && !hybrid_bad && on);
   bool ok = sig_ok && pk_ok && !qinf;
@@ -1003,19 +1080,24 @@ hipError_t launch_verify_lat(const VerifyParams& p, bool wide, hipStream_t st) {
   return hipGetLastError();
 }
 
+constexpr int LAT_WG_TRI = 192;  // three-wave form
 __global__ void __launch_bounds__(LAT_WG) recover_lat_kernel(RecoverParams prm) {
-  recover_lat_body<NoStamp, false>(prm, nullptr);
+  recover_lat_body<NoStamp, FORM_NARROW>(prm, nullptr);
 }
 __global__ void __launch_bounds__(LAT_WG_SPLIT) recover_lat_split_kernel(RecoverParams prm) {
-  recover_lat_body<NoStamp, true>(prm, nullptr);
+  recover_lat_body<NoStamp, FORM_SPLIT>(prm, nullptr);
+}
+__global__ void __launch_bounds__(LAT_WG_TRI) recover_lat_tri_kernel(RecoverParams prm) {
+  recover_lat_body<NoStamp, FORM_TRI>(prm, nullptr);
 }
 
-// the narrow form's launch: ceil(n / 128) root-helper workgroups first (dispatched before the
-// signatures' workgroups), tagged with a per-launch epoch so stale slot-row words never match
+// the narrow and three-wave forms' launch: ceil(n / 128) root-helper workgroups first (dispatched
+// before the signatures' workgroups), tagged with a per-launch epoch so stale slot-row words never
+// match
 static std::atomic<uint32_t> g_root_epoch{0};
 static RecoverParams with_helpers(const RecoverParams& p0) {
   RecoverParams p = p0;
-  p.n_helpers = p.wide ? 0u : (p.n + ROOT_WG - 1) / ROOT_WG;
+  p.n_helpers = p.wide == FORM_SPLIT ? 0u : (p.n + ROOT_WG - 1) / ROOT_WG;
   // tests only: no helper workgroups, so every signature wave takes root_fetch's own-root path
   if (knob(KNOB_ROOT_HELPERS) == 0) p.n_helpers = 0;
   p.epoch = g_root_epoch.fetch_add(1) + 1u;
@@ -1024,22 +1106,30 @@ static RecoverParams with_helpers(const RecoverParams& p0) {
 hipError_t launch_recover_lat(const RecoverParams& p0, hipStream_t st) {
   if (p0.n == 0) return hipSuccess;
   const RecoverParams p = with_helpers(p0);
-  if (p.wide) hipLaunchKernelGGL(recover_lat_split_kernel, dim3(p.n), dim3(LAT_WG_SPLIT), 0, st, p);
+  if (p.wide == FORM_SPLIT) hipLaunchKernelGGL(recover_lat_split_kernel, dim3(p.n), dim3(LAT_WG_SPLIT), 0, st, p);
+  else if (p.wide == FORM_TRI)
+    hipLaunchKernelGGL(recover_lat_tri_kernel, dim3(p.n_helpers + p.n), dim3(LAT_WG_TRI), 0, st, p);
   else hipLaunchKernelGGL(recover_lat_kernel, dim3(p.n_helpers + p.n), dim3(LAT_WG), 0, st, p);
   return hipGetLastError();
 }
 
 #ifdef EGES_PHASE_STAMPS
 __global__ void __launch_bounds__(LAT_WG) recover_lat_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
-  recover_lat_body<Stamper, false>(prm, stamps);
+  recover_lat_body<Stamper, FORM_NARROW>(prm, stamps);
 }
 __global__ void __launch_bounds__(LAT_WG_SPLIT) recover_lat_split_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
-  recover_lat_body<Stamper, true>(prm, stamps);
+  recover_lat_body<Stamper, FORM_SPLIT>(prm, stamps);
+}
+__global__ void __launch_bounds__(LAT_WG_TRI) recover_lat_tri_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
+  recover_lat_body<Stamper, FORM_TRI>(prm, stamps);
 }
 hipError_t launch_recover_lat_stamped(const RecoverParams& p0, hipStream_t st, uint64_t* stamps) {
   if (p0.n == 0) return hipSuccess;
   const RecoverParams p = with_helpers(p0);
-  if (p.wide) hipLaunchKernelGGL(recover_lat_split_kernel_stamped, dim3(p.n), dim3(LAT_WG_SPLIT), 0, st, p, stamps);
+  if (p.wide == FORM_SPLIT)
+    hipLaunchKernelGGL(recover_lat_split_kernel_stamped, dim3(p.n), dim3(LAT_WG_SPLIT), 0, st, p, stamps);
+  else if (p.wide == FORM_TRI)
+    hipLaunchKernelGGL(recover_lat_tri_kernel_stamped, dim3(p.n_helpers + p.n), dim3(LAT_WG_TRI), 0, st, p, stamps);
   else hipLaunchKernelGGL(recover_lat_kernel_stamped, dim3(p.n_helpers + p.n), dim3(LAT_WG), 0, st, p, stamps);
   return hipGetLastError();
 }

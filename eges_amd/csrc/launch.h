@@ -38,7 +38,8 @@ struct RecoverParams {
   // (prep_ecrecover_kernel fused away for small ecrecover calls)
   const uint8_t* raw_msg = nullptr;
   const uint8_t* raw_sig = nullptr;
-  // latency kernel only: the split form (four waves per signature, k_recover_lat.hip)
+  // latency kernel only: 0 the narrow form, 1 the split form (four waves per signature),
+  // 2 the three-wave form (k_recover_lat.hip FORM_*)
   uint32_t wide = 0;
   // latency kernel, narrow form: leading workgroups that compute R's y lane-serially (one lane
   // per signature) into the slot rows, tagged with this launch's epoch (set by the launcher)

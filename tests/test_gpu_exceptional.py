@@ -29,6 +29,8 @@ FORMS = {  # knob settings per form (recovery / verification)
     "lane_serial": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 0},
     "narrow": {"EGES_LAT_MAX": LAT_ALL, "EGES_LAT_WIDE_MAX": 0},
     "split": {"EGES_LAT_MAX": LAT_ALL, "EGES_LAT_WIDE_MAX": LAT_ALL},
+    # (recovery batches under the three-wave form's occupancy bound; verification runs narrow)
+    "tri": {"EGES_LAT_MAX": LAT_ALL, "EGES_LAT_WIDE_MAX": 0, "EGES_LAT_TRI_MAX": LAT_ALL},
     "mid": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": LAT_ALL, "EGES_MID_FORM": 0},
     "mid_bucket": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": LAT_ALL, "EGES_MID_FORM": 2},
 }
