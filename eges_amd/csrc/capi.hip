@@ -154,6 +154,7 @@ const KnobDef KNOB_DEFS[KNOB_COUNT] = {
     {"EGES_PIPE_FIRST", 262144},
     {"EGES_PIPE_STREAMS", 1},
     {"EGES_LAT_TRI_MAX", 0},
+    {"EGES_PIPE_SEG", 8 << 20},
     {"EGES_HOST_PARTS", EGES_PIPE_PARTS},
     {"EGES_TEST_SKIP_FLAG", 0},
 };
@@ -184,7 +185,7 @@ struct Route {
   long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, host_pipe = 1;
   size_t pipe_chunk = 786432, pipe_first = 262144;
   long long pipe_streams = 1;
-  size_t host_parts = EGES_PIPE_PARTS;
+  size_t host_parts = EGES_PIPE_PARTS, pipe_seg = size_t(8) << 20;
   uint32_t force_redo = 0, skip_flag = 0;
   static Route now() {
     Route r;
@@ -200,6 +201,7 @@ struct Route {
     r.pipe_first = (size_t)std::max<long long>(64, knob(KNOB_PIPE_FIRST));
     r.pipe_streams = knob(KNOB_PIPE_STREAMS);
     r.tri_max = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_LAT_TRI_MAX), 1u << 30));
+    r.pipe_seg = (size_t)std::max<long long>(1 << 20, knob(KNOB_PIPE_SEG));
     r.host_parts = (size_t)std::max<long long>(2, std::min<long long>(knob(KNOB_HOST_PARTS), 64));
     r.force_redo = knob(KNOB_FORCE_REDO) != 0 ? 1u : 0u;
     r.skip_flag = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TEST_SKIP_FLAG), 64));
@@ -1003,6 +1005,65 @@ class CopyPool {
     static CopyPool* p = new CopyPool(4);  // never destroyed: detached workers live to process exit
     return *p;
   }
+  // The tasks' bytes in segments of about seg bytes (whole pieces, never across tasks): the workers
+  // copy, and the calling thread runs on_seg(task, offset, bytes) for each segment as soon as its
+  // pieces are done, in order (e.g. the segment's DMA, which then overlaps the next copies).
+  template <class F>
+  void run_segments(const std::vector<Task>& tasks, size_t seg, F&& on_seg) {
+    struct Seg {
+      size_t task, off, n, p0, np;
+    };
+    std::vector<Task> pieces;
+    std::vector<Seg> segs;
+    const size_t per = std::max<size_t>(1, seg / PIECE);
+    for (size_t t = 0; t < tasks.size(); ++t)
+      for (size_t o = 0; o < tasks[t].n;) {
+        Seg s{t, o, 0, pieces.size(), 0};
+        for (size_t k = 0; k < per && o < tasks[t].n; ++k, o += PIECE) {
+          const size_t n = std::min(PIECE, tasks[t].n - o);
+          pieces.push_back({tasks[t].dst + o, tasks[t].src + o, n});
+          s.n += n;
+          ++s.np;
+        }
+        segs.push_back(s);
+      }
+    if (pieces.empty()) return;
+    std::lock_guard<std::mutex> one(run_mu_);
+    std::atomic<size_t> next{0};
+    std::unique_ptr<std::atomic<uint32_t>[]> done(new std::atomic<uint32_t>[pieces.size()]);
+    for (size_t k = 0; k < pieces.size(); ++k) done[k].store(0, std::memory_order_relaxed);
+    auto work = [&] {
+      for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
+        std::memcpy(pieces[k].dst, pieces[k].src, pieces[k].n);
+        done[k].store(1, std::memory_order_release);
+      }
+    };
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = work;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (const Seg& s : segs) {
+      for (size_t k = s.p0; k < s.p0 + s.np; ++k)
+        while (!done[k].load(std::memory_order_acquire)) {
+          // no worker woke yet (or all are busy elsewhere): copy the next piece here
+          const size_t j = next.fetch_add(1);
+          if (j < pieces.size()) {
+            std::memcpy(pieces[j].dst, pieces[j].src, pieces[j].n);
+            done[j].store(1, std::memory_order_release);
+          } else {
+            cpu_relax();
+          }
+        }
+      on_seg(s.task, s.off, s.n);
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = nullptr;
+    }
+    while (active_.load(std::memory_order_acquire) != 0) cpu_relax();
+  }
   void run(const std::vector<Task>& tasks) {
     std::vector<Task> pieces;
     for (const Task& t : tasks)
@@ -1191,14 +1252,18 @@ int run_host_pipe(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t 
     uint8_t* P = d.ring[r];
     const auto io = offs(in, m), oo = offs(out, m);
     // 1. host copy into the pinned slot (free: chunk ci - 2 was copied out in iteration ci - 1)
+    //    and 2. DMA in (after the kernels of chunk ci - 2, same device region), segment by
+    //    segment, so that the copies and the DMA overlap
+    if (ci >= 2) HIPCHK(hipStreamWaitEvent(d.hin, d.ev_k[r], 0));
     {
       std::vector<CopyPool::Task> t;
       for (size_t k = 0; k < in.size(); ++k) t.push_back({P + io[k], in[k].src + base * in[k].w, m * in[k].w});
-      CopyPool::get().run(t);
+      hipError_t e = hipSuccess;
+      CopyPool::get().run_segments(t, rt.pipe_seg, [&](size_t k, size_t o, size_t nb) {
+        if (e == hipSuccess) e = hipMemcpyAsync(B + io[k] + o, P + io[k] + o, nb, hipMemcpyHostToDevice, d.hin);
+      });
+      HIPCHK(e);
     }
-    // 2. DMA in, after the kernels of chunk ci - 2 (same device region) are done
-    if (ci >= 2) HIPCHK(hipStreamWaitEvent(d.hin, d.ev_k[r], 0));
-    HIPCHK(hipMemcpyAsync(B, P, io.back(), hipMemcpyHostToDevice, d.hin));
     HIPCHK(hipEventRecord(d.ev_in[r], d.hin));
     // 3. kernels on this slot's compute stream and workspace
     hipStream_t st = cs[r];

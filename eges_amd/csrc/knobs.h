@@ -33,6 +33,7 @@ enum KnobId : int {
   KNOB_PIPE_FIRST,        //   and its first, smaller chunk
   KNOB_PIPE_STREAMS,      //   compute streams the chunks alternate on (1 default, 2 for A/B)
   KNOB_LAT_TRI_MAX,       // latency batches above LAT_WIDE_MAX up to this size: the three-wave form
+  KNOB_PIPE_SEG,          //   host copy / DMA segment of the pipeline (bytes; 8 MB)
   KNOB_HOST_PARTS,        // host-buffer shards of >= 2 * PIPE_MIN items without the pipeline: chunks (4)
   KNOB_TEST_SKIP_FLAG,    // tests: k > 0 makes the first workgroup's producer of hand-off flag k - 1
                           //   skip publishing it (handoff.cuh), so its consumers time out

@@ -1,5 +1,6 @@
 """The pipelined host-buffer path (capi.hip run_host_pipe: pinned slots filled by host copy
-threads, DMA in / out on their own streams, two compute streams alternating) against the
+threads, DMA in / out on their own streams, the copies and the DMA overlapped segment by
+segment, one or two compute streams) against the
 fixtures and the older path, on ragged multi-chunk batches of every kind it takes: ecrecover,
 types.Sender, the precompile and VerifySignature. EGES_HOST_PIPE = 2 forces the pipeline for a
 batch above EGES_PIPE_FIRST; small chunks also exercise the latency and mid-size kernels inside
@@ -30,7 +31,9 @@ class knobs:
 
 
 def _pipe(first, chunk, streams=1):
-    return {"EGES_HOST_PIPE": 2, "EGES_PIPE_FIRST": first, "EGES_PIPE_CHUNK": chunk, "EGES_PIPE_STREAMS": streams}
+    # 1 MB copy / DMA segments (EGES_PIPE_SEG's minimum): the larger arrays take several
+    return {"EGES_HOST_PIPE": 2, "EGES_PIPE_FIRST": first, "EGES_PIPE_CHUNK": chunk, "EGES_PIPE_STREAMS": streams,
+            "EGES_PIPE_SEG": 1 << 20}
 
 
 def _tile(a, n):
