@@ -29,7 +29,8 @@ namespace {
 using namespace eges;
 
 constexpr size_t CHUNK = PASS_MAX;  // signatures per device pass (bounds scratch memory)
-// host-buffer shards of at least 2 * PIPE_MIN items are split into >= 2 pipelined chunks
+// host-buffer shards of at least 2 * PIPE_MIN items are split into EGES_HOST_PARTS chunks (copies of
+// one chunk overlap the kernels of the previous one; 8 parts at 1M: profiles/r04/c2host_*)
 constexpr size_t PIPE_MIN = size_t(1) << 18;
 // Single-chunk host-buffer calls whose device region fits this many bytes are staged through
 // one pinned host buffer: the caller's inputs are packed on the host, moved by ONE H2D copy,
@@ -37,7 +38,7 @@ constexpr size_t PIPE_MIN = size_t(1) << 18;
 // pageable H2D and two pageable D2H copies, ~0.1 ms).
 constexpr size_t PIN_BYTES = size_t(8) << 20;
 #ifndef EGES_PIPE_PARTS
-#define EGES_PIPE_PARTS 4
+#define EGES_PIPE_PARTS 8
 #endif
 
 thread_local std::string t_err;
@@ -149,11 +150,11 @@ const KnobDef KNOB_DEFS[KNOB_COUNT] = {
     {"EGES_COALESCE_SPIN_US", 2000},
     {"EGES_COALESCE_SPINNERS", 8},
     {"EGES_SENDER_FUSED", 1},
-    {"EGES_HOST_PIPE", 1},
+    {"EGES_HOST_PIPE", 0},
     {"EGES_PIPE_CHUNK", 786432},
     {"EGES_PIPE_FIRST", 262144},
     {"EGES_PIPE_STREAMS", 1},
-    {"EGES_LAT_TRI_MAX", 0},
+    {"EGES_LAT_TRI_MAX", 448},
     {"EGES_PIPE_SEG", 8 << 20},
     {"EGES_HOST_PARTS", EGES_PIPE_PARTS},
     {"EGES_TEST_SKIP_FLAG", 0},
@@ -723,7 +724,8 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   DevGuard g(d.id);
   // a shard big enough to pipeline runs as >= 2 chunks (each still a full resident grid)
   size_t c = std::min(CHUNK, cnt);
-  if (cnt >= 2 * PIPE_MIN && c > cnt / 2) c = std::min(CHUNK, align_up((cnt + rt.host_parts - 1) / rt.host_parts, 64));
+  if (cnt >= 2 * PIPE_MIN && c > cnt / 2)
+    c = std::min(CHUNK, std::max(PIPE_MIN / 2, align_up((cnt + rt.host_parts - 1) / rt.host_parts, 64)));
   size_t worst = 0;  // region size: SENDER_RAW depends on the bytes of each chunk
   for (size_t base = off; base < off + cnt; base += c) worst = std::max(worst, region_for(j, base, std::min(c, off + cnt - base)).total);
   const int nreg = cnt > c ? 2 : 1;

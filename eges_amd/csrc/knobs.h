@@ -27,15 +27,17 @@ enum KnobId : int {
   KNOB_COALESCE_SPINNERS,   //   at most this many callers spin at once
   KNOB_SENDER_FUSED,      // 1: sender rows of latency / mid-size batches are classified inside the
                           //   recover kernel (no prep_sender launch); 0: prep_sender_kernel first
-  KNOB_HOST_PIPE,         // 1: multi-chunk host-buffer calls run the pinned-slot pipeline (run_host_pipe);
-                          //   0: the older pageable-copy path; 2 (tests): any batch above PIPE_FIRST
+  KNOB_HOST_PIPE,         // 1: multi-chunk host-buffer calls run the pinned-slot pipeline (run_host_pipe;
+                          //   measured slower than 0 at 1M); 0 (default): the chunked
+                          //   pageable-copy path; 2 (tests): any batch above PIPE_FIRST
   KNOB_PIPE_CHUNK,        //   its chunk size (signatures)
   KNOB_PIPE_FIRST,        //   and its first, smaller chunk
   KNOB_PIPE_STREAMS,      //   compute streams the chunks alternate on (1 default, 2 for A/B)
   KNOB_LAT_TRI_MAX,       // latency batches above LAT_WIDE_MAX up to this size: the three-wave form
   KNOB_PIPE_SEG,          //   host copy / DMA segment of the pipeline (bytes; 8 MB)
-  KNOB_HOST_PARTS,        // host-buffer shards of >= 2 * PIPE_MIN items without the pipeline: chunks (4)
-  KNOB_TEST_SKIP_FLAG,    // tests: k > 0 makes the first workgroup's producer of hand-off flag k - 1
+  KNOB_HOST_PARTS,        // host-buffer shards of >= 2 * PIPE_MIN items without the pipeline: chunks (8;
+                          //   at least PIPE_MIN / 2 signatures each)
+  KNOB_TEST_SKIP_FLAG,    // tests: k > 0 makes item 0's workgroup's producer of hand-off flag k - 1
                           //   skip publishing it (handoff.cuh), so its consumers time out
   KNOB_COUNT
 };

@@ -27,7 +27,7 @@ pytestmark = pytest.mark.gpu
 LAT_ALL = 1 << 20
 FORMS = {  # knob settings per form (recovery / verification)
     "lane_serial": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 0},
-    "narrow": {"EGES_LAT_MAX": LAT_ALL, "EGES_LAT_WIDE_MAX": 0},
+    "narrow": {"EGES_LAT_MAX": LAT_ALL, "EGES_LAT_WIDE_MAX": 0, "EGES_LAT_TRI_MAX": 0},
     "split": {"EGES_LAT_MAX": LAT_ALL, "EGES_LAT_WIDE_MAX": LAT_ALL},
     # (recovery batches under the three-wave form's occupancy bound; verification runs narrow)
     "tri": {"EGES_LAT_MAX": LAT_ALL, "EGES_LAT_WIDE_MAX": 0, "EGES_LAT_TRI_MAX": LAT_ALL},

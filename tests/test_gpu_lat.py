@@ -40,10 +40,10 @@ class lat_max(env_knob):
         return {"EGES_LAT_MAX": v} if v else {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 0}
 
 
-class wide_max(env_knob):  # latency batches up to this size use the split (4-wave) form
+class wide_max(env_knob):  # latency batches up to this size use the split (4-wave) form; wide_max(0): narrow
     @staticmethod
     def knobs(v):
-        return {"EGES_LAT_WIDE_MAX": v}
+        return {"EGES_LAT_WIDE_MAX": v} if v else {"EGES_LAT_WIDE_MAX": 0, "EGES_LAT_TRI_MAX": 0}
 
 
 class root_helpers(env_knob):  # 0: the narrow form launches no root-helper workgroups

@@ -11,7 +11,8 @@ from conftest import load_golden
 pytestmark = pytest.mark.gpu
 
 FORMS = {
-    "narrow": {"EGES_LAT_MAX": 1 << 20, "EGES_LAT_WIDE_MAX": 0},
+    "narrow": {"EGES_LAT_MAX": 1 << 20, "EGES_LAT_WIDE_MAX": 0, "EGES_LAT_TRI_MAX": 0},
+    "tri": {"EGES_LAT_MAX": 1 << 20, "EGES_LAT_WIDE_MAX": 0, "EGES_LAT_TRI_MAX": 1 << 20},
     "split": {"EGES_LAT_MAX": 1 << 20, "EGES_LAT_WIDE_MAX": 1 << 20},
     "bucket": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2},
     "windowed": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 0},
