@@ -7,6 +7,7 @@
 // doubling, madd-2007-bl mixed addition with the ADD_ZINV variant of group_impl.h:463-517,
 // Meloni co-Z dblu / zaddu for the table, ge_set_xo_var group_impl.h:216-237). Levels:
 //   doubling        2M + 5S in 3 quad steps  {X^2, Y^2, YZ} {B^2, (X+B)^2, E^2} {E (2D - X3)}
+//   two doublings   in 5 quad steps (gejq_double2)
 //   mixed addition  8M + 3S in 5 quad steps  {Z1^2, y2 Z1} {U2 - X1, S2 - Y1} {H^2, Z1 H, R^2}
 //                                            {H I, X1 I} {R2 (V - X3), Y1 J}   (+1 for ZINV)
 //   co-Z addition   4M + 2S in 4 quad steps
@@ -37,6 +38,40 @@ DEV gejr gejq_double(const gejr& a) {
   r.x = fr_normalize_weak(fr_sub<3>(F, fr_mul_small(D, 4)));        // E^2 - 4D
   r.y = fr_mul_sub<1, 3>(E, fr_sub<1>(fr_add(D, D), r.x), C);      // E (4XY^2 - X3) - 8C
   r.z = fr_add(YZ, YZ);                                             // 2 Y Z
+  return r;
+}
+
+// Two doublings in 5 quad levels instead of 6. With U = 3X^3 formed beside Y^2, the doubling's
+// Y3 = 3X^2 (4XY^2 - X3) - 8Y^4 is 3U (4Y^2 - U) - 8Y^4: one product one level after Y^2, so the
+// second doubling's Y3 is ready in the same level as its X3 (gejq_double's E (2D - X3) waits a
+// level for X3). Same values as gejq_double twice. In: X m1, Y <= 2, Z <= 2. Out: X, Y m1, Z m2.
+//   {X^2, Y^2, YZ} {U, 2XY^2, E^2, Y^4} {Y', X'^2} {Y'^2, Y'Z', U', E'^2} {2X'Y'^2, 4Y'^4, 3U'(..)}
+DEV gejr gejq_double2(const gejr& a) {
+  fr A, B, YZ;
+  fr_mul3(A, B, YZ, a.x, a.x, a.y, a.y, a.y, a.z);
+  const fr E = fr_normalize_weak(fr_add(fr_add(A, A), A));  // 3 X^2
+  fr U, T2, F, BB;
+  fr_mul4(U, T2, F, BB, E, a.x, fr_add(a.x, a.x), B, E, E, B, B);  // 3X^3, 2XY^2, 9X^4, Y^4
+  gejr h;
+  h.x = fr_normalize_weak(fr_sub<3>(F, fr_mul_small(T2, 4)));       // 9X^4 - 8XY^2
+  h.z = fr_add(YZ, YZ);                                             // 2 Y Z, m2
+  const fr W = fr_normalize_weak(fr_sub<1>(fr_mul_small(B, 4), U));  // 4Y^2 - U
+  // row 0: 3U W - 8 Y^4 (the subtraction preset into its columns); row 1: X'^2
+  const uint64_t c0 = (uint64_t)rowsel(kconst<1>() - BB.v, 0u, 0u, 0u) << 3;
+  fr A1;
+  rep2(fr_mul_col(rowsel(fr_mul_small(U, 3), h.x, h.x, h.x), rowsel(W, h.x, h.x, h.x), c0), h.y, A1);
+  // second doubling
+  const fr E1 = fr_normalize_weak(fr_add(fr_add(A1, A1), A1));
+  fr B1, YZ1, U1, F1;
+  fr_mul4(B1, YZ1, U1, F1, h.y, h.y, h.y, h.z, E1, h.x, E1, E1);
+  gejr r;
+  r.z = fr_add(YZ1, YZ1);
+  const fr W1 = fr_normalize_weak(fr_sub<1>(fr_mul_small(B1, 4), U1));
+  fr T21, BB4, P;
+  const fr B12 = fr_add(B1, B1);
+  fr_mul3(T21, BB4, P, fr_add(h.x, h.x), B1, B12, B12, fr_mul_small(U1, 3), W1);  // 2X'Y'^2, 4Y'^4, 3U'W'
+  r.x = fr_normalize_weak(fr_sub<3>(F1, fr_mul_small(T21, 4)));
+  r.y = fr_normalize_weak(fr_sub<2>(P, fr_add(BB4, BB4)));         // 3U'W' - 8Y'^4
   return r;
 }
 

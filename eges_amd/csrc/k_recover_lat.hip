@@ -43,6 +43,19 @@ constexpr int LAT_WG = 128;
 #ifndef EGES_LAT_HOIST
 #define EGES_LAT_HOIST 1  // hoisted additions in the Strauss windows (strauss_win_fast); 0: plain steps
 #endif
+#ifndef EGES_LAT_DBL2
+#define EGES_LAT_DBL2 1  // doublings in pairs (frg.cuh gejq_double2: 5 quad levels per pair); 0: single
+#endif
+// k doublings of a (the unchecked chains: Strauss windows, D = 2^k R')
+DEV gejr gejq_double_n(gejr a, int k) {
+#if EGES_LAT_DBL2
+#pragma unroll 1
+  for (; k >= 2; k -= 2) a = gejq_double2(a);
+#endif
+#pragma unroll 1
+  for (; k > 0; --k) a = gejq_double(a);
+  return a;
+}
 constexpr int LAT_STAGE = 512;  // wire form: encodings up to this size decode out of LDS
 // Split form: windows [0, SPLIT_W0) of both GLV halves against the R' table on wave 0, windows
 // [SPLIT_W0, RWIN) against a table of D = 2^(RBITS SPLIT_W0) R' on waves 2 (R) and 3 (lambda R).
@@ -425,8 +438,7 @@ DEV void strauss_win_fast(gejr& acc, bool& inf, const TabT<NT>& tab, const ColT<
       if (db) add_r<false>(acc, inf, win_point(tab, btab, db, 1), true, dg);
       continue;
     }
-#pragma unroll 1
-    for (int k = 0; k < BITS - 1; ++k) acc = gejq_double(acc);
+    acc = gejq_double_n(acc, BITS - 1);
     if (!da && !db) {
       acc = gejq_double(acc);
       continue;
@@ -615,8 +627,7 @@ DEV void high_wave(LatLds& S, const fr& x, const fr& c, int j, const Diag& dg) {
   gejr D;
   fr_mul2(D.x, D.y, c, x, c, c);  // R' = (c x, c^2)
   D.z = fr_one();
-#pragma unroll 1
-  for (int k = 0; k < RBITS * SPLIT_W0; ++k) D = gejq_double(D);  // R' has odd order: never exceptional
+  D = gejq_double_n(D, RBITS * SPLIT_W0);  // R' has odd order: never exceptional
   ger Dp;
   Dp.x = D.x;
   Dp.y = D.y;
@@ -656,8 +667,7 @@ DEV void high_wave_tri(LatLds& S, const fr& x, const fr& c, const Diag& dg) {
   gejr D;
   fr_mul2(D.x, D.y, c, x, c, c);  // R' = (c x, c^2)
   D.z = fr_one();
-#pragma unroll 1
-  for (int k = 0; k < RBITS * TRI_W0; ++k) D = gejq_double(D);  // R' has odd order: never exceptional
+  D = gejq_double_n(D, RBITS * TRI_W0);  // R' has odd order: never exceptional
   ger Dp;
   Dp.x = D.x;
   Dp.y = D.y;
