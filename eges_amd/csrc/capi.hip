@@ -19,6 +19,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "eges.h"
@@ -158,6 +159,7 @@ const KnobDef KNOB_DEFS[KNOB_COUNT] = {
     {"EGES_PIPE_SEG", 8 << 20},
     {"EGES_HOST_PARTS", EGES_PIPE_PARTS},
     {"EGES_TEST_SKIP_FLAG", 0},
+    {"EGES_TEST_DELAY_X", 0},
 };
 std::atomic<long long> g_knob[KNOB_COUNT];
 std::once_flag g_knob_once;
@@ -187,7 +189,7 @@ struct Route {
   size_t pipe_chunk = 786432, pipe_first = 262144;
   long long pipe_streams = 1;
   size_t host_parts = EGES_PIPE_PARTS, pipe_seg = size_t(8) << 20;
-  uint32_t force_redo = 0, skip_flag = 0;
+  uint32_t force_redo = 0, skip_flag = 0, delay_x = 0;
   static Route now() {
     Route r;
     r.lat_max = (size_t)std::max<long long>(0, knob(KNOB_LAT_MAX));
@@ -206,6 +208,7 @@ struct Route {
     r.host_parts = (size_t)std::max<long long>(2, std::min<long long>(knob(KNOB_HOST_PARTS), 64));
     r.force_redo = knob(KNOB_FORCE_REDO) != 0 ? 1u : 0u;
     r.skip_flag = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TEST_SKIP_FLAG), 64));
+    r.delay_x = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TEST_DELAY_X), 4096));
     return r;
   }
 };
@@ -376,6 +379,7 @@ P with_diag(const Dev& d, P p, const Route& rt) {
   p.force_redo = rt.force_redo;
   p.test_skip_flag = rt.skip_flag;
   p.test_skip_block = 0;
+  if constexpr (std::is_same<P, RecoverParams>::value) p.test_delay_x = rt.delay_x;
   return p;
 }
 

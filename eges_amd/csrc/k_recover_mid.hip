@@ -699,6 +699,8 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
     S.pok[l] = live && q.ok ? 1u : 0u;
     BFLAG_SET(BF_PARSED);
   } else if (wv == 0) {  // R's x straight from the encoding, without waiting for S's checks
+#pragma unroll 1
+    for (uint32_t k = 0; k < prm.test_delay_x; ++k) __builtin_amdgcn_s_sleep(127);  // tests only
     q.ok = live && wire_r_only(S, prm, idx, stage_a0, stage_end, q.xr);
   } else {
     q.ok = false;  // Y waves: read from LDS at the end

@@ -39,6 +39,8 @@ enum KnobId : int {
                           //   at least PIPE_MIN / 2 signatures each)
   KNOB_TEST_SKIP_FLAG,    // tests: k > 0 makes item 0's workgroup's producer of hand-off flag k - 1
                           //   skip publishing it (handoff.cuh), so its consumers time out
+  KNOB_TEST_DELAY_X,      // tests: the bucket form's wave X sleeps k x ~3 us before it reads its
+                          //   workgroup's wire stage (the stage / part[0] release)
   KNOB_COUNT
 };
 

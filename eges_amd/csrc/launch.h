@@ -51,6 +51,8 @@ struct RecoverParams {
   // tests only (KNOB_TEST_SKIP_FLAG, handoff.cuh): workgroup test_skip_block's producer of hand-off
   // flag test_skip_flag - 1 skips publishing it
   uint32_t test_skip_flag = 0, test_skip_block = 0;
+  // tests only (KNOB_TEST_DELAY_X): the bucket form's wave X sleeps before it reads the wire stage
+  uint32_t test_delay_x = 0;
   // latency / mid-size kernels: types.Sender rows straight from the caller's SoA rows (n x 32
   // big-endian sighash, r, s, v, 4-byte aligned; vflags n bytes, nullable) instead of record rows:
   // prep_sender_kernel's classification (sender.cuh sender_meta) fused in (sender_parse_*)

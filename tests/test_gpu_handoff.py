@@ -118,6 +118,26 @@ def test_bucket_wire_form_skipped_flag_faults_one_workgroup(engine, flag):
     engine.diag_counters(reset=True)
 
 
+def test_bucket_wire_form_delayed_x_keeps_the_stage(engine):
+    """in the bucket form's wire path wave S's u1 G part shares LDS with the staged
+    encodings wave X reads R from. EGES_TEST_DELAY_X holds every X wave back ~0.7 ms before that
+    read, long after S would otherwise have written its part: S must wait for X's first published
+    point (the stage's release), so every address stays exact."""
+    import torch
+    from eges_amd import txs
+    n = 2000
+    h = txs.c1_sighashes(0, n)
+    sig_d, exp_d = engine.synth_sign_msg_dev(torch.from_numpy(h).cuda(), 0)
+    torch.cuda.synchronize()
+    sig_h, exp = sig_d.cpu().numpy(), exp_d.cpu().numpy()
+    packed = engine.pack_raw(txs.c1_raw(0, sig_h))
+    engine.diag_counters(reset=True)
+    with knobs(engine, dict(BUCKET, EGES_WIRE_FUSED=1, EGES_TEST_DELAY_X=200)):
+        a, s_, _ = engine.sender_raw_batch(packed, _lib.SIGNER_EIP155, txs.GEEC_CHAIN_ID)
+    assert (s_ == 0).all() and np.array_equal(a, exp)
+    assert engine.diag_counters(reset=True)["handoff"] == 0
+
+
 def test_verify_split_form_skipped_flag_faults_one_item(engine):
     g = load_golden("verify.npz")
     n = 40
