@@ -160,6 +160,7 @@ const KnobDef KNOB_DEFS[KNOB_COUNT] = {
     {"EGES_HOST_PARTS", EGES_PIPE_PARTS},
     {"EGES_TEST_SKIP_FLAG", 0},
     {"EGES_TEST_DELAY_X", 0},
+    {"EGES_HOST_STREAMS", 1},
 };
 std::atomic<long long> g_knob[KNOB_COUNT];
 std::once_flag g_knob_once;
@@ -189,6 +190,7 @@ struct Route {
   size_t pipe_chunk = 786432, pipe_first = 262144;
   long long pipe_streams = 1;
   size_t host_parts = EGES_PIPE_PARTS, pipe_seg = size_t(8) << 20;
+  long long host_streams = 1;
   uint32_t force_redo = 0, skip_flag = 0, delay_x = 0;
   static Route now() {
     Route r;
@@ -205,6 +207,7 @@ struct Route {
     r.pipe_streams = knob(KNOB_PIPE_STREAMS);
     r.tri_max = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_LAT_TRI_MAX), 1u << 30));
     r.pipe_seg = (size_t)std::max<long long>(1 << 20, knob(KNOB_PIPE_SEG));
+    r.host_streams = knob(KNOB_HOST_STREAMS);
     r.host_parts = (size_t)std::max<long long>(2, std::min<long long>(knob(KNOB_HOST_PARTS), 64));
     r.force_redo = knob(KNOB_FORCE_REDO) != 0 ? 1u : 0u;
     r.skip_flag = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TEST_SKIP_FLAG), 64));
@@ -503,6 +506,16 @@ extern "C" size_t eges_diag_read_stamps(uint64_t* out, size_t max_waves) {
 }
 #endif
 
+// the device's second compute stream and workspace (overlapped launches), created on first use
+int ensure_aux(Dev& d) {
+  if (d.aux) return EGES_SUCCESS;
+  HIPCHK(hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&d.ev_fork, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&d.ev_join, hipEventDisableTiming));
+  HIPCHK(hipMalloc(&d.ws2, ws_bytes_per_block() * (size_t)d.ws_blocks));
+  return EGES_SUCCESS;
+}
+
 int run_recover_dev_overlap(Dev& d, const Route& rt, const uint8_t* msg, const uint8_t* sig, size_t n, uint8_t* pub, uint8_t* addr,
                             uint8_t* status, hipStream_t st, int parts) {
   const size_t per = std::min(CHUNK, (n + parts - 1) / parts);
@@ -510,12 +523,7 @@ int run_recover_dev_overlap(Dev& d, const Route& rt, const uint8_t* msg, const u
   const size_t region = align_up(recover_scratch_bytes(n_pad), 256);
   int rc = dev_ensure_buf(d, 2 * region);
   if (rc) return rc;
-  if (!d.aux) {
-    HIPCHK(hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&d.ev_fork, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&d.ev_join, hipEventDisableTiming));
-    HIPCHK(hipMalloc(&d.ws2, ws_bytes_per_block() * (size_t)d.ws_blocks));
-  }
+  if ((rc = ensure_aux(d))) return rc;
   Serial ser(d, st);
   HIPCHK(hipEventRecord(d.ev_fork, st));
   HIPCHK(hipStreamWaitEvent(d.aux, d.ev_fork, 0));
@@ -765,18 +773,24 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   if (rc) return rc;
   // a single chunk has nothing to overlap: one stream, no cross-stream waits (C3 latency)
   hipStream_t st = small ? lane->stream : d.stream, sx = nreg > 1 ? d.copy : st;
-  // Every return after this point (errors included) first drains both streams, so the lane /
+  // EGES_HOST_STREAMS = 2: the chunks' kernels alternate between the device's two compute
+  // streams and workspaces, so one chunk's launch can start in the previous one's tail
+  const bool two = nreg > 1 && rt.host_streams >= 2;
+  if (two && (rc = ensure_aux(d))) return rc;
+  hipStream_t sa = two ? d.aux : st;
+  // Every return after this point (errors included) first drains every stream, so the lane /
   // device mutex is never released while kernels or copies of this call still touch its
   // pinned staging or scratch (the next caller writes its inputs there).
   struct Drain {
-    hipStream_t a, b;
+    hipStream_t a, b, c;
     bool armed;
     ~Drain() {
       if (!armed) return;
       (void)hipStreamSynchronize(a);
       if (b != a) (void)hipStreamSynchronize(b);
+      if (c != a) (void)hipStreamSynchronize(c);
     }
-  } drain{st, sx, true};
+  } drain{st, sx, sa, true};
   if (pinned && !pin && hipHostMalloc(&pin, PIN_BYTES, hipHostMallocDefault) != hipSuccess) {
     pin = nullptr;
     return set_err(EGES_E_NOMEM, "hipHostMalloc(%zu) failed", PIN_BYTES);
@@ -784,6 +798,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   if (!small) {
     HIPCHK(hipStreamWaitEvent(st, d.last, 0));
     HIPCHK(hipStreamWaitEvent(sx, d.last, 0));
+    if (two) HIPCHK(hipStreamWaitEvent(sa, d.last, 0));
   }
   HSTAMP(1);
   // Input staging: each input array goes to its offset in the region, either by its own
@@ -817,7 +832,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   do {                                                  \
     if (sx != st) {                                     \
       HIPCHK(hipEventRecord(ev_in[r], sx));             \
-      HIPCHK(hipStreamWaitEvent(st, ev_in[r], 0));      \
+      HIPCHK(hipStreamWaitEvent(sk, ev_in[r], 0));      \
     }                                                   \
   } while (0)
   struct Pending {
@@ -861,6 +876,8 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     const size_t m = std::min(c, off + cnt - base);
     const size_t m_pad = align_up(m, 64);
     const int r = ci % nreg;
+    hipStream_t sk = (two && r) ? sa : st;         // this chunk's compute stream
+    uint32_t* wsk = (two && r) ? d.ws2 : d.ws;     //   and workspace
     const Region rg = region_for(j, base, m);
     uint8_t* B = dbuf + (size_t)r * worst;
     uint8_t* I = pinned ? pin : B;  // where the kernels read the inputs
@@ -877,14 +894,14 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       FLUSH_IN(B);
       JOIN_IN(r);
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, j.addr ? o_addr : nullptr, j.pub ? o_pub : nullptr,
-                      d.gtab, d.ws};
+                      d.gtab, wsk};
       if (fused_parse(d, rt, m)) {  // the latency / mid-size kernels parse the bytes themselves
         p.raw_msg = dm;
         p.raw_sig = ds;
       } else {
-        HIPCHK(launch_prep_ecrecover(dm, ds, (uint32_t)m, (uint32_t)m_pad, rec, st));
+        HIPCHK(launch_prep_ecrecover(dm, ds, (uint32_t)m, (uint32_t)m_pad, rec, sk));
       }
-      HIPCHK(launch_recover_pass(d, rt, p, st));
+      HIPCHK(launch_recover_pass(d, rt, p, sk));
     } else if (j.kind == HostJob::SENDER) {
       uint8_t* dh = I;
       uint8_t* dr = dh + m * 32;
@@ -898,13 +915,13 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       if (j.e) H2D(B, df, j.e + base, m);
       FLUSH_IN(B);
       JOIN_IN(r);
-      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
+      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, wsk};
       if (sender_fused(d, rt, m, {dh, dr, dsv, dv}))  // the recover kernel reads the rows itself
         bind_sender_rows(p, dh, dr, dsv, dv, j.e ? df : nullptr, j.signer, j.chain_id);
       else
         HIPCHK(launch_prep_sender(dh, dr, dsv, dv, j.e ? df : nullptr, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id,
-                                  rec, st));
-      HIPCHK(launch_recover_pass(d, rt, p, st));
+                                  rec, sk));
+      HIPCHK(launch_recover_pass(d, rt, p, sk));
     } else if (j.kind == HostJob::PRECOMPILE) {
       uint8_t* din = I;
       uint32_t* dlen = reinterpret_cast<uint32_t*>(din + m * 128);
@@ -913,10 +930,10 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       FLUSH_IN(B);
       JOIN_IN(r);
       if (pinned) std::memset(o_addr, 0, m * 32);
-      else HIPCHK(hipMemsetAsync(o_addr, 0, m * 32, st));
-      HIPCHK(launch_prep_precompile(din, j.inlen ? dlen : nullptr, (uint32_t)m, (uint32_t)m_pad, rec, st));
-      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr + 12, nullptr, d.gtab, d.ws, 32};
-      HIPCHK(launch_recover_pass(d, rt, p, st));
+      else HIPCHK(hipMemsetAsync(o_addr, 0, m * 32, sk));
+      HIPCHK(launch_prep_precompile(din, j.inlen ? dlen : nullptr, (uint32_t)m, (uint32_t)m_pad, rec, sk));
+      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr + 12, nullptr, d.gtab, wsk, 32};
+      HIPCHK(launch_recover_pass(d, rt, p, sk));
     } else if (j.kind == HostJob::SENDER_RAW) {
       uint8_t* draw = I;
       uint64_t* doff = reinterpret_cast<uint64_t*>(draw + align_up(rg.raw_len, 8));
@@ -933,9 +950,9 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       FLUSH_IN(B);
       JOIN_IN(r);
       if (j.decode_only) {  // the decoder's flags straight into the status bytes
-        HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, o_st, st));
+        HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, o_st, sk));
       } else {
-        RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, d.ws};
+        RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, wsk};
         if (fused) {
           p.wire_raw = draw;
           p.wire_off = doff;
@@ -943,10 +960,10 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
           p.wire_chain_id = j.chain_id;
           p.wire_sighash = j.sighash ? hs : nullptr;
         } else {
-          HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, vf, st));
-          HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, st));
+          HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, vf, sk));
+          HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, sk));
         }
-        HIPCHK(launch_recover_pass(d, rt, p, st));
+        HIPCHK(launch_recover_pass(d, rt, p, sk));
       }
     } else {
       uint8_t* dp = I;
@@ -959,14 +976,14 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       H2D(B, ds, j.d + base * 64, m * 64);
       FLUSH_IN(B);
       JOIN_IN(r);
-      VerifyParams p{dp, dl, dm, ds, (uint32_t)m, o_st, d.gtab, d.ws};
+      VerifyParams p{dp, dl, dm, ds, (uint32_t)m, o_st, d.gtab, wsk};
       verify_scratch_bind(p, B + rg.o_rec, m_pad);
       p = with_diag(d, p, rt);
       // small (lane) calls must not touch the device's shared workspace: latency kernel
-      HIPCHK(launch_verify_any(d, rt, p, small, st));
+      HIPCHK(launch_verify_any(d, rt, p, small, sk));
     }
     HSTAMP(3);
-    if (sx != st) HIPCHK(hipEventRecord(ev_k[r], st));
+    if (sx != st) HIPCHK(hipEventRecord(ev_k[r], sk));
     // --- the previous chunk's outputs, while this chunk computes
     if (have_prev) {
       rc = outputs(prev);
@@ -982,6 +999,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   if (!small) HIPCHK(hipEventRecord(d.last, sx));
   HIPCHK(hipStreamSynchronize(sx));
   if (sx != st) HIPCHK(hipStreamSynchronize(st));  // (st's last work is already behind sx's events)
+  if (sa != st) HIPCHK(hipStreamSynchronize(sa));
   HSTAMP(4);
   drain.armed = false;
   if (pinned && have_prev) unpack(prev);

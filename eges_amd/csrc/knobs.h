@@ -41,6 +41,7 @@ enum KnobId : int {
                           //   skip publishing it (handoff.cuh), so its consumers time out
   KNOB_TEST_DELAY_X,      // tests: the bucket form's wave X sleeps k x ~3 us before it reads its
                           //   workgroup's wire stage (the stage / part[0] release)
+  KNOB_HOST_STREAMS,      // the chunked host path's kernels on 1 (default) or 2 alternating compute streams
   KNOB_COUNT
 };
 

@@ -94,3 +94,22 @@ def test_pipe_precompile_matches_single_chunk(engine):
         out0, st0 = engine.ecrecover_precompile_batch(inp)
     assert np.array_equal(st, st0) and np.array_equal(out, out0)
     assert (st[::7] != 0).all() and (st[1::7] == 0).all()
+
+
+@pytest.mark.parametrize("streams", [1, 2])
+def test_chunked_path_golden_tiled(engine, streams):
+    """the default chunked host path (EGES_HOST_PIPE = 0) on a ragged 5-chunk batch, its kernels
+    on one or on two alternating compute streams / workspaces (EGES_HOST_STREAMS)"""
+    g = load_golden("recover.npz")
+    n = 600011
+    msg, sig = _tile(g["msg"], n), _tile(g["sig"], n)
+    with knobs(engine, {"EGES_HOST_PIPE": 0, "EGES_HOST_PARTS": 5, "EGES_HOST_STREAMS": streams}):
+        pub, addr, st = engine.ecrecover_batch(msg, sig)
+    assert np.array_equal(st, _tile(g["status"], n))
+    assert np.array_equal(pub, _tile(g["pub"], n))
+    gs = load_golden("sender.npz")
+    sel = np.nonzero((gs["signer"] == 2) & (gs["chain_id"] == 930412))[0]
+    cols = {k: _tile(gs[k][sel], n) for k in ("sighash", "r", "s", "v", "vflags", "status", "addr")}
+    with knobs(engine, {"EGES_HOST_PIPE": 0, "EGES_HOST_PARTS": 5, "EGES_HOST_STREAMS": streams}):
+        a, s_ = engine.sender_batch(cols["sighash"], cols["r"], cols["s"], cols["v"], cols["vflags"], 2, 930412)
+    assert np.array_equal(s_, cols["status"]) and np.array_equal(a, cols["addr"])
