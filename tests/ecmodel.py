@@ -9,7 +9,12 @@ in advance which addition of which form meets P == +-Q:
                two 128-bit halves in 20-bit windows added every 4th window (core.cuh strauss)
   narrow       u_r R over the 26 windows (wave 0) and u_g G by the 16-bit comb (wave 1), joined
   split        windows [0, 15) of both halves (wave 0), the rest in 4-bit windows per half
-               against D = 2^75 R (waves 2, 3, joined), u_g G by the comb; joins (A + G) + H
+               against D = 2^75 R (waves 2, 3, joined), u_g G by the comb; joins (A + H) + G
+               (round 4: the R sums joined on E' first, y applied once)
+  tri          the three-wave form: windows [0, 20) on wave 0, the rest of both halves jointly
+               on wave 2 against D = 2^100 R; joins (A + H) + G
+  windowed     the mid-size kernel's windowed form (and the split form before round 4): the
+               split form's windows, joins (A + G) + H
   bucket       the mid-size kernel: each GLV half in signed 3-bit windows, window k's digit d
                adds sign(d) 2^(3k) R into bucket |d| (bottom-up), Q_h = (B1 + B3) +
                2 ((B2 + B3) + 2 B4), then (Q_1 + Q_2) + u_g G (k_recover_mid.hip recover_bkt_body)
@@ -41,6 +46,7 @@ RBITS, RWIN = 5, 26          # core.cuh
 GBITS, GWIN, GSTEP = 20, 7, 4
 CBITS, CWIN = 16, 16         # comb
 SPLIT_W0, HBITS = 15, 4      # k_recover_lat.hip
+TRI_W0 = 20
 BK_BITS, BK_WIN, BK_NB = 3, 43, 4  # k_recover_mid.hip bucket form
 HWIN = (130 - RBITS * SPLIT_W0 + HBITS) // HBITS
 
@@ -105,12 +111,13 @@ def digits_narrow(u):
     return recode(k1, RBITS, RWIN)[0], recode(k2, RBITS, RWIN)[0]
 
 
-def digits_split(u):
-    """recode_split: SPLIT_W0 5-bit windows, then (carry included) HWIN 4-bit windows."""
+def digits_split(u, w0=SPLIT_W0):
+    """recode_split: w0 5-bit windows, then (carry included) the high part's 4-bit windows."""
+    nh = (130 - RBITS * w0 + HBITS) // HBITS
     out = []
     for k in glv_split(u):
-        lo, carry, m = recode(k, RBITS, SPLIT_W0)
-        hi, _, _ = recode(m, HBITS, HWIN, carry=carry, out=k < 0)
+        lo, carry, m = recode(k, RBITS, w0)
+        hi, _, _ = recode(m, HBITS, nh, carry=carry, out=k < 0)
         out.append((lo, hi))
     return out
 
@@ -205,37 +212,71 @@ def narrow(u_r, u_g, rho):
     return (None if q.inf else q.v), ev
 
 
-def split_parts(u_r):
+def split_parts(u_r, w0=SPLIT_W0):
     """The split form's low and high scalars (low + high == u_r mod n)."""
-    (lo0, hi0), (lo1, hi1) = digits_split(u_r)
-    low = sum((lo0[w] + lo1[w] * LAM) * 32**w for w in range(SPLIT_W0)) % N
-    high = sum((hi0[w] + hi1[w] * LAM) * 16**w for w in range(HWIN)) * 2**(RBITS * SPLIT_W0) % N
+    nh = (130 - RBITS * w0 + HBITS) // HBITS
+    (lo0, hi0), (lo1, hi1) = digits_split(u_r, w0)
+    low = sum((lo0[w] + lo1[w] * LAM) * 32**w for w in range(w0)) % N
+    high = sum((hi0[w] + hi1[w] * LAM) * 16**w for w in range(nh)) * 2**(RBITS * w0) % N
     return low, high
 
 
-def split(u_r, u_g, rho):
-    """k_recover_lat.hip split form: wave 0 low windows, waves 2 / 3 high windows per half
-    (joined on wave 2), wave 1 the comb; Q = (low + u_g G) + high."""
-    ev = []
-    (lo0, hi0), (lo1, hi1) = digits_split(u_r)
+def _split_sums(u_r, rho, ev, w0, joint_high):
+    """wave 0's low windows (tag lat_lo) and the high sum: one wave per half joined (lat_hi0 /
+    lat_hi1, join_hi) or both halves on one wave (lat_hi)"""
+    nh = (130 - RBITS * w0 + HBITS) // HBITS
+    (lo0, hi0), (lo1, hi1) = digits_split(u_r, w0)
     a = Acc(ev, "lat_lo")
-    for w in range(SPLIT_W0 - 1, -1, -1):
-        if w != SPLIT_W0 - 1:
+    for w in range(w0 - 1, -1, -1):
+        if w != w0 - 1:
             a.dbl(RBITS)
         for j, (d, base) in enumerate(((lo0[w], rho), (lo1[w], rho * LAM))):
             if d:
                 a.add(d * base, (w, j))
-    D = rho * 2**(RBITS * SPLIT_W0)
+    D = rho * 2**(RBITS * w0)
+    if joint_high:
+        H = Acc(ev, "lat_hi")
+        for w in range(nh - 1, -1, -1):
+            if w != nh - 1:
+                H.dbl(HBITS)
+            for j, (hd, base) in enumerate(((hi0, D), (hi1, D * LAM))):
+                if hd[w]:
+                    H.add(hd[w] * base, (w, j))
+        return a, H
     hs = []
     for j, (hd, base) in enumerate(((hi0, D), (hi1, D * LAM))):
         h = Acc(ev, f"lat_hi{j}")
-        for w in range(HWIN - 1, -1, -1):
-            if w != HWIN - 1:
+        for w in range(nh - 1, -1, -1):
+            if w != nh - 1:
                 h.dbl(HBITS)
             if hd[w]:
                 h.add(hd[w] * base, (w, j))
         hs.append(h)
-    H = join(hs[0], hs[1], ev, "join_hi")
+    return a, join(hs[0], hs[1], ev, "join_hi")
+
+
+def split(u_r, u_g, rho):
+    """k_recover_lat.hip split form (round 4): wave 0 low windows, waves 2 / 3 high windows per
+    half (joined on wave 2), the R sums joined (join_lohi), then + u_g G (join)."""
+    ev = []
+    a, H = _split_sums(u_r, rho, ev, SPLIT_W0, False)
+    q = join(join(a, H, ev, "join_lohi"), comb(u_g, ev), ev, "join")
+    return (None if q.inf else q.v), ev
+
+
+def tri(u_r, u_g, rho):
+    """k_recover_lat.hip three-wave form: wave 0 windows [0, TRI_W0), wave 2 the rest of both
+    halves jointly; Q = (low + high) + u_g G."""
+    ev = []
+    a, H = _split_sums(u_r, rho, ev, TRI_W0, True)
+    q = join(join(a, H, ev, "join_lohi"), comb(u_g, ev), ev, "join")
+    return (None if q.inf else q.v), ev
+
+
+def windowed(u_r, u_g, rho):
+    """k_recover_mid.hip windowed form (the split form's windows, joins (A + u_g G) + H)."""
+    ev = []
+    a, H = _split_sums(u_r, rho, ev, SPLIT_W0, False)
     q = join(join(a, comb(u_g, ev), ev, "join"), H, ev, "join")
     return (None if q.inf else q.v), ev
 
@@ -284,8 +325,9 @@ def recover_input(rho, R, u1, u2):
 def recover_cases(rng, count=8):
     """Recovery inputs that make each form meet an exceptional sum, with the form and branch each
     targets: ("ls", "dbl"/"inf") the lane-serial loop at window 0 (u_g < 2^19, u_r R == +-u_g G),
-    ("join", ...) the narrow join (u_r R == +-u_g G), ("split1", ...) the split form's first join
-    (low(u_r) R == +-u_g G), ("split2", ...) its second ((low R + u_g G) == +-high R)."""
+    ("join", ...) the narrow, split and three-wave forms' final join (u_r R == +-u_g G), ("split1",
+    ...) the windowed form's first join (low(u_r) R == +-u_g G), ("split2", ...) its second
+    ((low R + u_g G) == +-high R)."""
     out = []
     for i in range(count):
         rho, R = point_for(rng.randrange(1, N))

@@ -44,7 +44,7 @@ def test_random_scalars_meet_no_exceptional_sum():
         rho = rnd.randrange(1, M.N)
         u_r, u_g = rnd.randrange(1, M.N), rnd.randrange(1, M.N)
         want = (u_r * rho + u_g) % M.N
-        for form in (M.lane_serial, M.narrow, M.split, M.bucket):
+        for form in (M.lane_serial, M.narrow, M.split, M.tri, M.windowed, M.bucket):
             q, ev = form(u_r, u_g, rho)
             assert q == want and ev == [], (form.__name__, ev)
 
@@ -64,9 +64,9 @@ def test_verdict_construction_does_not_poison_the_r_loops():
                 e = rnd.randrange(-15, 17)
                 u_r = ((a + b * M.LAM) * 32**(w + 1) + (j + e * M.LAM) * 32**w + low) % M.N
                 rho = rnd.randrange(1, M.N)
-                for form in (M.narrow, M.split, M.bucket):
+                for form in (M.narrow, M.split, M.tri, M.windowed, M.bucket):
                     _, ev = form(u_r, rnd.randrange(1, M.N), rho)
-                    assert not [x for x in ev if x[0] in ("lat_r", "lat_lo", "lat_hi0", "lat_hi1", "bk0", "bk1")], (w, j, ev)
+                    assert not [x for x in ev if x[0] in ("lat_r", "lat_lo", "lat_hi", "lat_hi0", "lat_hi1", "bk0", "bk1")], (w, j, ev)
                 _, ev = M.lane_serial(u_r, rnd.randrange(1, M.N), rho)
                 assert ev == [], (w, j, ev)
                 hits += 1
@@ -91,7 +91,7 @@ def test_constructions_reach_every_reachable_branch():
     seen = set()
     for kind, sign, rho, R, u1, u2 in M.recover_cases(rnd, 10):
         want = (u2 * rho + u1) % M.N
-        res = {f.__name__: f(u2, u1, rho) for f in (M.lane_serial, M.narrow, M.split)}
+        res = {f.__name__: f(u2, u1, rho) for f in (M.lane_serial, M.narrow, M.split, M.tri, M.windowed)}
         for name, (q, ev) in res.items():
             assert (q if q is not None else 0) == want, (kind, name)
         br = "dbl" if sign == 1 else "inf"
@@ -99,13 +99,14 @@ def test_constructions_reach_every_reachable_branch():
             assert ("ls", br) in {(t, b) for t, b, _ in res["lane_serial"][1]}, res["lane_serial"][1]
             assert ("join", br) in {(t, b) for t, b, _ in res["narrow"][1]}
         elif kind == "join":
-            assert ("join", br) in {(t, b) for t, b, _ in res["narrow"][1]}
+            for f in ("narrow", "split", "tri"):
+                assert ("join", br) in {(t, b) for t, b, _ in res[f][1]}, (f, res[f][1])
         else:
-            assert ("join", br) in {(t, b) for t, b, _ in res["split"][1]}, (kind, res["split"][1])
+            assert ("join", br) in {(t, b) for t, b, _ in res["windowed"][1]}, (kind, res["windowed"][1])
         seen |= {(kind, br)}
         # the R-table loops stay clear in every construction
         for name, (q, ev) in res.items():
-            assert not [x for x in ev if x[0] in ("lat_r", "lat_lo", "lat_hi0", "lat_hi1", "comb")]
+            assert not [x for x in ev if x[0] in ("lat_r", "lat_lo", "lat_hi", "lat_hi0", "lat_hi1", "comb")]
     assert len(seen) == 8
     # recover inputs encode u1 = -z / r, u2 = s / r
     for kind, sign, rho, R, u1, u2 in M.recover_cases(rnd, 2):
@@ -123,7 +124,7 @@ def test_verify_constructions():
         assert 0 < s <= M.N // 2
         u1, u2 = z * pow(s, -1, M.N) % M.N, r * pow(s, -1, M.N) % M.N
         br = "dbl" if sign == 1 else "inf"
-        form = {"ls": M.lane_serial, "join": M.narrow, "split1": M.split, "split2": M.split}[kind]
+        form = {"ls": M.lane_serial, "join": M.narrow, "split1": M.windowed, "split2": M.windowed}[kind]
         q, ev = form(u2, u1, rho)
         tag = "ls" if kind == "ls" else "join"
         assert (tag, br) in {(t, b) for t, b, _ in ev}, (kind, ev)
