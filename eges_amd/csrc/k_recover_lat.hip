@@ -621,8 +621,8 @@ DEV void helper_split(LatLds& S, const uint32_t* gcomb, bool need_y, const fr& c
 }
 // Split form, waves 2 (j = 0: R) and 3 (j = 1: lambda R): D = 2^(RBITS SPLIT_W0) R' by doublings
 // (each wave its own copy, no hand-off), the table of D's (X, Y) on the curve where it is affine,
-// the high windows of one GLV half: a sum (X, Y, Z) there is the E' point (X, Y, Z zeta_D Z_D).
-// Wave 2 joins wave 3's part on E'; wave 0 maps the whole R sum to E with y once.
+// the high windows of one GLV half, then back to the true curve: a sum (X, Y, Z) there is the E'
+// point (X, Y, Z zeta_D Z_D) and the E point (X, Y, Z zeta_D Z_D y). Wave 2 joins wave 3's part.
 DEV void high_wave(LatLds& S, const fr& x, const fr& c, int j, const Diag& dg) {
   gejr D;
   fr_mul2(D.x, D.y, c, x, c, c);  // R' = (c x, c^2)
@@ -638,7 +638,8 @@ DEV void high_wave(LatLds& S, const fr& x, const fr& c, int j, const Diag& dg) {
   gejr A;
   bool ainf;
   strauss_win_exact<HBITS, HTAB>(A, ainf, S.dtab[j], S.dbtab, S.hdig[0], S.hdig[1], 1 << j, 0, HWIN, dg);
-  A.z = fr_mul(A.z, scale);
+  flag_wait(S, F_Y);
+  A.z = fr_mul(A.z, fr_mul(scale, fr{S.ylift[row_lane()]}));
   if (j == 1) {
     put_part(S, 4, A, ainf);
     flag_set(S, F_LHI);
@@ -709,16 +710,15 @@ DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& 
   bool ainf;
   strauss_win_exact<RBITS, PTAB>(A, ainf, S.tab, S.btab, S.rdig[0], S.rdig[1], 3, 0,
                                  SPLIT ? SPLIT_W0 : FORM == FORM_TRI ? TRI_W0 : RWIN, dg);
-  if constexpr (FORM != FORM_NARROW) {
+  if constexpr (FORM == FORM_TRI) {
     // the low and high sums joined on E' (the addition formulas do not involve b), then to E
-    // with y (split: wave 1's root; three-wave: the root helpers') once, then + u_g G
+    // with y (from the root helpers) once, then + u_g G
     A.z = fr_mul(A.z, zeta);
     flag_wait(S, F_HI);
     bool hinf;
     const gejr Hp = get_part(S, 3, hinf);
     A = join_parts(A, ainf, Hp, hinf, ainf, dg);
-    if (SPLIT) flag_wait(S, F_Y);
-    else root_fetch(*root->prm, root->idx, c, root->odd, S);
+    root_fetch(*root->prm, root->idx, c, root->odd, S);
     A.z = fr_mul(A.z, fr{S.ylift[row_lane()]});
     flag_wait(S, F_G);
     bool ginf;
@@ -727,13 +727,20 @@ DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& 
     st->mark(4);
     return;
   }
-  // narrow form
-  __syncthreads();  // partial sums (and y) ready
+  if (SPLIT) flag_wait(S, F_Y);
+  else __syncthreads();  // partial sums (and y) ready
   if (root) root_fetch(*root->prm, root->idx, c, root->odd, S);  // (this wave's own LDS words)
   A.z = fr_mul(A.z, fr_mul(zeta, fr{S.ylift[row_lane()]}));  // the true curve
   bool ginf;
+  if (SPLIT) flag_wait(S, F_G);
   const gejr Gp = get_part(S, 2, ginf);
   Q = join_parts(A, ainf, Gp, ginf, qinf, dg);
+  if (SPLIT) {
+    flag_wait(S, F_HI);
+    bool hinf;
+    const gejr Hp = get_part(S, 3, hinf);
+    Q = join_parts(Q, qinf, Hp, hinf, qinf, dg);
+  }
   st->mark(4);
 }
 

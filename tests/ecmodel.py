@@ -9,12 +9,10 @@ in advance which addition of which form meets P == +-Q:
                two 128-bit halves in 20-bit windows added every 4th window (core.cuh strauss)
   narrow       u_r R over the 26 windows (wave 0) and u_g G by the 16-bit comb (wave 1), joined
   split        windows [0, 15) of both halves (wave 0), the rest in 4-bit windows per half
-               against D = 2^75 R (waves 2, 3, joined), u_g G by the comb; joins (A + H) + G
-               (round 4: the R sums joined on E' first, y applied once)
+               against D = 2^75 R (waves 2, 3, joined), u_g G by the comb; joins (A + G) + H
   tri          the three-wave form: windows [0, 20) on wave 0, the rest of both halves jointly
                on wave 2 against D = 2^100 R; joins (A + H) + G
-  windowed     the mid-size kernel's windowed form (and the split form before round 4): the
-               split form's windows, joins (A + G) + H
+  windowed     the mid-size kernel's windowed form: the split form's schedule
   bucket       the mid-size kernel: each GLV half in signed 3-bit windows, window k's digit d
                adds sign(d) 2^(3k) R into bucket |d| (bottom-up), Q_h = (B1 + B3) +
                2 ((B2 + B3) + 2 B4), then (Q_1 + Q_2) + u_g G (k_recover_mid.hip recover_bkt_body)
@@ -256,11 +254,12 @@ def _split_sums(u_r, rho, ev, w0, joint_high):
 
 
 def split(u_r, u_g, rho):
-    """k_recover_lat.hip split form (round 4): wave 0 low windows, waves 2 / 3 high windows per
-    half (joined on wave 2), the R sums joined (join_lohi), then + u_g G (join)."""
+    """k_recover_lat.hip split form: wave 0 low windows, waves 2 / 3 high windows per half
+    (joined on wave 2), wave 1 the comb; Q = (low + u_g G) + high. (Joining the R sums first, on
+    E', puts a second join after the high waves' finish: measured slower, not kept.)"""
     ev = []
     a, H = _split_sums(u_r, rho, ev, SPLIT_W0, False)
-    q = join(join(a, H, ev, "join_lohi"), comb(u_g, ev), ev, "join")
+    q = join(join(a, comb(u_g, ev), ev, "join"), H, ev, "join")
     return (None if q.inf else q.v), ev
 
 
@@ -274,11 +273,8 @@ def tri(u_r, u_g, rho):
 
 
 def windowed(u_r, u_g, rho):
-    """k_recover_mid.hip windowed form (the split form's windows, joins (A + u_g G) + H)."""
-    ev = []
-    a, H = _split_sums(u_r, rho, ev, SPLIT_W0, False)
-    q = join(join(a, comb(u_g, ev), ev, "join"), H, ev, "join")
-    return (None if q.inf else q.v), ev
+    """k_recover_mid.hip windowed form: the split form's schedule (joins (A + u_g G) + H)."""
+    return split(u_r, u_g, rho)
 
 
 def bucket(u_r, u_g, rho):
@@ -325,8 +321,8 @@ def recover_input(rho, R, u1, u2):
 def recover_cases(rng, count=8):
     """Recovery inputs that make each form meet an exceptional sum, with the form and branch each
     targets: ("ls", "dbl"/"inf") the lane-serial loop at window 0 (u_g < 2^19, u_r R == +-u_g G),
-    ("join", ...) the narrow, split and three-wave forms' final join (u_r R == +-u_g G), ("split1",
-    ...) the windowed form's first join (low(u_r) R == +-u_g G), ("split2", ...) its second
+    ("join", ...) the narrow and three-wave forms' final join (u_r R == +-u_g G), ("split1", ...)
+    the split (and windowed) form's first join (low(u_r) R == +-u_g G), ("split2", ...) its second
     ((low R + u_g G) == +-high R)."""
     out = []
     for i in range(count):

@@ -99,10 +99,11 @@ def test_constructions_reach_every_reachable_branch():
             assert ("ls", br) in {(t, b) for t, b, _ in res["lane_serial"][1]}, res["lane_serial"][1]
             assert ("join", br) in {(t, b) for t, b, _ in res["narrow"][1]}
         elif kind == "join":
-            for f in ("narrow", "split", "tri"):
+            for f in ("narrow", "tri"):
                 assert ("join", br) in {(t, b) for t, b, _ in res[f][1]}, (f, res[f][1])
         else:
-            assert ("join", br) in {(t, b) for t, b, _ in res["windowed"][1]}, (kind, res["windowed"][1])
+            for f in ("split", "windowed"):
+                assert ("join", br) in {(t, b) for t, b, _ in res[f][1]}, (kind, f, res[f][1])
         seen |= {(kind, br)}
         # the R-table loops stay clear in every construction
         for name, (q, ev) in res.items():
@@ -124,7 +125,7 @@ def test_verify_constructions():
         assert 0 < s <= M.N // 2
         u1, u2 = z * pow(s, -1, M.N) % M.N, r * pow(s, -1, M.N) % M.N
         br = "dbl" if sign == 1 else "inf"
-        form = {"ls": M.lane_serial, "join": M.narrow, "split1": M.windowed, "split2": M.windowed}[kind]
+        form = {"ls": M.lane_serial, "join": M.narrow, "split1": M.split, "split2": M.split}[kind]
         q, ev = form(u2, u1, rho)
         tag = "ls" if kind == "ls" else "join"
         assert (tag, br) in {(t, b) for t, b, _ in ev}, (kind, ev)

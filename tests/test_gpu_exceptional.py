@@ -102,7 +102,7 @@ def test_recover_exceptional_sums_every_form(engine, oracle):
             # window 0: the u1 G addition meets u2 R == +-u1 G, the wave redoes its loop exactly
             assert d["ls_redo"] > 0 and d["ls_exc"] > 0, d
         elif form == "mid":
-            # the split1 / split2 constructions meet the windowed form's joins ((A + u1 G) + H)
+            # the split1 / split2 constructions meet the windowed form's joins ((A + u1 G) + H, as split)
             assert d["mid_join"] > 0 and d["mid_redo"] == 0 and d["mid_exc"] == 0, d
         elif form == "mid_bucket":
             # the ls / join constructions (u2 R == +-u1 G) meet the bucket form's final join
@@ -110,8 +110,8 @@ def test_recover_exceptional_sums_every_form(engine, oracle):
         else:
             assert d["join_dbl"] > 0 and d["join_inf"] > 0, (form, d)
             assert d["lat_redo"] == 0 and d["comb_redo"] == 0 and d["lat_exc"] == 0, (form, d)
-    # kinds split1 / split2 target the windowed form's join order (ecmodel.windowed); the latency
-    # split and three-wave forms join (A + H) + u1 G and meet the "join" kind's branches
+    # kinds split1 / split2 target the split (and windowed) form's joins; the three-wave form joins
+    # (A + H) + u1 G and meets the "join" kind's branches
     assert {"ls", "join", "split1", "split2"} == set(kinds.tolist())
 
 
