@@ -79,7 +79,7 @@ SIGNATURES = {
 
 # EGES_DIAG_* (include/eges.h): rare exact branches the kernels count
 DIAG_NAMES = ["ls_redo", "ls_exc", "lat_redo", "lat_exc", "comb_redo", "join_dbl", "join_inf", "mid_redo",
-              "mid_exc", "mid_join", "handoff", "lat_tri"]
+              "mid_exc", "mid_join", "handoff", "lat_tri", "resident"]
 ENGINE_FAULT = 255  # EGES_ENGINE_FAULT: an item whose in-kernel wave hand-off timed out
 DIAG_COUNT = 16
 

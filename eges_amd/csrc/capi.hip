@@ -79,6 +79,9 @@ int env_int(const char* name, int dflt) {
 constexpr int NLANES = 4;
 struct Lane {
   std::mutex mu;
+  // the resident server runs on lane 0's stream (its persistent kernel holds that stream's
+  // hardware queue): while it does, lane 0 takes no calls
+  std::atomic<bool> reserved{false};
   hipStream_t stream = nullptr;
   uint8_t* buf = nullptr;
   size_t buf_cap = 0;
@@ -86,6 +89,22 @@ struct Lane {
   hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_k[2] = {nullptr, nullptr};
 };
 
+// Resident single-call server of a device (k_recover_lat.hip lat_resident_kernel): a few
+// split-form workgroups polling a job word in coherent pinned memory (resident_run below).
+struct Resident {
+  std::mutex mu;  // one job at a time; a group that finds it busy takes a lane instead
+  bool block = false;  // the block server (narrow form, lane 1) or the single-call one (split, lane 0)
+  int lane = 0;
+  hipStream_t stream = nullptr;
+  ResidentJob* job = nullptr;  // coherent pinned
+  uint8_t* data = nullptr;     // coherent pinned, resident_layout / resident_block_layout (cap)
+  uint32_t* counter = nullptr;  // device, 2 words
+  uint32_t* scratch = nullptr;  // block server: record / root rows (device)
+  uint32_t cap = 0, wgs = 0;
+  bool running = false;  // (guarded by mu; while true, the stream's lane is reserved)
+  uint32_t seq = 0;  // the last job handed over (== job->done once served)
+  std::chrono::steady_clock::time_point last_use{};
+};
 struct Dev {
   int id = -1;
   int cus = 0;
@@ -112,6 +131,11 @@ struct Dev {
   size_t ring_cap = 0;
   std::mutex mu;
   Lane lanes[NLANES];
+  Resident res, res_blk;
+  Dev() {
+    res_blk.block = true;
+    res_blk.lane = 1;
+  }
   ~Dev();
 };
 using DevPtr = std::shared_ptr<Dev>;
@@ -161,6 +185,12 @@ const KnobDef KNOB_DEFS[KNOB_COUNT] = {
     {"EGES_TEST_SKIP_FLAG", 0},
     {"EGES_TEST_DELAY_X", 0},
     {"EGES_HOST_STREAMS", 1},
+    {"EGES_RESIDENT", 1},
+    {"EGES_RESIDENT_WGS", 16},
+    {"EGES_RESIDENT_CAP", 64},
+    {"EGES_RESIDENT_IDLE_MS", 4},
+    {"EGES_RESIDENT_BLOCK", 0},
+    {"EGES_RESIDENT_BLOCK_CAP", 1024},
 };
 std::atomic<long long> g_knob[KNOB_COUNT];
 std::once_flag g_knob_once;
@@ -310,8 +340,16 @@ int init_device(int id, DevPtr* out) {
 
 // Resources go when the last reference does: eges_shutdown drops the registry's references,
 // and a call still in flight keeps its device alive until it returns.
+void resident_stop(Dev& d);
 Dev::~Dev() {
   DevGuard g(id);
+  resident_stop(*this);  // (their streams are lanes 0 and 1's)
+  for (Resident* r : {&res, &res_blk}) {
+    if (r->job) (void)hipHostFree(r->job);
+    if (r->data) (void)hipHostFree(r->data);
+    if (r->counter) (void)hipFree(r->counter);
+    if (r->scratch) (void)hipFree(r->scratch);
+  }
   if (stream) (void)hipStreamSynchronize(stream);
   if (last) (void)hipEventSynchronize(last);  // the last engine work, on whichever stream the caller gave
   if (gtab) (void)hipFree(gtab);
@@ -727,8 +765,16 @@ Region region_for(const HostJob& j, size_t base, size_t m) {
 // i-1's outputs (host order H2D(i+1), K(i+1), D2H(i): the pageable D2H blocks this thread
 // until K(i) is done, by which time K(i+1) is queued behind it). Synchronous overall.
 int run_host_pipe(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t cnt);
+int resident_block_run(Dev& d, const HostJob& j, size_t off, size_t n);
 int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t cnt) {
   HSTAMP(0);
+  // blocks for the latency kernel's narrow form (above the three-wave form's range): the resident
+  // block server, when it is on and free (no launch, dispatch or completion signal per block)
+  if ((j.kind == HostJob::RECOVER || j.kind == HostJob::SENDER) && cnt <= rt.lat_max &&
+      cnt > std::max<size_t>(rt.wide_max, rt.tri_max)) {
+    const int rc = resident_block_run(d, j, off, cnt);
+    if (rc >= 0) return rc;
+  }
   // (EGES_HOST_PIPE = 2: tests force the pipeline for any batch larger than its first chunk)
   if (j.kind != HostJob::SENDER_RAW &&
       ((rt.host_pipe == 1 && cnt >= 2 * PIPE_MIN) || (rt.host_pipe == 2 && cnt > rt.pipe_first)))
@@ -750,18 +796,22 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   if (small) {
     for (Lane& l : d.lanes) {
       std::unique_lock<std::mutex> t(l.mu, std::try_to_lock);
-      if (t.owns_lock()) {
+      if (t.owns_lock() && !l.reserved.load(std::memory_order_acquire)) {
         lane = &l;
         lk = std::move(t);
         break;
       }
     }
-    if (!lane) {
+    while (!lane) {
       static std::atomic<unsigned> rr{0};
-      lane = &d.lanes[rr++ % NLANES];
-      lk = std::unique_lock<std::mutex>(lane->mu);
+      Lane& l = d.lanes[rr++ % NLANES];
+      std::unique_lock<std::mutex> t(l.mu);
+      if (l.reserved.load(std::memory_order_acquire)) continue;  // (the resident server's)
+      lane = &l;
+      lk = std::move(t);
     }
   } else {
+    resident_stop(d);  // device-wide work: the resident server leaves the CUs first
     lk = std::unique_lock<std::mutex>(d.mu);
   }
   uint8_t*& dbuf = small ? lane->buf : d.buf;
@@ -1159,6 +1209,7 @@ struct PipeArr {
 };
 int run_host_pipe(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t cnt) {
   DevGuard g(d.id);
+  resident_stop(d);
   std::unique_lock<std::mutex> lk(d.mu);
   // chunk schedule: a smaller first chunk, then near-equal chunks of at most rt.pipe_chunk
   std::vector<std::pair<size_t, size_t>> ch;
@@ -1545,8 +1596,191 @@ struct VerifyReq {
   std::atomic<bool> queued{false};
 };
 
+// ------------------------------------------------------------------ resident single-call server
+// Stops the device's resident server (before device-wide work, which it would otherwise share the
+// CUs with, and at teardown): the stop word, then its stream drains.
+void resident_halt(Dev& d, Resident& r) {  // r.mu held
+  if (!r.running) return;
+  DevGuard g(d.id);
+  __atomic_store_n(&r.job->stop, 1u, __ATOMIC_RELEASE);
+  (void)hipStreamSynchronize(r.stream);
+  __atomic_store_n(&r.job->stop, 0u, __ATOMIC_RELEASE);
+  r.running = false;
+  d.lanes[r.lane].reserved.store(false, std::memory_order_release);
+}
+void resident_stop(Dev& d) {
+  for (Resident* r : {&d.res, &d.res_blk}) {
+    std::lock_guard<std::mutex> lk(r->mu);
+    resident_halt(d, *r);
+  }
+}
+
+// One job on the resident server of device d: fill(data, layout) writes the inputs, read(...)
+// takes the outputs. Returns -1 when the server is off, busy or the group too large (the caller
+// takes a lane), else an EGES status.
+// the block server's cap: its grid (helpers + one workgroup per item, two waves each) must stay
+// within half the device's wave slots at the narrow form's occupancy (3 per SIMD)
+uint32_t resident_cap(const Dev& d, bool block) {
+  if (!block) return (uint32_t)std::max<long long>(1, std::min<long long>(knob(KNOB_RESIDENT_CAP), 4096));
+  const long long slots = (long long)d.cus * 4 * 3 / 2 / 2;  // workgroups of two waves in half the slots
+  return (uint32_t)std::max<long long>(64, std::min<long long>(knob(KNOB_RESIDENT_BLOCK_CAP), slots - 16));
+}
+template <class Fill, class Read>
+int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& read) {
+  if (knob(r.block ? KNOB_RESIDENT_BLOCK : KNOB_RESIDENT) == 0 || n == 0) return -1;
+  // the test-only knobs act on launches: their runs take the lanes
+  if (knob(KNOB_FORCE_REDO) != 0 || knob(KNOB_TEST_SKIP_FLAG) != 0 || knob(KNOB_ROOT_HELPERS) == 0) return -1;
+  const uint32_t cap = resident_cap(d, r.block);
+  if (n > cap) return -1;
+  std::unique_lock<std::mutex> lk(r.mu, std::try_to_lock);
+  if (!lk.owns_lock()) return -1;
+  DevGuard g(d.id);
+  if (!r.job || r.cap < cap) {
+    if (r.running) return -1;  // (a knob raised while it runs: the lanes until it exits)
+    r.stream = d.lanes[r.lane].stream;
+    if (!r.job) {
+      if (hipHostMalloc(&r.job, 4096, hipHostMallocCoherent) != hipSuccess) return set_err(EGES_E_NOMEM, "hipHostMalloc(job)");
+      std::memset(r.job, 0, 4096);
+      HIPCHK(hipMalloc(&r.counter, 64));
+    }
+    if (r.data) (void)hipHostFree(r.data);
+    r.data = nullptr;
+    const size_t bytes = r.block ? resident_block_layout(cap).total : resident_layout(cap).total;
+    if (hipHostMalloc(&r.data, bytes, hipHostMallocCoherent) != hipSuccess)
+      return set_err(EGES_E_NOMEM, "hipHostMalloc(resident data)");
+    if (r.block) {
+      if (r.scratch) (void)hipFree(r.scratch);
+      HIPCHK(hipMalloc(&r.scratch, recover_scratch_bytes((cap + 63) / 64 * 64)));
+    }
+    r.cap = cap;
+  }
+  const long long idle_ms = std::max<long long>(1, knob(KNOB_RESIDENT_IDLE_MS));
+  const auto now = std::chrono::steady_clock::now();
+  // a server idle for half its bound may be deciding to exit: restart it rather than race it
+  if (r.running && (hipStreamQuery(r.stream) == hipSuccess ||
+                    now - r.last_use > std::chrono::microseconds(idle_ms * 500)))
+    resident_halt(d, r);
+  auto launch = [&]() -> int {
+    if (!r.running) {  // the lane finishes what it runs and takes no more calls
+      std::lock_guard<std::mutex> l0(d.lanes[r.lane].mu);
+      d.lanes[r.lane].reserved.store(true, std::memory_order_release);
+    }
+    HIPCHK(hipMemsetAsync(r.counter, 0, 64, r.stream));
+    ResidentParams rp{r.job, r.data, r.scratch, r.cap, __atomic_load_n(&r.job->done, __ATOMIC_ACQUIRE), r.counter,
+                      (uint64_t)idle_ms * 100000ull, d.gtab, d.diag};
+    r.wgs = (uint32_t)std::max<long long>(1, std::min<long long>(knob(KNOB_RESIDENT_WGS), 1024));
+    const hipError_t e = r.block ? launch_lat_resident_block(rp, r.stream) : launch_lat_resident(rp, r.wgs, r.stream);
+    if (e != hipSuccess) {
+      r.running = false;
+      d.lanes[r.lane].reserved.store(false, std::memory_order_release);
+      return set_err(EGES_E_HIP, "resident server launch failed");
+    }
+    r.running = true;
+    return EGES_SUCCESS;
+  };
+  if (!r.running) {
+    const int rc = launch();
+    if (rc) return rc;
+  }
+  fill(r.data, r.job);
+  __atomic_store_n(&r.job->n, (uint32_t)n, __ATOMIC_RELAXED);
+  __atomic_store_n(&r.job->kind, (uint32_t)kind, __ATOMIC_RELAXED);
+  const uint32_t seq = ++r.seq;
+  __atomic_store_n(&r.job->seq, seq, __ATOMIC_RELEASE);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t spins = 0; __atomic_load_n(&r.job->done, __ATOMIC_ACQUIRE) != seq; ++spins) {
+    cpu_relax();
+    if ((spins & 1023) != 1023) continue;
+    if (hipStreamQuery(r.stream) == hipSuccess && __atomic_load_n(&r.job->done, __ATOMIC_ACQUIRE) != seq) {
+      // the server exited without taking the job (its idle bound): a fresh one takes it (lane 0
+      // stays reserved in between)
+      const int rc = launch();
+      if (rc) return rc;
+    }
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+      resident_halt(d, r);
+      return set_err(EGES_E_HIP, "resident server: job %u not served within 2 s", seq);
+    }
+  }
+  read(r.data);
+  r.last_use = std::chrono::steady_clock::now();
+  return EGES_SUCCESS;
+}
+// A host-buffer block (ecrecover or types.Sender rows) on the resident block server; -1: not taken.
+int resident_block_run(Dev& d, const HostJob& j, size_t off, size_t n) {
+  const ResidentBlockLayout L = resident_block_layout(resident_cap(d, true));
+  const bool snd = j.kind == HostJob::SENDER;
+  bool fault = false;
+  const int rc = resident_job(
+      d, d.res_blk, snd ? RESIDENT_SENDER : RESIDENT_RECOVER, n,
+      [&](uint8_t* D, ResidentJob* job) {
+        if (snd) {
+          std::memcpy(D + L.sh, j.a + off * 32, n * 32);
+          std::memcpy(D + L.sr, j.b + off * 32, n * 32);
+          std::memcpy(D + L.ss, j.c + off * 32, n * 32);
+          std::memcpy(D + L.sv, j.d + off * 32, n * 32);
+          if (j.e) std::memcpy(D + L.sf, j.e + off, n);
+          else std::memset(D + L.sf, 0, n);
+          job->signer = (uint32_t)j.signer;
+          job->chain_id = j.chain_id;
+        } else {
+          std::memcpy(D + L.msg, j.a + off * 32, n * 32);
+          std::memcpy(D + L.sig, j.b + off * 65, n * 65);
+          job->want = (j.pub ? 1u : 0u) | (j.addr ? 2u : 0u);
+        }
+      },
+      [&](const uint8_t* D) {
+        const uint8_t* st = D + (snd ? L.sstatus : L.status);
+        if (j.status) std::memcpy(j.status + off, st, n);
+        fault = std::memchr(st, EGES_ENGINE_FAULT, n) != nullptr;
+        if (snd) {
+          if (j.addr) std::memcpy(j.addr + off * 20, D + L.saddr, n * 20);
+        } else {
+          if (j.pub) std::memcpy(j.pub + off * 65, D + L.pub, n * 65);
+          if (j.addr) std::memcpy(j.addr + off * 20, D + L.addr, n * 20);
+        }
+      });
+  if (rc == EGES_SUCCESS && fault)
+    return set_err(EGES_E_HIP, "a kernel hand-off timed out (EGES_ENGINE_FAULT items; EGES_DIAG_HANDOFF)");
+  return rc;
+}
+DevPtr first_dev() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return g_devs.empty() ? nullptr : g_devs[0];
+}
+
 void run_group(std::vector<RecoverReq*>& g) {
   const size_t n = g.size();
+  if (ensure_init() == EGES_SUCCESS) {
+    if (DevPtr d = first_dev()) {
+      const ResidentLayout L = resident_layout(resident_cap(*d, false));
+      const int rc = resident_job(
+          *d, d->res, RESIDENT_RECOVER, n,
+          [&](uint8_t* D, ResidentJob*) {
+            for (size_t i = 0; i < n; ++i) {
+              std::memcpy(D + L.msg + i * 32, g[i]->msg, 32);
+              std::memcpy(D + L.sig + i * 65, g[i]->sig, 65);
+            }
+          },
+          [&](const uint8_t* D) {
+            bool fault = false;
+            for (size_t i = 0; i < n; ++i) fault = fault || D[L.status + i] == EGES_ENGINE_FAULT;
+            const int rc2 = fault ? set_err(EGES_E_HIP, "a kernel hand-off timed out (EGES_ENGINE_FAULT items)") : EGES_SUCCESS;
+            for (size_t i = 0; i < n; ++i) {
+              const bool ok = rc2 == EGES_SUCCESS && D[L.status + i] == EGES_OK;
+              if (ok) std::memcpy(g[i]->pub, D + L.pub + i * 65, 65);
+              g[i]->result = ok ? 1 : 0;
+              g[i]->rc = rc2;
+              if (rc2) g[i]->err = t_err;
+            }
+          });
+      if (rc >= 0) {
+        if (rc)
+          for (RecoverReq* q : g) q->result = 0, q->rc = rc, q->err = t_err;
+        return;
+      }
+    }
+  }
   std::vector<uint8_t> msg(n * 32), sig(n * 65), pub(n * 65), st(n);
   for (size_t i = 0; i < n; ++i) {
     std::memcpy(&msg[i * 32], g[i]->msg, 32);
@@ -1563,6 +1797,37 @@ void run_group(std::vector<RecoverReq*>& g) {
 }
 void run_group(std::vector<VerifyReq*>& g) {
   const size_t n = g.size();
+  if (ensure_init() == EGES_SUCCESS) {
+    if (DevPtr d = first_dev()) {
+      const ResidentLayout L = resident_layout(resident_cap(*d, false));
+      const int rc = resident_job(
+          *d, d->res, RESIDENT_VERIFY, n,
+          [&](uint8_t* D, ResidentJob*) {
+            for (size_t i = 0; i < n; ++i) {
+              std::memset(D + L.vpub + i * 65, 0, 65);
+              std::memcpy(D + L.vpub + i * 65, g[i]->pub, g[i]->publen);
+              D[L.vpublen + i] = g[i]->publen;
+              std::memcpy(D + L.vmsg + i * 32, g[i]->msg, 32);
+              std::memcpy(D + L.vsig + i * 64, g[i]->sig, 64);
+            }
+          },
+          [&](const uint8_t* D) {
+            bool fault = false;
+            for (size_t i = 0; i < n; ++i) fault = fault || D[L.vok + i] == EGES_ENGINE_FAULT;
+            const int rc2 = fault ? set_err(EGES_E_HIP, "a kernel hand-off timed out (EGES_ENGINE_FAULT items)") : EGES_SUCCESS;
+            for (size_t i = 0; i < n; ++i) {
+              g[i]->result = (rc2 == EGES_SUCCESS && D[L.vok + i] == 1) ? 1 : 0;
+              g[i]->rc = rc2;
+              if (rc2) g[i]->err = t_err;
+            }
+          });
+      if (rc >= 0) {
+        if (rc)
+          for (VerifyReq* q : g) q->result = 0, q->rc = rc, q->err = t_err;
+        return;
+      }
+    }
+  }
   std::vector<uint8_t> pub(n * 65, 0), publen(n), msg(n * 32), sig(n * 64), ok(n);
   for (size_t i = 0; i < n; ++i) {
     std::memcpy(&pub[i * 65], g[i]->pub, g[i]->publen);
@@ -1720,6 +1985,7 @@ void eges_shutdown(void) {
   }
   // each device is released once its in-flight calls (which hold references) have returned
   for (DevPtr& d : devs) {
+    resident_stop(*d);
     { std::lock_guard<std::mutex> dl(d->mu); }
     d.reset();
   }
@@ -1888,6 +2154,7 @@ int eges_ecrecover_batch_dev(int device, const uint8_t* msg, const uint8_t* sig,
   if (rc) return rc;
   DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
+  resident_stop(*d);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
   return run_recover_dev(*d, Route::now(), msg, sig, n, pub_out, addr_out, status, (hipStream_t)stream);
@@ -1903,6 +2170,7 @@ int eges_sender_batch_dev(int device, const uint8_t* sighash, const uint8_t* r, 
   if (rc) return rc;
   DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
+  resident_stop(*d);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
   return run_sender_dev(*d, Route::now(), sighash, r, s, v, vflags, n, signer, chain_id, addr_out, status,
@@ -1919,6 +2187,7 @@ int eges_sender_raw_batch_dev(int device, const uint8_t* raw, const uint64_t* of
   if (rc) return rc;
   DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
+  resident_stop(*d);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
   return run_sender_raw_dev(*d, Route::now(), raw, offsets, n, signer, chain_id, addr_out, status, sighash_out,
@@ -1933,6 +2202,7 @@ int eges_ecrecover_precompile_batch_dev(int device, const uint8_t* input, const 
   if (rc) return rc;
   DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
+  resident_stop(*d);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
   return run_precompile_dev(*d, Route::now(), input, inlen, n, out32, status, (hipStream_t)stream);
@@ -1946,6 +2216,7 @@ int eges_verify_batch_dev(int device, const uint8_t* pub, const uint8_t* publen,
   if (rc) return rc;
   DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
+  resident_stop(*d);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
   return run_verify_dev(*d, Route::now(), pub, publen, msg, sig, n, ok_out, (hipStream_t)stream);
@@ -1957,6 +2228,7 @@ static int synth_common(int device, uint64_t first_index, size_t n, const uint8_
   if (rc) return rc;
   DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
+  resident_stop(*d);
   std::lock_guard<std::mutex> lk(d->mu);
   DevGuard g(device);
   hipStream_t st = (hipStream_t)stream;

@@ -832,18 +832,25 @@ DEV uint32_t hw_place() {
 // y and u1 G; waves 2 and 3 the high windows of the two GLV halves against their own table of
 // D = 2^75 R'; wave 0 the low windows of both halves, then joins the three partial sums.
 template <class ST, int FORM>
+DEV void recover_lat_item(const RecoverParams& prm, uint32_t idx, LatLds& S, uint64_t* stamps);
+template <class ST, int FORM>
 DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
-  constexpr bool SPLIT = FORM == FORM_SPLIT;   // four waves, wave 1 computes y
-  constexpr bool FLAGS = FORM != FORM_NARROW;  // LDS flag hand-offs instead of barriers
+  constexpr bool SPLIT = FORM == FORM_SPLIT;
   __shared__ LatLds S;
-  ST st_;
-  ST* st = &st_;
-  const Diag dg = diag_of(prm);
   if (!SPLIT && blockIdx.x < prm.n_helpers) {  // narrow / three-wave forms: the lane-serial roots
     root_helper(prm);
     return;
   }
-  const uint32_t idx = blockIdx.x - (SPLIT ? 0u : prm.n_helpers);  // every wave has a signature
+  recover_lat_item<ST, FORM>(prm, blockIdx.x - (SPLIT ? 0u : prm.n_helpers), S, stamps);  // a signature per workgroup
+}
+// signature idx on this workgroup (all its waves enter; each returns when its part is done)
+template <class ST, int FORM>
+DEV void recover_lat_item(const RecoverParams& prm, uint32_t idx, LatLds& S, uint64_t* stamps) {
+  constexpr bool SPLIT = FORM == FORM_SPLIT;   // four waves, wave 1 computes y
+  constexpr bool FLAGS = FORM != FORM_NARROW;  // LDS flag hand-offs instead of barriers
+  ST st_;
+  ST* st = &st_;
+  const Diag dg = diag_of(prm);
   // the helpers' lane-serial roots are a dense VALU stream: the signature waves (latency-bound
   // chains) take issue priority over them on a shared SIMD
   if (!SPLIT) __builtin_amdgcn_s_setprio(2);
@@ -994,14 +1001,19 @@ DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
 // (the square root for 33-byte keys, the curve equation for 65-byte ones); then Q = u2 P + u1 G
 // and x(Q) == r checked projectively (r Z^2 == X), no field inversion.
 template <bool SPLIT>
+DEV void verify_lat_item(const VerifyParams& prm, uint32_t idx, LatLds& S);
+template <bool SPLIT>
 DEV void verify_lat_body(const VerifyParams& prm) {
   __shared__ LatLds S;
+  verify_lat_item<SPLIT>(prm, blockIdx.x, S);  // grid = n
+}
+template <bool SPLIT>
+DEV void verify_lat_item(const VerifyParams& prm, uint32_t idx, LatLds& S) {
   NoStamp st_;
   const Diag dg = diag_of(prm);
-  const uint32_t idx = blockIdx.x;  // grid = n
   if (SPLIT) {
     if (threadIdx.x < NFLAGS) S.flag[threadIdx.x] = 0u;
-    if (threadIdx.x == 0) S.skip = blockIdx.x == prm.test_skip_block ? prm.test_skip_flag : 0u;
+    if (threadIdx.x == 0) S.skip = idx == prm.test_skip_block ? prm.test_skip_flag : 0u;
     __syncthreads();  // the only barrier of the split form
   }
   uint32_t l[8];
@@ -1120,6 +1132,166 @@ hipError_t launch_recover_lat(const RecoverParams& p0, hipStream_t st) {
   else if (p.wide == FORM_TRI)
     hipLaunchKernelGGL(recover_lat_tri_kernel, dim3(p.n_helpers + p.n), dim3(LAT_WG_TRI), 0, st, p);
   else hipLaunchKernelGGL(recover_lat_kernel, dim3(p.n_helpers + p.n), dim3(LAT_WG), 0, st, p);
+  return hipGetLastError();
+}
+
+// ---- resident single-call server (launch.h ResidentParams). Every workgroup polls the job word
+// (thread 0, system-scope acquire, s_sleep between polls), takes items blockIdx.x, + gridDim.x, ...
+// of a job through the split form, and counts itself done; the last one stores the job's sequence
+// into `done` after every workgroup's outputs (each releases at system scope before its count).
+// Exits on the stop word or after idle_ticks without a job (the host restarts it on demand and
+// never hands a job to a server older than half that: capi.hip Resident).
+__global__ void __launch_bounds__(LAT_WG_SPLIT) lat_resident_kernel(ResidentParams rp) {
+  __shared__ LatLds S;
+  __shared__ uint32_t jseq, jn, jkind, jexit;
+  uint32_t seen = rp.seen0;
+  uint64_t last = __builtin_amdgcn_s_memrealtime();
+#pragma unroll 1
+  for (;;) {
+    if (threadIdx.x == 0) {
+      uint32_t q = seen, stop = 0;
+#pragma unroll 1
+      for (;;) {
+        q = __hip_atomic_load(&rp.job->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        stop = __hip_atomic_load(&rp.job->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (stop || q != seen) break;
+        if (__builtin_amdgcn_s_memrealtime() - last > rp.idle_ticks) break;
+        __builtin_amdgcn_s_sleep(8);
+      }
+      jexit = (stop || q == seen) ? 1u : 0u;
+      jseq = q;
+      jn = __hip_atomic_load(&rp.job->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      jkind = __hip_atomic_load(&rp.job->kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __syncthreads();
+    if (jexit) return;
+    const uint32_t seq = jseq, n = jn < rp.cap ? jn : rp.cap, kind = jkind;
+    const ResidentLayout L = resident_layout(rp.cap);
+#pragma unroll 1
+    for (uint32_t idx = blockIdx.x; idx < n; idx += gridDim.x) {
+      if (kind == RESIDENT_RECOVER) {
+        RecoverParams p{nullptr, n, n, rp.data + L.status, nullptr, rp.data + L.pub, rp.gtab, nullptr};
+        p.raw_msg = rp.data + L.msg;
+        p.raw_sig = rp.data + L.sig;
+        p.wide = FORM_SPLIT;
+        p.diag = rp.diag;
+        recover_lat_item<NoStamp, FORM_SPLIT>(p, idx, S, nullptr);
+      } else {
+        VerifyParams v{rp.data + L.vpub, rp.data + L.vpublen, rp.data + L.vmsg, rp.data + L.vsig, n,
+                       rp.data + L.vok, rp.gtab, nullptr};
+        v.diag = rp.diag;
+        verify_lat_item<true>(v, idx, S);
+      }
+      __syncthreads();  // every wave done with this item's LDS
+    }
+    if (threadIdx.x == 0) {
+      if (blockIdx.x == 0 && rp.diag) __hip_atomic_fetch_add(rp.diag + EGES_DIAG_RESIDENT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this workgroup's outputs (thread 0 wrote them), system scope
+      const uint32_t c = __hip_atomic_fetch_add(&rp.counter[seq & 1u], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (c == gridDim.x - 1) {
+        __hip_atomic_store(&rp.counter[seq & 1u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&rp.job->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    seen = seq;
+    last = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();  // (jseq / jn / jkind are rewritten by the next poll)
+  }
+}
+hipError_t launch_lat_resident(const ResidentParams& p, uint32_t wgs, hipStream_t st) {
+  hipLaunchKernelGGL(lat_resident_kernel, dim3(wgs), dim3(LAT_WG_SPLIT), 0, st, p);
+  return hipGetLastError();
+}
+
+// The block server (blocks of EGES_LAT_TRI_MAX + 1 ... cap items, ecrecover or types.Sender
+// rows): the narrow form's launch kept resident. The first ceil(cap / 128) workgroups are the
+// root helpers (their lanes take items j < n), then one workgroup per item; each job's epoch is
+// its sequence number, so root words of an earlier job never match.
+__global__ void __launch_bounds__(LAT_WG, 3) lat_resident_block_kernel(ResidentParams rp) {
+  __shared__ LatLds S;
+  __shared__ uint32_t jseq, jn, jkind, jexit, jsigner, jwant;
+  __shared__ uint64_t jcid;
+  __shared__ __attribute__((aligned(16))) unsigned char jp_raw[sizeof(RecoverParams)];
+  RecoverParams& jp = *reinterpret_cast<RecoverParams*>(jp_raw);
+  const uint32_t H = resident_block_helpers(rp.cap), n_pad = (rp.cap + 63) / 64 * 64;
+  uint32_t seen = rp.seen0;
+  uint64_t last = __builtin_amdgcn_s_memrealtime();
+#pragma unroll 1
+  for (;;) {
+    if (threadIdx.x == 0) {
+      uint32_t q = seen, stop = 0;
+#pragma unroll 1
+      for (;;) {
+        q = __hip_atomic_load(&rp.job->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        stop = __hip_atomic_load(&rp.job->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (stop || q != seen) break;
+        if (__builtin_amdgcn_s_memrealtime() - last > rp.idle_ticks) break;
+        __builtin_amdgcn_s_sleep(8);
+      }
+      jexit = (stop || q == seen) ? 1u : 0u;
+      jseq = q;
+      jn = __hip_atomic_load(&rp.job->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      jkind = __hip_atomic_load(&rp.job->kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      jsigner = __hip_atomic_load(&rp.job->signer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      jwant = __hip_atomic_load(&rp.job->want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      jcid = __hip_atomic_load(&rp.job->chain_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __syncthreads();
+    if (jexit) return;
+    const uint32_t seq = jseq, n = jn < rp.cap ? jn : rp.cap;
+    // the job's parameters in LDS (read where the item needs them, as a kernel's would be from
+    // its argument segment; a register copy pushed the kernel past 168 VGPRs)
+    if (threadIdx.x == 0) {
+    const ResidentBlockLayout L = resident_block_layout(rp.cap);
+    RecoverParams& p = jp;
+    p = RecoverParams{rp.scratch, n, n_pad, nullptr, nullptr, nullptr, rp.gtab, nullptr};
+    if (jkind == RESIDENT_SENDER) {
+      p.status = rp.data + L.sstatus;
+      p.addr = rp.data + L.saddr;
+      p.snd_h = rp.data + L.sh;
+      p.snd_r = rp.data + L.sr;
+      p.snd_s = rp.data + L.ss;
+      p.snd_v = rp.data + L.sv;
+      p.snd_f = rp.data + L.sf;
+      p.snd_signer = (int)jsigner;
+      p.snd_chain_id = jcid;
+    } else {
+      p.status = rp.data + L.status;
+      p.addr = (jwant & 2u) ? rp.data + L.addr : nullptr;
+      p.pub = (jwant & 1u) ? rp.data + L.pub : nullptr;
+      p.raw_msg = rp.data + L.msg;
+      p.raw_sig = rp.data + L.sig;
+    }
+    p.wide = FORM_NARROW;
+    p.n_helpers = H;
+    p.epoch = seq;
+    p.diag = rp.diag;
+    }
+    __syncthreads();
+    if (blockIdx.x < H) {
+      root_helper(jp);
+    } else if (blockIdx.x - H < n) {
+      recover_lat_item<NoStamp, FORM_NARROW>(jp, blockIdx.x - H, S, nullptr);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (blockIdx.x == 0 && rp.diag) __hip_atomic_fetch_add(rp.diag + EGES_DIAG_RESIDENT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this workgroup's outputs (thread 0 wrote them), system scope
+      const uint32_t c = __hip_atomic_fetch_add(&rp.counter[seq & 1u], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (c == gridDim.x - 1) {
+        __hip_atomic_store(&rp.counter[seq & 1u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&rp.job->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    seen = seq;
+    last = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+  }
+}
+hipError_t launch_lat_resident_block(const ResidentParams& p, hipStream_t st) {
+  const uint32_t grid = resident_block_helpers(p.cap) + p.cap;
+  hipLaunchKernelGGL(lat_resident_block_kernel, dim3(grid), dim3(LAT_WG), 0, st, p);
   return hipGetLastError();
 }
 

@@ -42,6 +42,12 @@ enum KnobId : int {
   KNOB_TEST_DELAY_X,      // tests: the bucket form's wave X sleeps k x ~3 us before it reads its
                           //   workgroup's wire stage (the stage / part[0] release)
   KNOB_HOST_STREAMS,      // the chunked host path's kernels on 1 (default) or 2 alternating compute streams
+  KNOB_RESIDENT,          // 1: coalesced single calls go to the resident server (capi.hip Resident)
+  KNOB_RESIDENT_WGS,      //   its workgroups (split form, four waves each)
+  KNOB_RESIDENT_CAP,      //   the largest group it takes (larger groups launch on a lane)
+  KNOB_RESIDENT_IDLE_MS,  //   it exits after this long without a job (restarted on demand)
+  KNOB_RESIDENT_BLOCK,    // 1: latency-kernel blocks above LAT_TRI_MAX go to the resident block server
+  KNOB_RESIDENT_BLOCK_CAP,  //   its largest block (and grid: helpers + one workgroup per item)
   KNOB_COUNT
 };
 

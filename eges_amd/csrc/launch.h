@@ -149,6 +149,87 @@ hipError_t launch_verify_mid(const VerifyParams& p, hipStream_t st);
 // one item per 128-thread workgroup (k_recover_lat.hip; wide: 192 threads, three partial sums);
 // uses pub/publen/msg/sig/n/ok/gtab only
 hipError_t launch_verify_lat(const VerifyParams& p, bool wide, hipStream_t st);
+
+// ---- resident single-call server (k_recover_lat.hip lat_resident_kernel; capi.hip Resident).
+// A few split-form workgroups stay resident and poll a job word in coherent pinned host memory,
+// so a coalesced group of eges_ecdsa_recover / eges_ecdsa_verify calls pays no launch, dispatch or
+// completion signal (tools/resident_probe.cpp: 4.6 us round trip against 12 us for an empty
+// launch + stream sync).
+struct ResidentJob {  // coherent pinned host memory, 128 bytes
+  uint32_t seq;   // host: the job's sequence number, stored last (release)
+  uint32_t n;     // items (<= the server's cap)
+  uint32_t kind;  // RESIDENT_RECOVER / RESIDENT_VERIFY / RESIDENT_SENDER
+  uint32_t stop;  // host: exit now
+  uint32_t done;  // device: the last finished sequence, stored after every output (release)
+  uint32_t signer;     // RESIDENT_SENDER: types.Sender's signer and chain id
+  uint64_t chain_id;
+  uint32_t want;       // RESIDENT_RECOVER on the block server: bit 0 pub, bit 1 addr
+  uint32_t pad[23];
+};
+enum { RESIDENT_RECOVER = 0, RESIDENT_VERIFY = 1, RESIDENT_SENDER = 2 };
+// the data area (coherent pinned, cap items): recover msg | sig | pub | status; verify pub |
+// publen | msg | sig | ok (offsets from resident_layout)
+struct ResidentLayout {
+  size_t msg, sig, pub, status;        // recover
+  size_t vpub, vpublen, vmsg, vsig, vok;  // verify
+  size_t total;
+};
+__host__ __device__ inline ResidentLayout resident_layout(uint32_t cap) {
+  ResidentLayout L;
+  const size_t c = cap;
+  L.msg = 0;
+  L.sig = L.msg + c * 32;
+  L.pub = L.sig + c * 65;
+  L.status = L.pub + c * 65;
+  L.vpub = 0;
+  L.vpublen = L.vpub + c * 65;
+  L.vmsg = L.vpublen + c;
+  L.vsig = L.vmsg + c * 32;
+  L.vok = L.vsig + c * 64;
+  L.total = L.status + c > L.vok + c ? L.status + c : L.vok + c;
+  return L;
+}
+// the block server's data area (narrow form, blocks of up to cap items): recover msg | sig | pub |
+// addr | status; sender rows h | r | s | v | vflags | addr | status (4-byte aligned rows)
+struct ResidentBlockLayout {
+  size_t msg, sig, pub, addr, status;
+  size_t sh, sr, ss, sv, sf, saddr, sstatus;
+  size_t total;
+};
+__host__ __device__ inline ResidentBlockLayout resident_block_layout(uint32_t cap) {
+  ResidentBlockLayout L;
+  const size_t c = ((size_t)cap + 63) / 64 * 64;
+  L.msg = 0;
+  L.sig = L.msg + c * 32;
+  L.pub = L.sig + c * 65;
+  L.addr = L.pub + c * 65;
+  L.status = L.addr + c * 20;
+  L.sh = 0;
+  L.sr = L.sh + c * 32;
+  L.ss = L.sr + c * 32;
+  L.sv = L.ss + c * 32;
+  L.sf = L.sv + c * 32;
+  L.saddr = L.sf + c;
+  L.sstatus = L.saddr + c * 20;
+  const size_t a = L.status + c, b = L.sstatus + c;
+  L.total = a > b ? a : b;
+  return L;
+}
+struct ResidentParams {
+  ResidentJob* job;
+  uint8_t* data;
+  uint32_t* scratch;     // block server: the narrow form's record / root rows (n_pad = cap padded)
+  uint32_t cap;
+  uint32_t seen0;        // the last sequence finished before this launch
+  uint32_t* counter;     // device memory, 2 words, zero at launch
+  uint64_t idle_ticks;   // exit after this long without a job (s_memrealtime, 100 MHz)
+  const uint32_t* gtab;
+  uint32_t* diag;
+};
+hipError_t launch_lat_resident(const ResidentParams& p, uint32_t wgs, hipStream_t st);
+// the block server: ceil(cap / 128) root-helper workgroups, then cap narrow-form workgroups
+hipError_t launch_lat_resident_block(const ResidentParams& p, hipStream_t st);
+__host__ __device__ inline uint32_t resident_block_helpers(uint32_t cap) { return (cap + 127) / 128; }
 // Blocks the lane-serial kernels may need for a pass of n signatures at a resident grid of
 // max_blocks (grid_for_lane_serial: more than resident when n > max_blocks * WG * MAX_SLOTS).
 int lane_serial_grid(uint32_t n, int max_blocks);

@@ -224,6 +224,7 @@ int eges_synth_sign_msg_dev(int device, uint64_t first_index, size_t n, const ui
 #define EGES_DIAG_MID_JOIN 9  /* mid-size kernel: partial sums joined with a == +-b */
 #define EGES_DIAG_HANDOFF 10  /* a wave hand-off timed out: the workgroup's items got EGES_ENGINE_FAULT */
 #define EGES_DIAG_LAT_TRI 11  /* latency kernels: launches that ran the three-wave form */
+#define EGES_DIAG_RESIDENT 12 /* resident single-call server: jobs served */
 #define EGES_DIAG_COUNT 16
 /* Copies min(n, EGES_DIAG_COUNT) counters of `device` (summed over the engine's instances of
  * it) into out; reset != 0 zeroes them afterwards. Synchronises the device. */
