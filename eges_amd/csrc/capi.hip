@@ -103,6 +103,10 @@ struct Resident {
   uint32_t cap = 0, wgs = 0;
   bool running = false;  // (guarded by mu; while true, the stream's lane is reserved)
   uint32_t seq = 0;  // the last job handed over (== job->done once served)
+  uint32_t inst = 0;  // launches so far (each launch's id, nonzero)
+  // block server: the configuration its queued launches were made for (kind, outputs, signer, chain id)
+  uint32_t cfg_kind = ~0u, cfg_want = 0, cfg_signer = 0;
+  uint64_t cfg_cid = 0;
   std::chrono::steady_clock::time_point last_use{};
 };
 struct Dev {
@@ -1618,15 +1622,23 @@ void resident_stop(Dev& d) {
 // One job on the resident server of device d: fill(data, layout) writes the inputs, read(...)
 // takes the outputs. Returns -1 when the server is off, busy or the group too large (the caller
 // takes a lane), else an EGES status.
-// the block server's cap: its grid (helpers + one workgroup per item, two waves each) must stay
-// within half the device's wave slots at the narrow form's occupancy (3 per SIMD)
+// the block server's cap: its grid (helpers + one workgroup per item, two waves each) stays
+// within three quarters of the device's workgroup slots at the narrow form's occupancy (3 waves
+// per SIMD), so the single server and lane kernels still find room beside it
 uint32_t resident_cap(const Dev& d, bool block) {
   if (!block) return (uint32_t)std::max<long long>(1, std::min<long long>(knob(KNOB_RESIDENT_CAP), 4096));
-  const long long slots = (long long)d.cus * 4 * 3 / 2 / 2;  // workgroups of two waves in half the slots
-  return (uint32_t)std::max<long long>(64, std::min<long long>(knob(KNOB_RESIDENT_BLOCK_CAP), slots - 16));
+  const long long wg_slots = (long long)d.cus * 4 * 3 / 2;
+  return (uint32_t)std::max<long long>(64, std::min<long long>(knob(KNOB_RESIDENT_BLOCK_CAP), wg_slots * 3 / 4 - 16));
 }
+// base (block server only): fills the launch parameters of its kind / outputs / signer / chain
+// id from the server's buffers (called at each launch, after they exist); a job with others
+// first drains the queued launches. The single-call server is one launch that
+// loops over jobs; the block server is one launch per job, the next one enqueued (launch API
+// time overlapped with the GPU's work) while the current job runs, so one is always polling.
 template <class Fill, class Read>
-int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& read) {
+int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& read,
+                 const std::function<void(RecoverParams&)>* base = nullptr,
+                 uint32_t want = 0, uint32_t signer = 0, uint64_t cid = 0) {
   if (knob(r.block ? KNOB_RESIDENT_BLOCK : KNOB_RESIDENT) == 0 || n == 0) return -1;
   // the test-only knobs act on launches: their runs take the lanes
   if (knob(KNOB_FORCE_REDO) != 0 || knob(KNOB_TEST_SKIP_FLAG) != 0 || knob(KNOB_ROOT_HELPERS) == 0) return -1;
@@ -1641,12 +1653,17 @@ int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& re
     if (!r.job) {
       if (hipHostMalloc(&r.job, 4096, hipHostMallocCoherent) != hipSuccess) return set_err(EGES_E_NOMEM, "hipHostMalloc(job)");
       std::memset(r.job, 0, 4096);
-      HIPCHK(hipMalloc(&r.counter, 64));
+      HIPCHK(hipMalloc(&r.counter, RESIDENT_COUNTER_BYTES));
+      HIPCHK(hipMemset(r.counter, 0, RESIDENT_COUNTER_BYTES));
     }
     if (r.data) (void)hipHostFree(r.data);
     r.data = nullptr;
     const size_t bytes = r.block ? resident_block_layout(cap).total : resident_layout(cap).total;
-    if (hipHostMalloc(&r.data, bytes, hipHostMallocCoherent) != hipSuccess)
+    // the data area is ordinary (cacheable) pinned memory, like the lanes' staging: uncached
+    // (coherent) memory made the root helpers' scattered row reads one PCIe read per lane. The
+    // servers order it by system-scope fences around each job (k_recover_lat.hip resident_next
+    // / resident_done); only the job word is coherent.
+    if (hipHostMalloc(&r.data, bytes, hipHostMallocDefault) != hipSuccess)
       return set_err(EGES_E_NOMEM, "hipHostMalloc(resident data)");
     if (r.block) {
       if (r.scratch) (void)hipFree(r.scratch);
@@ -1657,19 +1674,32 @@ int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& re
   const long long idle_ms = std::max<long long>(1, knob(KNOB_RESIDENT_IDLE_MS));
   const auto now = std::chrono::steady_clock::now();
   // a server idle for half its bound may be deciding to exit: restart it rather than race it
-  if (r.running && (hipStreamQuery(r.stream) == hipSuccess ||
-                    now - r.last_use > std::chrono::microseconds(idle_ms * 500)))
+  // (the block server's queued launch instead serves whatever job is pending when it starts)
+  if (!r.block && r.running &&
+      (hipStreamQuery(r.stream) == hipSuccess || now - r.last_use > std::chrono::microseconds(idle_ms * 500)))
+    resident_halt(d, r);
+  if (r.block && r.running &&
+      (r.cfg_kind != (uint32_t)kind || r.cfg_want != want || r.cfg_signer != signer || r.cfg_cid != cid))
     resident_halt(d, r);
   auto launch = [&]() -> int {
     if (!r.running) {  // the lane finishes what it runs and takes no more calls
       std::lock_guard<std::mutex> l0(d.lanes[r.lane].mu);
       d.lanes[r.lane].reserved.store(true, std::memory_order_release);
     }
-    HIPCHK(hipMemsetAsync(r.counter, 0, 64, r.stream));
+    if (!r.block) HIPCHK(hipMemsetAsync(r.counter, 0, RESIDENT_COUNTER_BYTES, r.stream));
+    if (++r.inst == 0) r.inst = 1;
     ResidentParams rp{r.job, r.data, r.scratch, r.cap, __atomic_load_n(&r.job->done, __ATOMIC_ACQUIRE), r.counter,
-                      (uint64_t)idle_ms * 100000ull, d.gtab, d.diag};
+                      (uint64_t)idle_ms * 100000ull, r.inst, d.gtab, d.diag};
     r.wgs = (uint32_t)std::max<long long>(1, std::min<long long>(knob(KNOB_RESIDENT_WGS), 1024));
-    const hipError_t e = r.block ? launch_lat_resident_block(rp, r.stream) : launch_lat_resident(rp, r.wgs, r.stream);
+    if (!r.data || !r.counter || (r.block && !r.scratch)) return set_err(EGES_E_HIP, "resident server: buffers missing");
+    hipError_t e;
+    if (r.block) {
+      RecoverParams bp{r.scratch, r.cap, (r.cap + 63) / 64 * 64, nullptr, nullptr, nullptr, d.gtab, nullptr};
+      (*base)(bp);
+      e = launch_lat_resident_block(rp, bp, r.stream);
+    } else {
+      e = launch_lat_resident(rp, r.wgs, r.stream);
+    }
     if (e != hipSuccess) {
       r.running = false;
       d.lanes[r.lane].reserved.store(false, std::memory_order_release);
@@ -1678,20 +1708,28 @@ int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& re
     r.running = true;
     return EGES_SUCCESS;
   };
-  if (!r.running) {
-    const int rc = launch();
+  if (!r.running || (r.block && now - r.last_use > std::chrono::microseconds(idle_ms * 500))) {
+    const int rc = launch();  // (block: the queued launch may be about to idle out; this one follows it)
     if (rc) return rc;
+    r.cfg_kind = (uint32_t)kind;
+    r.cfg_want = want;
+    r.cfg_signer = signer;
+    r.cfg_cid = cid;
   }
   fill(r.data, r.job);
   __atomic_store_n(&r.job->n, (uint32_t)n, __ATOMIC_RELAXED);
   __atomic_store_n(&r.job->kind, (uint32_t)kind, __ATOMIC_RELAXED);
   const uint32_t seq = ++r.seq;
   __atomic_store_n(&r.job->seq, seq, __ATOMIC_RELEASE);
+  if (r.block) {  // the next job's launch, queued behind this one while the GPU works
+    const int rc = launch();
+    if (rc) return rc;
+  }
   const auto t0 = std::chrono::steady_clock::now();
   for (uint64_t spins = 0; __atomic_load_n(&r.job->done, __ATOMIC_ACQUIRE) != seq; ++spins) {
     cpu_relax();
     if ((spins & 1023) != 1023) continue;
-    if (hipStreamQuery(r.stream) == hipSuccess && __atomic_load_n(&r.job->done, __ATOMIC_ACQUIRE) != seq) {
+    if (!r.block && hipStreamQuery(r.stream) == hipSuccess && __atomic_load_n(&r.job->done, __ATOMIC_ACQUIRE) != seq) {
       // the server exited without taking the job (its idle bound): a fresh one takes it (lane 0
       // stays reserved in between)
       const int rc = launch();
@@ -1708,11 +1746,31 @@ int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& re
 }
 // A host-buffer block (ecrecover or types.Sender rows) on the resident block server; -1: not taken.
 int resident_block_run(Dev& d, const HostJob& j, size_t off, size_t n) {
-  const ResidentBlockLayout L = resident_block_layout(resident_cap(d, true));
+  const uint32_t cap = resident_cap(d, true);
+  const ResidentBlockLayout L = resident_block_layout(cap);
   const bool snd = j.kind == HostJob::SENDER;
+  const uint32_t want = snd ? 0u : ((j.pub ? 1u : 0u) | (j.addr ? 2u : 0u));
+  // the block server's launch parameters for this kind (the data area's fixed layout)
+  Resident& r = d.res_blk;
+  const std::function<void(RecoverParams&)> base = [&](RecoverParams& p) {  // (r.data / r.scratch exist)
+    if (snd) {
+      p.status = r.data + L.sstatus;
+      p.addr = r.data + L.saddr;
+      bind_sender_rows(p, r.data + L.sh, r.data + L.sr, r.data + L.ss, r.data + L.sv, r.data + L.sf, j.signer, j.chain_id);
+    } else {
+      p.status = r.data + L.status;
+      p.addr = j.addr ? r.data + L.addr : nullptr;
+      p.pub = j.pub ? r.data + L.pub : nullptr;
+      p.raw_msg = r.data + L.msg;
+      p.raw_sig = r.data + L.sig;
+    }
+    p.wide = 0;  // narrow form
+    p.n_helpers = resident_block_helpers(r.cap);
+    p.diag = d.diag;
+  };
   bool fault = false;
   const int rc = resident_job(
-      d, d.res_blk, snd ? RESIDENT_SENDER : RESIDENT_RECOVER, n,
+      d, r, snd ? RESIDENT_SENDER : RESIDENT_RECOVER, n,
       [&](uint8_t* D, ResidentJob* job) {
         if (snd) {
           std::memcpy(D + L.sh, j.a + off * 32, n * 32);
@@ -1739,7 +1797,8 @@ int resident_block_run(Dev& d, const HostJob& j, size_t off, size_t n) {
           if (j.pub) std::memcpy(j.pub + off * 65, D + L.pub, n * 65);
           if (j.addr) std::memcpy(j.addr + off * 20, D + L.addr, n * 20);
         }
-      });
+      },
+      &base, want, snd ? (uint32_t)j.signer : 0u, snd ? j.chain_id : 0u);
   if (rc == EGES_SUCCESS && fault)
     return set_err(EGES_E_HIP, "a kernel hand-off timed out (EGES_ENGINE_FAULT items; EGES_DIAG_HANDOFF)");
   return rc;

@@ -688,11 +688,12 @@ DEV void high_wave_tri(LatLds& S, const fr& x, const fr& c, const Diag& dg) {
 // on E, and the table's isomorphic curve adds the factor zeta. y comes from LDS (helper wave).
 // Narrow: both GLV halves over every window here, two barriers. Split: the low windows of both
 // halves here; the high windows' sum (waves 2, 3) and u_g G (wave 1) are joined at the end.
-DEV void root_fetch(const RecoverParams& prm, uint32_t idx, const fr& c, bool odd, LatLds& S);  // below
+DEV void root_fetch(const RecoverParams& prm, uint32_t idx, const fr& c, bool odd, uint32_t epoch, LatLds& S);  // below
 struct RootSrc {  // narrow recover form: where wave 0 finds R's y (root_fetch)
   const RecoverParams* prm;
   uint32_t idx;
   bool odd;
+  uint32_t epoch;  // the launch's (or the resident server's job's) root-word tag
 };
 template <class ST, int FORM>
 DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& S, ST* st, const Diag& dg,
@@ -718,7 +719,7 @@ DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& 
     bool hinf;
     const gejr Hp = get_part(S, 3, hinf);
     A = join_parts(A, ainf, Hp, hinf, ainf, dg);
-    root_fetch(*root->prm, root->idx, c, root->odd, S);
+    root_fetch(*root->prm, root->idx, c, root->odd, root->epoch, S);
     A.z = fr_mul(A.z, fr{S.ylift[row_lane()]});
     flag_wait(S, F_G);
     bool ginf;
@@ -729,7 +730,7 @@ DEV void ecmult_deferred(gejr& Q, bool& qinf, const fr& x, const fr& c, LatLds& 
   }
   if (SPLIT) flag_wait(S, F_Y);
   else __syncthreads();  // partial sums (and y) ready
-  if (root) root_fetch(*root->prm, root->idx, c, root->odd, S);  // (this wave's own LDS words)
+  if (root) root_fetch(*root->prm, root->idx, c, root->odd, root->epoch, S);  // (this wave's own LDS words)
   A.z = fr_mul(A.z, fr_mul(zeta, fr{S.ylift[row_lane()]}));  // the true curve
   bool ginf;
   if (SPLIT) flag_wait(S, F_G);
@@ -760,9 +761,9 @@ DEV uint32_t* root_area(const RecoverParams& prm) {
   return const_cast<uint32_t*>(prm.rec) + (size_t)REC_ROWS * prm.n_pad;
 }
 
-DEV void root_helper(const RecoverParams& prm) {
+DEV void root_helper(const RecoverParams& prm, uint32_t epoch, uint32_t n) {
   const uint32_t j = blockIdx.x * ROOT_WG + threadIdx.x;
-  if (j >= prm.n) return;
+  if (j >= n) return;
   LatParse q;
   if (prm.wire_raw) {  // wire form: this lane decodes item j itself (x, recid, ok: the waves' record)
     uint64_t ra, len;
@@ -783,19 +784,19 @@ DEV void root_helper(const RecoverParams& prm) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) a[i * np + j] = y[i];
   a[8 * np + j] = ok ? 1u : 0u;
-  a[9 * np + j] = prm.epoch ^ ROOT_TAG2;
-  __hip_atomic_store(&a[10 * np + j], prm.epoch ^ ROOT_TAG, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  a[9 * np + j] = epoch ^ ROOT_TAG2;
+  __hip_atomic_store(&a[10 * np + j], epoch ^ ROOT_TAG, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // wave 0 of signature idx: y and ok into LDS, from the helpers or (bounded wait) computed here
-DEV void root_fetch(const RecoverParams& prm, uint32_t idx, const fr& c, bool odd, LatLds& S) {
+DEV void root_fetch(const RecoverParams& prm, uint32_t idx, const fr& c, bool odd, uint32_t epoch, LatLds& S) {
   uint32_t* a = root_area(prm);
   const size_t np = prm.n_pad;
   bool got = false;
 #pragma unroll 1
   for (int it = 0; it < 40000; ++it) {  // ~4 ms: the helpers normally finish long before
-    if (__hip_atomic_load(&a[10 * np + idx], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == (prm.epoch ^ ROOT_TAG) &&
-        __hip_atomic_load(&a[9 * np + idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (prm.epoch ^ ROOT_TAG2)) {
+    if (__hip_atomic_load(&a[10 * np + idx], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == (epoch ^ ROOT_TAG) &&
+        __hip_atomic_load(&a[9 * np + idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (epoch ^ ROOT_TAG2)) {
       got = true;
       break;
     }
@@ -832,20 +833,20 @@ DEV uint32_t hw_place() {
 // y and u1 G; waves 2 and 3 the high windows of the two GLV halves against their own table of
 // D = 2^75 R'; wave 0 the low windows of both halves, then joins the three partial sums.
 template <class ST, int FORM>
-DEV void recover_lat_item(const RecoverParams& prm, uint32_t idx, LatLds& S, uint64_t* stamps);
+DEV void recover_lat_item(const RecoverParams& prm, uint32_t idx, LatLds& S, uint64_t* stamps, uint32_t epoch);
 template <class ST, int FORM>
 DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   constexpr bool SPLIT = FORM == FORM_SPLIT;
   __shared__ LatLds S;
   if (!SPLIT && blockIdx.x < prm.n_helpers) {  // narrow / three-wave forms: the lane-serial roots
-    root_helper(prm);
+    root_helper(prm, prm.epoch, prm.n);
     return;
   }
-  recover_lat_item<ST, FORM>(prm, blockIdx.x - (SPLIT ? 0u : prm.n_helpers), S, stamps);  // a signature per workgroup
+  recover_lat_item<ST, FORM>(prm, blockIdx.x - (SPLIT ? 0u : prm.n_helpers), S, stamps, prm.epoch);  // a signature per workgroup
 }
 // signature idx on this workgroup (all its waves enter; each returns when its part is done)
 template <class ST, int FORM>
-DEV void recover_lat_item(const RecoverParams& prm, uint32_t idx, LatLds& S, uint64_t* stamps) {
+DEV void recover_lat_item(const RecoverParams& prm, uint32_t idx, LatLds& S, uint64_t* stamps, uint32_t epoch) {
   constexpr bool SPLIT = FORM == FORM_SPLIT;   // four waves, wave 1 computes y
   constexpr bool FLAGS = FORM != FORM_NARROW;  // LDS flag hand-offs instead of barriers
   ST st_;
@@ -934,7 +935,7 @@ DEV void recover_lat_item(const RecoverParams& prm, uint32_t idx, LatLds& S, uin
   // --- Q = u2 R + u1 G, R's y (the square root) computed beside the Strauss loop
   gejr Q;
   bool qinf;
-  const RootSrc root{&prm, idx, odd};
+  const RootSrc root{&prm, idx, odd, epoch};
   ecmult_deferred<ST, FORM>(Q, qinf, x, c, S, st, dg, SPLIT ? nullptr : &root);
   const bool fault = FLAGS && ho_failed(&S.flag[F_ERR], dg);  // after wave 0's last wait
   ok = ok && S.yok != 0 && !qinf && !fault;  // ge_set_xo_var failure, main_impl.h:120
@@ -1135,37 +1136,114 @@ hipError_t launch_recover_lat(const RecoverParams& p0, hipStream_t st) {
   return hipGetLastError();
 }
 
-// ---- resident single-call server (launch.h ResidentParams). Every workgroup polls the job word
-// (thread 0, system-scope acquire, s_sleep between polls), takes items blockIdx.x, + gridDim.x, ...
-// of a job through the split form, and counts itself done; the last one stores the job's sequence
-// into `done` after every workgroup's outputs (each releases at system scope before its count).
-// Exits on the stop word or after idle_ticks without a job (the host restarts it on demand and
-// never hands a job to a server older than half that: capi.hip Resident).
+// ---- resident servers (launch.h ResidentParams). Workgroup 0's thread 0 polls the host's job word
+// (system-scope acquire, s_sleep between polls) and mirrors each job into device memory (the
+// words after the completion counters); every other workgroup polls the mirror, so the host
+// memory sees one poller whatever the grid (a poller per workgroup over PCIe slowed a
+// 1,000-workgroup grid tenfold). Workgroup 0 alone decides to exit (the stop word, or idle_ticks
+// without a job), so the grid leaves together. Each workgroup takes items blockIdx.x,
+// + gridDim.x, ... and counts itself done; the last one stores the job's sequence into `done`
+// after every workgroup's outputs (each releases at system scope before its count).
+// RM_SEQ: one 64-bit word (launch id << 32 | sequence), so a workgroup never pairs this launch's
+// id with an earlier launch's sequence (launch.h RESIDENT_COUNTER_BYTES covers the mirror)
+enum { RM_SEQ = 8, RM_EXIT = 10, RM_N, RM_KIND, RM_SIGNER, RM_WANT, RM_CID_LO, RM_CID_HI, RM_END };
+static_assert(RM_END * 4 <= RESIDENT_COUNTER_BYTES, "resident mirror");
+struct ResidentNext {
+  uint32_t seq, n, kind, signer, want, exit;
+  uint64_t cid;
+};
+// thread 0: the next job (one the host handed over and no launch has served yet: seq > done)
+// after `seen`, or this launch's exit, into J. The mirror entries carry the launch's id, so a
+// launch queued behind another never takes the earlier one's mirror for its own.
+DEV void resident_next(const ResidentParams& rp, uint32_t seen, uint64_t last, ResidentNext& J) {
+  uint32_t* M = rp.counter;
+  if (blockIdx.x == 0) {
+    uint32_t q = seen, stop = 0;
+#pragma unroll 1
+    for (;;) {
+      q = __hip_atomic_load(&rp.job->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      stop = __hip_atomic_load(&rp.job->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint32_t d = __hip_atomic_load(&rp.job->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (stop || (q != seen && q > d)) break;
+      if (__builtin_amdgcn_s_memrealtime() - last > rp.idle_ticks) {
+        stop = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+    if (stop) {
+      J.exit = 1;
+      __hip_atomic_store(&M[RM_EXIT], rp.inst, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    J.exit = 0;
+    J.seq = q;
+    J.n = __hip_atomic_load(&rp.job->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    J.kind = __hip_atomic_load(&rp.job->kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    J.signer = __hip_atomic_load(&rp.job->signer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    J.want = __hip_atomic_load(&rp.job->want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    J.cid = __hip_atomic_load(&rp.job->chain_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (gridDim.x > 1) {
+      __hip_atomic_store(&M[RM_N], J.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&M[RM_KIND], J.kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&M[RM_SIGNER], J.signer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&M[RM_WANT], J.want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&M[RM_CID_LO], (uint32_t)J.cid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&M[RM_CID_HI], (uint32_t)(J.cid >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(M + RM_SEQ), (uint64_t)rp.inst << 32 | q, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+#pragma unroll 1
+  for (;;) {
+    const uint32_t e = __hip_atomic_load(&M[RM_EXIT], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t qi = __hip_atomic_load(reinterpret_cast<uint64_t*>(M + RM_SEQ), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t q = (uint32_t)qi, inst = (uint32_t)(qi >> 32);
+    if (e == rp.inst) {  // (this launch's exit; earlier launches' marks carry their own ids)
+      J.exit = 1;
+      return;
+    }
+    if (inst == rp.inst && q > seen) {
+      // the job's inputs sit in cacheable pinned memory the host just wrote: a system-scope
+      // acquire (cache invalidation) on this workgroup's side too
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      J.exit = 0;
+      J.seq = q;
+      J.n = __hip_atomic_load(&M[RM_N], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      J.kind = __hip_atomic_load(&M[RM_KIND], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      J.signer = __hip_atomic_load(&M[RM_SIGNER], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      J.want = __hip_atomic_load(&M[RM_WANT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      J.cid = (uint64_t)__hip_atomic_load(&M[RM_CID_LO], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+              (uint64_t)__hip_atomic_load(&M[RM_CID_HI], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 32;
+      return;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+// thread 0: this workgroup is done with job seq; the last one publishes it
+DEV void resident_done(const ResidentParams& rp, uint32_t seq) {
+  if (blockIdx.x == 0 && rp.diag) __hip_atomic_fetch_add(rp.diag + EGES_DIAG_RESIDENT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this workgroup's outputs (thread 0 wrote them), system scope
+  const uint32_t c = __hip_atomic_fetch_add(&rp.counter[seq & 1u], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (c == gridDim.x - 1) {
+    __hip_atomic_store(&rp.counter[seq & 1u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&rp.job->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// The single-call server: coalesced groups of eges_ecdsa_recover / eges_ecdsa_verify (split form).
 __global__ void __launch_bounds__(LAT_WG_SPLIT) lat_resident_kernel(ResidentParams rp) {
   __shared__ LatLds S;
-  __shared__ uint32_t jseq, jn, jkind, jexit;
+  __shared__ ResidentNext J;
   uint32_t seen = rp.seen0;
   uint64_t last = __builtin_amdgcn_s_memrealtime();
 #pragma unroll 1
   for (;;) {
-    if (threadIdx.x == 0) {
-      uint32_t q = seen, stop = 0;
-#pragma unroll 1
-      for (;;) {
-        q = __hip_atomic_load(&rp.job->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        stop = __hip_atomic_load(&rp.job->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (stop || q != seen) break;
-        if (__builtin_amdgcn_s_memrealtime() - last > rp.idle_ticks) break;
-        __builtin_amdgcn_s_sleep(8);
-      }
-      jexit = (stop || q == seen) ? 1u : 0u;
-      jseq = q;
-      jn = __hip_atomic_load(&rp.job->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      jkind = __hip_atomic_load(&rp.job->kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (threadIdx.x == 0) resident_next(rp, seen, last, J);
     __syncthreads();
-    if (jexit) return;
-    const uint32_t seq = jseq, n = jn < rp.cap ? jn : rp.cap, kind = jkind;
+    if (J.exit) return;
+    const uint32_t seq = J.seq, n = J.n < rp.cap ? J.n : rp.cap, kind = J.kind;
     const ResidentLayout L = resident_layout(rp.cap);
 #pragma unroll 1
     for (uint32_t idx = blockIdx.x; idx < n; idx += gridDim.x) {
@@ -1175,7 +1253,7 @@ __global__ void __launch_bounds__(LAT_WG_SPLIT) lat_resident_kernel(ResidentPara
         p.raw_sig = rp.data + L.sig;
         p.wide = FORM_SPLIT;
         p.diag = rp.diag;
-        recover_lat_item<NoStamp, FORM_SPLIT>(p, idx, S, nullptr);
+        recover_lat_item<NoStamp, FORM_SPLIT>(p, idx, S, nullptr, 0u);
       } else {
         VerifyParams v{rp.data + L.vpub, rp.data + L.vpublen, rp.data + L.vmsg, rp.data + L.vsig, n,
                        rp.data + L.vok, rp.gtab, nullptr};
@@ -1184,18 +1262,10 @@ __global__ void __launch_bounds__(LAT_WG_SPLIT) lat_resident_kernel(ResidentPara
       }
       __syncthreads();  // every wave done with this item's LDS
     }
-    if (threadIdx.x == 0) {
-      if (blockIdx.x == 0 && rp.diag) __hip_atomic_fetch_add(rp.diag + EGES_DIAG_RESIDENT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this workgroup's outputs (thread 0 wrote them), system scope
-      const uint32_t c = __hip_atomic_fetch_add(&rp.counter[seq & 1u], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (c == gridDim.x - 1) {
-        __hip_atomic_store(&rp.counter[seq & 1u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&rp.job->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
+    if (threadIdx.x == 0) resident_done(rp, seq);
     seen = seq;
     last = __builtin_amdgcn_s_memrealtime();
-    __syncthreads();  // (jseq / jn / jkind are rewritten by the next poll)
+    __syncthreads();  // (J is rewritten by the next poll)
   }
 }
 hipError_t launch_lat_resident(const ResidentParams& p, uint32_t wgs, hipStream_t st) {
@@ -1207,91 +1277,30 @@ hipError_t launch_lat_resident(const ResidentParams& p, uint32_t wgs, hipStream_
 // rows): the narrow form's launch kept resident. The first ceil(cap / 128) workgroups are the
 // root helpers (their lanes take items j < n), then one workgroup per item; each job's epoch is
 // its sequence number, so root words of an earlier job never match.
-__global__ void __launch_bounds__(LAT_WG, 3) lat_resident_block_kernel(ResidentParams rp) {
+// base: the server's RecoverParams (the layout's pointers for its kind, signer, chain id and
+// outputs fixed per launch: the host relaunches when a job needs others), read from the argument
+// segment as a launch's are. One job per launch: the host enqueues the next instance while this
+// one works, so it is already polling when the next job comes (a loop over jobs inside one
+// launch kept the item's invariants live across jobs and pushed the kernel into spills).
+// Each job supplies n and its sequence number as the epoch of its root words.
+__global__ void __launch_bounds__(LAT_WG) lat_resident_block_kernel(ResidentParams rp, RecoverParams base) {
   __shared__ LatLds S;
-  __shared__ uint32_t jseq, jn, jkind, jexit, jsigner, jwant;
-  __shared__ uint64_t jcid;
-  __shared__ __attribute__((aligned(16))) unsigned char jp_raw[sizeof(RecoverParams)];
-  RecoverParams& jp = *reinterpret_cast<RecoverParams*>(jp_raw);
-  const uint32_t H = resident_block_helpers(rp.cap), n_pad = (rp.cap + 63) / 64 * 64;
-  uint32_t seen = rp.seen0;
-  uint64_t last = __builtin_amdgcn_s_memrealtime();
-#pragma unroll 1
-  for (;;) {
-    if (threadIdx.x == 0) {
-      uint32_t q = seen, stop = 0;
-#pragma unroll 1
-      for (;;) {
-        q = __hip_atomic_load(&rp.job->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        stop = __hip_atomic_load(&rp.job->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (stop || q != seen) break;
-        if (__builtin_amdgcn_s_memrealtime() - last > rp.idle_ticks) break;
-        __builtin_amdgcn_s_sleep(8);
-      }
-      jexit = (stop || q == seen) ? 1u : 0u;
-      jseq = q;
-      jn = __hip_atomic_load(&rp.job->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      jkind = __hip_atomic_load(&rp.job->kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      jsigner = __hip_atomic_load(&rp.job->signer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      jwant = __hip_atomic_load(&rp.job->want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      jcid = __hip_atomic_load(&rp.job->chain_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    __syncthreads();
-    if (jexit) return;
-    const uint32_t seq = jseq, n = jn < rp.cap ? jn : rp.cap;
-    // the job's parameters in LDS (read where the item needs them, as a kernel's would be from
-    // its argument segment; a register copy pushed the kernel past 168 VGPRs)
-    if (threadIdx.x == 0) {
-    const ResidentBlockLayout L = resident_block_layout(rp.cap);
-    RecoverParams& p = jp;
-    p = RecoverParams{rp.scratch, n, n_pad, nullptr, nullptr, nullptr, rp.gtab, nullptr};
-    if (jkind == RESIDENT_SENDER) {
-      p.status = rp.data + L.sstatus;
-      p.addr = rp.data + L.saddr;
-      p.snd_h = rp.data + L.sh;
-      p.snd_r = rp.data + L.sr;
-      p.snd_s = rp.data + L.ss;
-      p.snd_v = rp.data + L.sv;
-      p.snd_f = rp.data + L.sf;
-      p.snd_signer = (int)jsigner;
-      p.snd_chain_id = jcid;
-    } else {
-      p.status = rp.data + L.status;
-      p.addr = (jwant & 2u) ? rp.data + L.addr : nullptr;
-      p.pub = (jwant & 1u) ? rp.data + L.pub : nullptr;
-      p.raw_msg = rp.data + L.msg;
-      p.raw_sig = rp.data + L.sig;
-    }
-    p.wide = FORM_NARROW;
-    p.n_helpers = H;
-    p.epoch = seq;
-    p.diag = rp.diag;
-    }
-    __syncthreads();
-    if (blockIdx.x < H) {
-      root_helper(jp);
-    } else if (blockIdx.x - H < n) {
-      recover_lat_item<NoStamp, FORM_NARROW>(jp, blockIdx.x - H, S, nullptr);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      if (blockIdx.x == 0 && rp.diag) __hip_atomic_fetch_add(rp.diag + EGES_DIAG_RESIDENT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this workgroup's outputs (thread 0 wrote them), system scope
-      const uint32_t c = __hip_atomic_fetch_add(&rp.counter[seq & 1u], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (c == gridDim.x - 1) {
-        __hip_atomic_store(&rp.counter[seq & 1u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&rp.job->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
-    seen = seq;
-    last = __builtin_amdgcn_s_memrealtime();
-    __syncthreads();
+  __shared__ ResidentNext J;
+  if (threadIdx.x == 0) resident_next(rp, 0u, __builtin_amdgcn_s_memrealtime(), J);
+  __syncthreads();
+  if (J.exit) return;
+  const uint32_t seq = J.seq, n = J.n < rp.cap ? J.n : rp.cap;
+  if (blockIdx.x < base.n_helpers) {
+    root_helper(base, seq, n);
+  } else if (blockIdx.x - base.n_helpers < n) {
+    recover_lat_item<NoStamp, FORM_NARROW>(base, blockIdx.x - base.n_helpers, S, nullptr, seq);
   }
+  __syncthreads();
+  if (threadIdx.x == 0) resident_done(rp, seq);
 }
-hipError_t launch_lat_resident_block(const ResidentParams& p, hipStream_t st) {
-  const uint32_t grid = resident_block_helpers(p.cap) + p.cap;
-  hipLaunchKernelGGL(lat_resident_block_kernel, dim3(grid), dim3(LAT_WG), 0, st, p);
+hipError_t launch_lat_resident_block(const ResidentParams& p, const RecoverParams& base, hipStream_t st) {
+  const uint32_t grid = base.n_helpers + p.cap;
+  hipLaunchKernelGGL(lat_resident_block_kernel, dim3(grid), dim3(LAT_WG), 0, st, p, base);
   return hipGetLastError();
 }
 

@@ -215,20 +215,23 @@ __host__ __device__ inline ResidentBlockLayout resident_block_layout(uint32_t ca
   L.total = a > b ? a : b;
   return L;
 }
+// bytes of ResidentParams::counter: the completion counters, then the block server's job mirror
+constexpr uint32_t RESIDENT_COUNTER_BYTES = 256;
 struct ResidentParams {
   ResidentJob* job;
   uint8_t* data;
   uint32_t* scratch;     // block server: the narrow form's record / root rows (n_pad = cap padded)
   uint32_t cap;
   uint32_t seen0;        // the last sequence finished before this launch
-  uint32_t* counter;     // device memory, 2 words, zero at launch
+  uint32_t* counter;     // device memory, 2 words: zero at launch (single) / left zero by the last WG (block)
   uint64_t idle_ticks;   // exit after this long without a job (s_memrealtime, 100 MHz)
+  uint32_t inst;         // this launch's id (nonzero): its workgroups' exit mark in the mirror
   const uint32_t* gtab;
   uint32_t* diag;
 };
 hipError_t launch_lat_resident(const ResidentParams& p, uint32_t wgs, hipStream_t st);
 // the block server: ceil(cap / 128) root-helper workgroups, then cap narrow-form workgroups
-hipError_t launch_lat_resident_block(const ResidentParams& p, hipStream_t st);
+hipError_t launch_lat_resident_block(const ResidentParams& p, const RecoverParams& base, hipStream_t st);
 __host__ __device__ inline uint32_t resident_block_helpers(uint32_t cap) { return (cap + 127) / 128; }
 // Blocks the lane-serial kernels may need for a pass of n signatures at a resident grid of
 // max_blocks (grid_for_lane_serial: more than resident when n > max_blocks * WG * MAX_SLOTS).
