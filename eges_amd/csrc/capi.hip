@@ -77,6 +77,13 @@ int env_int(const char* name, int dflt) {
 // single-chunk host calls that run on the latency kernel (which needs no shared workspace) do
 // not queue behind each other on the device mutex.
 constexpr int NLANES = 4;
+// A host-buffer call's input gate (handoff.cuh gate_wait): word 0 the last sequence opened,
+// word 1 set by a wave whose wait ran out. Coherent pinned memory, one per lane / device.
+struct Gate {
+  uint32_t* w = nullptr;
+  uint32_t* dev = nullptr;  // device word: workgroup 0's mirror of the opened sequence
+  uint32_t seq = 0;
+};
 struct Lane {
   std::mutex mu;
   // the resident server runs on lane 0's stream (its persistent kernel holds that stream's
@@ -86,6 +93,7 @@ struct Lane {
   uint8_t* buf = nullptr;
   size_t buf_cap = 0;
   uint8_t* pin = nullptr;
+  Gate gate;
   hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_k[2] = {nullptr, nullptr};
 };
 
@@ -124,6 +132,7 @@ struct Dev {
   uint8_t* buf = nullptr;  // per-call device scratch, grown on demand
   size_t buf_cap = 0;
   uint8_t* pin = nullptr;  // pinned host staging of single-chunk host-buffer calls (PIN_BYTES)
+  Gate gate;               //   and their input gate
   // overlapped recover launches (EGES_OVERLAP): a second stream, workspace and its events
   hipStream_t aux = nullptr;
   uint32_t* ws2 = nullptr;
@@ -195,6 +204,7 @@ const KnobDef KNOB_DEFS[KNOB_COUNT] = {
     {"EGES_RESIDENT_IDLE_MS", 4},
     {"EGES_RESIDENT_BLOCK", 0},
     {"EGES_RESIDENT_BLOCK_CAP", 1024},
+    {"EGES_GATE", 1},
 };
 std::atomic<long long> g_knob[KNOB_COUNT];
 std::once_flag g_knob_once;
@@ -361,6 +371,8 @@ Dev::~Dev() {
   if (diag) (void)hipFree(diag);
   if (buf) (void)hipFree(buf);
   if (pin) (void)hipHostFree(pin);
+  if (gate.w) (void)hipHostFree(gate.w);
+  if (gate.dev) (void)hipFree(gate.dev);
   if (last) (void)hipEventDestroy(last);
   for (int r = 0; r < 2; ++r) {
     if (ev_in[r]) (void)hipEventDestroy(ev_in[r]);
@@ -384,6 +396,8 @@ Dev::~Dev() {
     if (l.stream) (void)hipStreamSynchronize(l.stream);
     if (l.buf) (void)hipFree(l.buf);
     if (l.pin) (void)hipHostFree(l.pin);
+    if (l.gate.w) (void)hipHostFree(l.gate.w);
+    if (l.gate.dev) (void)hipFree(l.gate.dev);
     for (int r = 0; r < 2; ++r) {
       if (l.ev_in[r]) (void)hipEventDestroy(l.ev_in[r]);
       if (l.ev_k[r]) (void)hipEventDestroy(l.ev_k[r]);
@@ -519,6 +533,7 @@ hipError_t launch_recover_pass(Dev& d, const Route& rt, const RecoverParams& p0,
   const bool mid = use_mid(d, rt, p.n);
   if (p.wire_raw && !(mid ? mid_bucket(d, rt, p.n) : p.n <= rt.lat_max)) return hipErrorInvalidValue;  // wire_fused() decides
   if (p.snd_r && !(mid || p.n <= rt.lat_max)) return hipErrorInvalidValue;  // sender_fused() decides
+  if (p.gate && !(mid || p.n <= rt.lat_max || p.raw_sig)) return hipErrorInvalidValue;  // (lane-serial: no gate)
 #ifdef EGES_PHASE_STAMPS
   if (mid) {
     hipError_t e = stamp_buf((p.n + 63) / 64 * 4, st);  // one row per wave
@@ -849,6 +864,54 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     pin = nullptr;
     return set_err(EGES_E_NOMEM, "hipHostMalloc(%zu) failed", PIN_BYTES);
   }
+  // A pinned call whose kernels read the inputs themselves (the fused latency / mid-size forms)
+  // launches first and copies its inputs into the pinned buffer while the launch is in flight:
+  // the kernels wait at the gate (handoff.cuh gate_wait), which opens after the copies. Opening is
+  // also the guard's destructor, so no return path leaves a launched kernel waiting (declared
+  // after `drain`: it runs first).
+  Gate& gate = small ? lane->gate : d.gate;
+  const bool gating = pinned && knob(KNOB_GATE) != 0 &&
+                      (j.kind == HostJob::RECOVER || j.kind == HostJob::SENDER || (j.kind == HostJob::SENDER_RAW && !j.decode_only));
+  if (gating && !gate.w) {
+    if (hipHostMalloc(&gate.w, 64, hipHostMallocCoherent) != hipSuccess) {
+      gate.w = nullptr;
+      return set_err(EGES_E_NOMEM, "hipHostMalloc(gate) failed");
+    }
+    std::memset(gate.w, 0, 64);
+    if (hipMalloc(&gate.dev, 64) != hipSuccess || hipMemset(gate.dev, 0, 64) != hipSuccess) {
+      (void)hipHostFree(gate.w);
+      gate.w = nullptr;
+      gate.dev = nullptr;
+      return set_err(EGES_E_NOMEM, "hipMalloc(gate) failed");
+    }
+  }
+  struct GateOpen {
+    struct Copy {
+      uint8_t* dst;
+      const void* src;
+      size_t n;
+    } q[8];
+    int nq = 0;
+    uint32_t* w = nullptr;  // armed: the kernels wait for sequence `seq`
+    uint32_t seq = 0;
+    void open() {
+      for (int i = 0; i < nq; ++i) std::memcpy(q[i].dst, q[i].src, q[i].n);
+      nq = 0;
+      if (w) __atomic_store_n(w, seq, __ATOMIC_RELEASE);
+      w = nullptr;
+    }
+    ~GateOpen() { open(); }
+  } gopen;
+  bool defer = false;  // this chunk's inputs wait for gopen.open()
+  auto arm = [&](RecoverParams& p) {  // a deferred chunk's kernels wait at the gate
+    if (!defer) return;
+    if (++gate.seq == 0) gate.seq = 1;
+    p.gate = gate.w;
+    p.gate_dev = gate.dev;
+    p.gate_seq = gate.seq;
+    gopen.w = gate.w;
+    gopen.seq = gate.seq;
+  };
   if (!small) {
     HIPCHK(hipStreamWaitEvent(st, d.last, 0));
     HIPCHK(hipStreamWaitEvent(sx, d.last, 0));
@@ -861,8 +924,9 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   // H2D / D2H operations at all, the outputs are written straight into the pinned buffer too).
   auto h2d = [&](uint8_t* B, uint8_t* dst, const void* src, size_t bytes) -> int {
     if (!bytes) return EGES_SUCCESS;
-    if (pinned) {
-      std::memcpy(dst, src, bytes);  // dst points into the pinned buffer (see I below)
+    if (pinned) {  // dst points into the pinned buffer (see I below)
+      if (defer) gopen.q[gopen.nq++] = {dst, src, bytes};
+      else std::memcpy(dst, src, bytes);
       return EGES_SUCCESS;
     }
     (void)B;
@@ -943,18 +1007,21 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     if (j.kind == HostJob::RECOVER) {
       uint8_t* dm = I;
       uint8_t* ds = dm + m * 32;
+      const bool fused = fused_parse(d, rt, m);
+      defer = gating && fused;
       H2D(B, dm, j.a + base * 32, m * 32);
       H2D(B, ds, j.b + base * 65, m * 65);
       FLUSH_IN(B);
       JOIN_IN(r);
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, j.addr ? o_addr : nullptr, j.pub ? o_pub : nullptr,
                       d.gtab, wsk};
-      if (fused_parse(d, rt, m)) {  // the latency / mid-size kernels parse the bytes themselves
+      if (fused) {  // the latency / mid-size kernels parse the bytes themselves
         p.raw_msg = dm;
         p.raw_sig = ds;
       } else {
         HIPCHK(launch_prep_ecrecover(dm, ds, (uint32_t)m, (uint32_t)m_pad, rec, sk));
       }
+      arm(p);
       HIPCHK(launch_recover_pass(d, rt, p, sk));
     } else if (j.kind == HostJob::SENDER) {
       uint8_t* dh = I;
@@ -962,6 +1029,8 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       uint8_t* dsv = dr + m * 32;
       uint8_t* dv = dsv + m * 32;
       uint8_t* df = dv + m * 32;
+      const bool fused = sender_fused(d, rt, m, {dh, dr, dsv, dv});
+      defer = gating && fused;
       H2D(B, dh, j.a + base * 32, m * 32);
       H2D(B, dr, j.b + base * 32, m * 32);
       H2D(B, dsv, j.c + base * 32, m * 32);
@@ -970,11 +1039,12 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       FLUSH_IN(B);
       JOIN_IN(r);
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, wsk};
-      if (sender_fused(d, rt, m, {dh, dr, dsv, dv}))  // the recover kernel reads the rows itself
+      if (fused)  // the recover kernel reads the rows itself
         bind_sender_rows(p, dh, dr, dsv, dv, j.e ? df : nullptr, j.signer, j.chain_id);
       else
         HIPCHK(launch_prep_sender(dh, dr, dsv, dv, j.e ? df : nullptr, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id,
                                   rec, sk));
+      arm(p);
       HIPCHK(launch_recover_pass(d, rt, p, sk));
     } else if (j.kind == HostJob::PRECOMPILE) {
       uint8_t* din = I;
@@ -999,6 +1069,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       // (the fused form reads the encodings straight from the pinned buffer: a pipelined host copy
       // + DMA into device memory measured 0.486-0.508 ms against 0.450 ms for C1, same kernel)
       const bool fused = !j.decode_only && wire_fused(d, rt, m, draw);
+      defer = gating && fused;
       if (rg.raw_len) H2D(B, draw, j.a + rg.raw_lo, rg.raw_len);
       H2D(B, reinterpret_cast<uint8_t*>(doff), j.offsets + base, 8 * (m + 1));
       FLUSH_IN(B);
@@ -1017,6 +1088,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
           HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, vf, sk));
           HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, sk));
         }
+        arm(p);
         HIPCHK(launch_recover_pass(d, rt, p, sk));
       }
     } else {
@@ -1037,6 +1109,8 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       HIPCHK(launch_verify_any(d, rt, p, small, sk));
     }
     HSTAMP(3);
+    if (defer) gopen.open();  // the inputs, while the launch is in flight; then the gate
+    defer = false;
     if (sx != st) HIPCHK(hipEventRecord(ev_k[r], sk));
     // --- the previous chunk's outputs, while this chunk computes
     if (have_prev) {
@@ -1056,6 +1130,10 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   if (sa != st) HIPCHK(hipStreamSynchronize(sa));
   HSTAMP(4);
   drain.armed = false;
+  if (gating && __atomic_load_n(&gate.w[1], __ATOMIC_ACQUIRE) != 0u) {
+    __atomic_store_n(&gate.w[1], 0u, __ATOMIC_RELAXED);
+    return set_err(EGES_E_HIP, "a kernel's input gate timed out");
+  }
   if (pinned && have_prev) unpack(prev);
   HSTAMP(5);
   // items a kernel marked EGES_ENGINE_FAULT (a wave hand-off timed out, handoff.cuh) have no

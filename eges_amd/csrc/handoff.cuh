@@ -46,6 +46,40 @@ DEV bool ho_failed(const uint32_t* err, const Diag& dg) {
   if (bad) diag_bump(dg, EGES_DIAG_HANDOFF);
   return bad;
 }
+// Host-buffer calls launch before their inputs are in the pinned buffer (capi.hip Gate): the
+// host copies them while the launch is in flight and then stores the call's sequence into the
+// gate word (coherent pinned memory). Workgroup 0's first wave alone polls that word (a poller
+// per wave over PCIe slowed a 1,000-workgroup launch 2.4x) and mirrors the sequence into a
+// device word that every wave waits for here before reading an input. No input line can be
+// cached on the device before that (the launch invalidated the caches, and nothing reads the
+// inputs before the gate), so no system-scope cache invalidation follows. A wait that runs out
+// (4 s; the host opens the gate on every path, microseconds after its launch) marks gate[1], and
+// the host fails the call rather than return results from stale inputs.
+DEV bool seq_before(uint32_t have, uint32_t want) { return (int32_t)(have - want) < 0; }
+DEV void gate_wait(const uint32_t* gate, uint32_t* mirror, uint32_t seq) {
+  if (!gate) return;
+  constexpr uint64_t BOUND = 400000000ull;  // s_memrealtime ticks (100 MHz): 4 s
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    uint32_t* g = const_cast<uint32_t*>(gate);
+#pragma unroll 1
+    while (seq_before(__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), seq)) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > BOUND) {
+        if (threadIdx.x == 0) __hip_atomic_store(g + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(mirror, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+#pragma unroll 1
+  while (seq_before(__hip_atomic_load(mirror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), seq)) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > BOUND + BOUND / 4) break;  // (workgroup 0 marks the failure)
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
 // tests only: workgroup 0's producer of flag k skips publishing it once per launch
 template <class P>
 DEV bool ho_skip(const P& prm, int k) {

@@ -48,6 +48,8 @@ enum KnobId : int {
   KNOB_RESIDENT_IDLE_MS,  //   it exits after this long without a job (restarted on demand)
   KNOB_RESIDENT_BLOCK,    // 1: latency-kernel blocks above LAT_TRI_MAX go to the resident block server
   KNOB_RESIDENT_BLOCK_CAP,  //   its largest block (and grid: helpers + one workgroup per item)
+  KNOB_GATE,              // 1: single-chunk host-buffer calls on the latency / mid-size kernels launch first
+                          //   and copy their inputs while the launch is in flight (capi.hip Gate)
   KNOB_COUNT
 };
 

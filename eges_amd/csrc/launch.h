@@ -46,6 +46,11 @@ struct RecoverParams {
   uint32_t n_helpers = 0, epoch = 0;
   // diagnostic counters of the device (EGES_DIAG_*, bumped by the rare exact branches; nullable)
   uint32_t* diag = nullptr;
+  // host-buffer calls (latency and mid-size kernels only): wait for *gate >= gate_seq before
+  // reading inputs (handoff.cuh gate_wait); null: the inputs are in place at launch
+  const uint32_t* gate = nullptr;
+  uint32_t* gate_dev = nullptr;  // its device-memory mirror (workgroup 0 copies the sequence there)
+  uint32_t gate_seq = 0;
   // tests only (KNOB_FORCE_REDO): run every exact-redo pass as if an accumulator was poisoned
   uint32_t force_redo = 0;
   // tests only (KNOB_TEST_SKIP_FLAG, handoff.cuh): workgroup test_skip_block's producer of hand-off
