@@ -533,7 +533,7 @@ hipError_t launch_recover_pass(Dev& d, const Route& rt, const RecoverParams& p0,
   const bool mid = use_mid(d, rt, p.n);
   if (p.wire_raw && !(mid ? mid_bucket(d, rt, p.n) : p.n <= rt.lat_max)) return hipErrorInvalidValue;  // wire_fused() decides
   if (p.snd_r && !(mid || p.n <= rt.lat_max)) return hipErrorInvalidValue;  // sender_fused() decides
-  if (p.gate && !(mid || p.n <= rt.lat_max || p.raw_sig)) return hipErrorInvalidValue;  // (lane-serial: no gate)
+  if (p.gate && !mid) return hipErrorInvalidValue;  // (the host waits for the mid-size kernels' completion word)
 #ifdef EGES_PHASE_STAMPS
   if (mid) {
     hipError_t e = stamp_buf((p.n + 63) / 64 * 4, st);  // one row per wave
@@ -864,7 +864,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     pin = nullptr;
     return set_err(EGES_E_NOMEM, "hipHostMalloc(%zu) failed", PIN_BYTES);
   }
-  // A pinned call whose kernels read the inputs themselves (the fused latency / mid-size forms)
+  // A pinned call whose mid-size kernel reads the inputs itself (the fused bucket / windowed forms)
   // launches first and copies its inputs into the pinned buffer while the launch is in flight:
   // the kernels wait at the gate (handoff.cuh gate_wait), which opens after the copies. Opening is
   // also the guard's destructor, so no return path leaves a launched kernel waiting (declared
@@ -903,9 +903,11 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     ~GateOpen() { open(); }
   } gopen;
   bool defer = false;  // this chunk's inputs wait for gopen.open()
+  bool gated = false;  // a gated mid-size launch ran: its last workgroup stores the sequence into gate.w[2]
   auto arm = [&](RecoverParams& p) {  // a deferred chunk's kernels wait at the gate
-    if (!defer) return;
+    if (!defer || p.n == 0) return;
     if (++gate.seq == 0) gate.seq = 1;
+    gated = true;  // (a mid-size launch: its kernels store the completion word)
     p.gate = gate.w;
     p.gate_dev = gate.dev;
     p.gate_seq = gate.seq;
@@ -1008,7 +1010,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       uint8_t* dm = I;
       uint8_t* ds = dm + m * 32;
       const bool fused = fused_parse(d, rt, m);
-      defer = gating && fused;
+      defer = gating && fused && use_mid(d, rt, m);  // (the latency kernels measured +-0 to +1.5 % slower)
       H2D(B, dm, j.a + base * 32, m * 32);
       H2D(B, ds, j.b + base * 65, m * 65);
       FLUSH_IN(B);
@@ -1030,7 +1032,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       uint8_t* dv = dsv + m * 32;
       uint8_t* df = dv + m * 32;
       const bool fused = sender_fused(d, rt, m, {dh, dr, dsv, dv});
-      defer = gating && fused;
+      defer = gating && fused && use_mid(d, rt, m);  // (the latency kernels measured +-0 to +1.5 % slower)
       H2D(B, dh, j.a + base * 32, m * 32);
       H2D(B, dr, j.b + base * 32, m * 32);
       H2D(B, dsv, j.c + base * 32, m * 32);
@@ -1069,7 +1071,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       // (the fused form reads the encodings straight from the pinned buffer: a pipelined host copy
       // + DMA into device memory measured 0.486-0.508 ms against 0.450 ms for C1, same kernel)
       const bool fused = !j.decode_only && wire_fused(d, rt, m, draw);
-      defer = gating && fused;
+      defer = gating && fused && use_mid(d, rt, m);  // (the latency kernels measured +-0 to +1.5 % slower)
       if (rg.raw_len) H2D(B, draw, j.a + rg.raw_lo, rg.raw_len);
       H2D(B, reinterpret_cast<uint8_t*>(doff), j.offsets + base, 8 * (m + 1));
       FLUSH_IN(B);
@@ -1125,9 +1127,27 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     if (rc) return rc;
   }
   if (!small) HIPCHK(hipEventRecord(d.last, sx));
-  HIPCHK(hipStreamSynchronize(sx));
-  if (sx != st) HIPCHK(hipStreamSynchronize(st));  // (st's last work is already behind sx's events)
-  if (sa != st) HIPCHK(hipStreamSynchronize(sa));
+  // a gated single launch with nothing queued behind it: its completion word instead of the
+  // stream's completion signal (handoff.cuh gate_done); later work on the stream stays ordered
+  // after it, and nothing of this call reads the pinned buffer any more once the word is set
+  bool done = false;
+  if (gated && nreg == 1 && !(j.kind == HostJob::SENDER_RAW && j.sighash)) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spins = 0; !(done = __atomic_load_n(&gate.w[2], __ATOMIC_ACQUIRE) == gate.seq); ++spins) {
+      cpu_relax();
+      if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+    }
+    if (done) (void)hipStreamQuery(st);  // (lets the runtime retire the launch)
+  }
+  if (!done) {
+    HIPCHK(hipStreamSynchronize(sx));
+    if (sx != st) HIPCHK(hipStreamSynchronize(st));  // (st's last work is already behind sx's events)
+    if (sa != st) HIPCHK(hipStreamSynchronize(sa));
+    if (gated && __atomic_load_n(&gate.w[2], __ATOMIC_ACQUIRE) != gate.seq) {
+      (void)hipMemset(gate.dev + 1, 0, 4);  // (the workgroup count, for the next call)
+      return set_err(EGES_E_HIP, "a gated launch ended without its completion word");
+    }
+  }
   HSTAMP(4);
   drain.armed = false;
   if (gating && __atomic_load_n(&gate.w[1], __ATOMIC_ACQUIRE) != 0u) {

@@ -80,6 +80,26 @@ DEV void gate_wait(const uint32_t* gate, uint32_t* mirror, uint32_t seq) {
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
+// A gated call's completion (capi.hip run_host_shard): after its last output each workgroup
+// counts itself done (system-scope release first); the last one stores the call's sequence into
+// gate[2], which the host polls instead of synchronising the stream (the kernel-end signal's
+// path measured ~5 us from the kernel's end to the sync's return). At kernel level, after the
+// body: every wave of the workgroup reaches the barrier. The mid-size kernels only: on the
+// latency kernels' 1,000-workgroup grids the per-workgroup system-scope release cost more than
+// it saved (C3 0.184-0.188 -> 0.201-0.207 ms, profiles/r04/gate_r04_q.txt).
+template <class P>
+DEV void gate_done(const P& prm) {
+  if (!prm.gate) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    const uint32_t c = __hip_atomic_fetch_add(prm.gate_dev + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (c == gridDim.x - 1) {
+      __hip_atomic_store(prm.gate_dev + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(const_cast<uint32_t*>(prm.gate) + 2, prm.gate_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
 // tests only: workgroup 0's producer of flag k skips publishing it once per launch
 template <class P>
 DEV bool ho_skip(const P& prm, int k) {

@@ -965,6 +965,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
 
 __global__ void __launch_bounds__(MID_WG, 1) recover_bkt_kernel(RecoverParams prm) {
   recover_bkt_body<NoStamp>(prm, nullptr);
+  gate_done(prm);
 }
 
 __global__ void __launch_bounds__(MID_WG, 1) verify_bkt_kernel(RecoverParams prm) {
@@ -973,6 +974,7 @@ __global__ void __launch_bounds__(MID_WG, 1) verify_bkt_kernel(RecoverParams prm
 
 __global__ void __launch_bounds__(MID_WG, 2) recover_mid_kernel(RecoverParams prm) {
   recover_mid_body<NoStamp>(prm, nullptr);
+  gate_done(prm);
 }
 
 size_t mid_ws_bytes_per_block() { return MID_WS_WORDS * sizeof(uint32_t); }
@@ -1009,9 +1011,11 @@ hipError_t launch_recover_mid(const RecoverParams& p, bool bucket, size_t ws_byt
 #ifdef EGES_PHASE_STAMPS
 __global__ void __launch_bounds__(MID_WG, 2) recover_mid_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
   recover_mid_body<Stamper>(prm, stamps);
+  gate_done(prm);
 }
 __global__ void __launch_bounds__(MID_WG, 1) recover_bkt_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
   recover_bkt_body<Stamper>(prm, stamps);
+  gate_done(prm);
 }
 hipError_t launch_recover_mid_stamped(const RecoverParams& p, bool bucket, size_t ws_bytes, hipStream_t st,
                                       uint64_t* stamps) {

@@ -1,8 +1,10 @@
 """Host-buffer calls that launch before their inputs are copied (EGES_GATE = 1, the default:
-capi.hip run_host_shard GateOpen, handoff.cuh gate_wait): the fused latency and mid-size kernels
-wait at the call's gate word while the host copies the inputs into the pinned buffer. Every
-golden recovery and sender item through each form with the gate on and off, byte for byte the
-fixtures, and many back-to-back calls of changing sizes (the gate's sequence advancing per lane)."""
+capi.hip run_host_shard GateOpen, handoff.cuh gate_wait / gate_done): the fused mid-size kernels
+(bucket, windowed) wait at the call's gate word while the host copies the inputs into the pinned
+buffer, and their last workgroup stores the completion word the host waits on. The latency forms
+run ungated either way (measured slower gated). Every golden recovery and sender item through
+each form with the gate on and off, byte for byte the fixtures, and many back-to-back calls of
+changing sizes across the routes (the gate's sequence advancing per call)."""
 import numpy as np
 import pytest
 
