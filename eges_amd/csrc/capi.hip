@@ -927,8 +927,8 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   auto h2d = [&](uint8_t* B, uint8_t* dst, const void* src, size_t bytes) -> int {
     if (!bytes) return EGES_SUCCESS;
     if (pinned) {  // dst points into the pinned buffer (see I below)
-      if (defer) gopen.q[gopen.nq++] = {dst, src, bytes};
-      else std::memcpy(dst, src, bytes);
+      if (defer && gopen.nq < 8) gopen.q[gopen.nq++] = {dst, src, bytes};
+      else std::memcpy(dst, src, bytes);  // (at most 5 inputs per kind: q never fills)
       return EGES_SUCCESS;
     }
     (void)B;
@@ -1737,7 +1737,7 @@ template <class Fill, class Read>
 int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& read,
                  const std::function<void(RecoverParams&)>* base = nullptr,
                  uint32_t want = 0, uint32_t signer = 0, uint64_t cid = 0) {
-  if (knob(r.block ? KNOB_RESIDENT_BLOCK : KNOB_RESIDENT) == 0 || n == 0) return -1;
+  if (knob(r.block ? KNOB_RESIDENT_BLOCK : KNOB_RESIDENT) == 0 || n == 0 || (r.block && !base)) return -1;
   // the test-only knobs act on launches: their runs take the lanes
   if (knob(KNOB_FORCE_REDO) != 0 || knob(KNOB_TEST_SKIP_FLAG) != 0 || knob(KNOB_ROOT_HELPERS) == 0) return -1;
   const uint32_t cap = resident_cap(d, r.block);
