@@ -508,6 +508,7 @@ def measure_block(c, n, raw_mode, warmup, iters, cpu=True):
     ok = ok and bool((sd == 0).all().item()) and np.array_equal(ad.cpu().numpy(), exp_h)
     out = {"median_ms": round(float(np.median(lat)), 3), "p99_ms": round(float(np.percentile(lat, 99)), 3),
            "blocks": iters, "txs": n, "correct": ok,
+           "native_caller": None if raw_mode else native_block(n, iters),
            "roofline": roofline(n / (kms / 1e3), W_RECOVER, n, kms, kernel="eges::recover_lat_kernel"),
            "path": ("wire-format txdata RLP through eges_sender_raw_batch (H2D + decode + sighash RLP/Keccak + "
                     "recovery kernels + D2H)" if raw_mode else "host buffers through eges_sender_batch (H2D + "
@@ -532,6 +533,22 @@ def measure_block(c, n, raw_mode, warmup, iters, cpu=True):
     return out
 
 
+def native_block(n, iters):
+    """The same block size through eges_sender_batch from a native caller (tools/block_bench, built
+    by build(): preallocated host buffers, every result checked), as a child process on the same
+    GPU: what a cgo caller pays per block, without the Python ctypes call's own overhead."""
+    exe = os.path.join(ROOT, "tools", "block_bench")
+    if not os.path.exists(exe):
+        return None
+    try:
+        cp = subprocess.run([exe, str(n), str(max(iters, 300))], capture_output=True, text=True, timeout=120)
+        m = json.loads(cp.stdout.strip().splitlines()[-1])
+        return {"median_ms": round(m["median_ms"], 4), "p99_ms": round(m["p99_ms"], 4), "blocks": m["iters"],
+                "correct": m["errors"] == 0 and cp.returncode == 0, "path": "tools/block_bench (C++ caller)"}
+    except Exception as e:  # noqa: BLE001
+        return {"note": f"block_bench failed: {e}"}
+
+
 def run_block_latency(c):
     a = c.args
     n = a.batch or 1000
@@ -545,8 +562,9 @@ def run_block_latency(c):
             "higher_is_better": False, "dtype": "u32", "data": "synthetic",
             "config": {"workload": "configs[2]: Geec block import, 1000 txns/block (txnSize 100), EIP155Signer(930412), "
                                    + m["path"], "correct": m["correct"]}, "roofline": m.get("roofline"),
-            "cpu_baseline": m.get("cpu")}
-    c.finish(line, m["correct"])
+            "cpu_baseline": m.get("cpu"), "native_caller": m.get("native_caller")}
+    nc = m.get("native_caller") or {}
+    c.finish(line, m["correct"] and nc.get("correct", True))
 
 
 # ------------------------------------------------------------------ single-item seam
