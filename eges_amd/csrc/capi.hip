@@ -77,8 +77,9 @@ int env_int(const char* name, int dflt) {
 // single-chunk host calls that run on the latency kernel (which needs no shared workspace) do
 // not queue behind each other on the device mutex.
 constexpr int NLANES = 4;
-// A host-buffer call's input gate (handoff.cuh gate_wait): word 0 the last sequence opened,
-// word 1 set by a wave whose wait ran out. Coherent pinned memory, one per lane / device.
+// A host-buffer call's input gate (handoff.cuh gate_wait / gate_done): word 0 the last sequence
+// opened, word 1 set by a wave whose wait ran out, word 2 the last completed sequence. Coherent
+// pinned memory, one per device (the gated mid-size calls hold the device mutex).
 struct Gate {
   uint32_t* w = nullptr;
   uint32_t* dev = nullptr;  // device word: workgroup 0's mirror of the opened sequence
@@ -93,7 +94,6 @@ struct Lane {
   uint8_t* buf = nullptr;
   size_t buf_cap = 0;
   uint8_t* pin = nullptr;
-  Gate gate;
   hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_k[2] = {nullptr, nullptr};
 };
 
@@ -396,8 +396,6 @@ Dev::~Dev() {
     if (l.stream) (void)hipStreamSynchronize(l.stream);
     if (l.buf) (void)hipFree(l.buf);
     if (l.pin) (void)hipHostFree(l.pin);
-    if (l.gate.w) (void)hipHostFree(l.gate.w);
-    if (l.gate.dev) (void)hipFree(l.gate.dev);
     for (int r = 0; r < 2; ++r) {
       if (l.ev_in[r]) (void)hipEventDestroy(l.ev_in[r]);
       if (l.ev_k[r]) (void)hipEventDestroy(l.ev_k[r]);
@@ -869,8 +867,8 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   // the kernels wait at the gate (handoff.cuh gate_wait), which opens after the copies. Opening is
   // also the guard's destructor, so no return path leaves a launched kernel waiting (declared
   // after `drain`: it runs first).
-  Gate& gate = small ? lane->gate : d.gate;
-  const bool gating = pinned && knob(KNOB_GATE) != 0 &&
+  Gate& gate = d.gate;  // (the mid-size kernels run above EGES_LAT_MAX: never on a lane)
+  const bool gating = pinned && !small && knob(KNOB_GATE) != 0 &&
                       (j.kind == HostJob::RECOVER || j.kind == HostJob::SENDER || (j.kind == HostJob::SENDER_RAW && !j.decode_only));
   if (gating && !gate.w) {
     if (hipHostMalloc(&gate.w, 64, hipHostMallocCoherent) != hipSuccess) {
