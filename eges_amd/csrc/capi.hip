@@ -94,6 +94,7 @@ struct Lane {
   uint8_t* buf = nullptr;
   size_t buf_cap = 0;
   uint8_t* pin = nullptr;
+  uint32_t* vfault = nullptr;  // coherent pinned: a VerifySignature call's hand-off fault word
   hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_k[2] = {nullptr, nullptr};
 };
 
@@ -101,20 +102,15 @@ struct Lane {
 // split-form workgroups polling a job word in coherent pinned memory (resident_run below).
 struct Resident {
   std::mutex mu;  // one job at a time; a group that finds it busy takes a lane instead
-  bool block = false;  // the block server (narrow form, lane 1) or the single-call one (split, lane 0)
   int lane = 0;
   hipStream_t stream = nullptr;
   ResidentJob* job = nullptr;  // coherent pinned
-  uint8_t* data = nullptr;     // coherent pinned, resident_layout / resident_block_layout (cap)
-  uint32_t* counter = nullptr;  // device, 2 words
-  uint32_t* scratch = nullptr;  // block server: record / root rows (device)
+  uint8_t* data = nullptr;     // pinned, resident_layout (cap)
+  uint32_t* counter = nullptr;  // device, 2 words + the job mirror
   uint32_t cap = 0, wgs = 0;
   bool running = false;  // (guarded by mu; while true, the stream's lane is reserved)
   uint32_t seq = 0;  // the last job handed over (== job->done once served)
   uint32_t inst = 0;  // launches so far (each launch's id, nonzero)
-  // block server: the configuration its queued launches were made for (kind, outputs, signer, chain id)
-  uint32_t cfg_kind = ~0u, cfg_want = 0, cfg_signer = 0;
-  uint64_t cfg_cid = 0;
   std::chrono::steady_clock::time_point last_use{};
 };
 struct Dev {
@@ -133,22 +129,17 @@ struct Dev {
   size_t buf_cap = 0;
   uint8_t* pin = nullptr;  // pinned host staging of single-chunk host-buffer calls (PIN_BYTES)
   Gate gate;               //   and their input gate
+  uint32_t* vfault = nullptr;  // coherent pinned: a VerifySignature call's hand-off fault word
   // overlapped recover launches (EGES_OVERLAP): a second stream, workspace and its events
   hipStream_t aux = nullptr;
   uint32_t* ws2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  // pipelined host-buffer calls (run_host_pipe): H2D / D2H streams, two pinned staging slots
-  hipStream_t hin = nullptr, hout = nullptr;
-  hipEvent_t ev_out[2] = {nullptr, nullptr};
-  uint8_t* ring[2] = {nullptr, nullptr};
-  size_t ring_cap = 0;
   std::mutex mu;
+  // device-wide calls in progress (DeviceWide): while nonzero, or while their last enqueued work
+  // (`last`) is still pending, the resident server takes no job and is not relaunched
+  std::atomic<int> wide{0};
   Lane lanes[NLANES];
-  Resident res, res_blk;
-  Dev() {
-    res_blk.block = true;
-    res_blk.lane = 1;
-  }
+  Resident res;
   ~Dev();
 };
 using DevPtr = std::shared_ptr<Dev>;
@@ -174,7 +165,7 @@ struct KnobDef {
 #ifndef EGES_MID_MAX_DEFAULT
 #define EGES_MID_MAX_DEFAULT 40000
 #endif
-const KnobDef KNOB_DEFS[KNOB_COUNT] = {
+const KnobDef KNOB_DEFS[] = {
     {"EGES_LAT_MAX", EGES_LAT_MAX_DEFAULT},
     {"EGES_LAT_WIDE_MAX", 256},
     {"EGES_MID_MAX", EGES_MID_MAX_DEFAULT},
@@ -188,24 +179,17 @@ const KnobDef KNOB_DEFS[KNOB_COUNT] = {
     {"EGES_COALESCE_SPIN_US", 2000},
     {"EGES_COALESCE_SPINNERS", 8},
     {"EGES_SENDER_FUSED", 1},
-    {"EGES_HOST_PIPE", 0},
-    {"EGES_PIPE_CHUNK", 786432},
-    {"EGES_PIPE_FIRST", 262144},
-    {"EGES_PIPE_STREAMS", 1},
     {"EGES_LAT_TRI_MAX", 448},
-    {"EGES_PIPE_SEG", 8 << 20},
     {"EGES_HOST_PARTS", EGES_PIPE_PARTS},
     {"EGES_TEST_SKIP_FLAG", 0},
     {"EGES_TEST_DELAY_X", 0},
-    {"EGES_HOST_STREAMS", 1},
     {"EGES_RESIDENT", 1},
     {"EGES_RESIDENT_WGS", 16},
     {"EGES_RESIDENT_CAP", 64},
     {"EGES_RESIDENT_IDLE_MS", 4},
-    {"EGES_RESIDENT_BLOCK", 0},
-    {"EGES_RESIDENT_BLOCK_CAP", 1024},
     {"EGES_GATE", 1},
 };
+static_assert(sizeof(KNOB_DEFS) / sizeof(KNOB_DEFS[0]) == KNOB_COUNT, "a name and default for every knob");
 std::atomic<long long> g_knob[KNOB_COUNT];
 std::once_flag g_knob_once;
 
@@ -230,11 +214,8 @@ int knob_index(const char* name) {
 struct Route {
   size_t lat_max = 0, mid_max = 0;
   uint32_t wide_max = 0, tri_max = 0;
-  long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, host_pipe = 1;
-  size_t pipe_chunk = 786432, pipe_first = 262144;
-  long long pipe_streams = 1;
-  size_t host_parts = EGES_PIPE_PARTS, pipe_seg = size_t(8) << 20;
-  long long host_streams = 1;
+  long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, gate = 1;
+  size_t host_parts = EGES_PIPE_PARTS;
   uint32_t force_redo = 0, skip_flag = 0, delay_x = 0;
   static Route now() {
     Route r;
@@ -245,13 +226,8 @@ struct Route {
     r.wire_fused = knob(KNOB_WIRE_FUSED);
     r.overlap = knob(KNOB_OVERLAP);
     r.sender_fused = knob(KNOB_SENDER_FUSED);
-    r.host_pipe = knob(KNOB_HOST_PIPE);
-    r.pipe_chunk = (size_t)std::max<long long>(64, knob(KNOB_PIPE_CHUNK));
-    r.pipe_first = (size_t)std::max<long long>(64, knob(KNOB_PIPE_FIRST));
-    r.pipe_streams = knob(KNOB_PIPE_STREAMS);
+    r.gate = knob(KNOB_GATE);
     r.tri_max = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_LAT_TRI_MAX), 1u << 30));
-    r.pipe_seg = (size_t)std::max<long long>(1 << 20, knob(KNOB_PIPE_SEG));
-    r.host_streams = knob(KNOB_HOST_STREAMS);
     r.host_parts = (size_t)std::max<long long>(2, std::min<long long>(knob(KNOB_HOST_PARTS), 64));
     r.force_redo = knob(KNOB_FORCE_REDO) != 0 ? 1u : 0u;
     r.skip_flag = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TEST_SKIP_FLAG), 64));
@@ -263,6 +239,8 @@ static int overlap_parts(const Route& rt, size_t n) {
   if (rt.overlap >= 0) return (int)std::min<long long>(rt.overlap, 64);
   return n > CHUNK ? 2 : 0;
 }
+
+void resident_stop(Dev& d);
 
 std::mutex g_mu;
 std::vector<DevPtr> g_devs;
@@ -354,16 +332,12 @@ int init_device(int id, DevPtr* out) {
 
 // Resources go when the last reference does: eges_shutdown drops the registry's references,
 // and a call still in flight keeps its device alive until it returns.
-void resident_stop(Dev& d);
 Dev::~Dev() {
   DevGuard g(id);
-  resident_stop(*this);  // (their streams are lanes 0 and 1's)
-  for (Resident* r : {&res, &res_blk}) {
-    if (r->job) (void)hipHostFree(r->job);
-    if (r->data) (void)hipHostFree(r->data);
-    if (r->counter) (void)hipFree(r->counter);
-    if (r->scratch) (void)hipFree(r->scratch);
-  }
+  resident_stop(*this);  // (its stream is lane 0's)
+  if (res.job) (void)hipHostFree(res.job);
+  if (res.data) (void)hipHostFree(res.data);
+  if (res.counter) (void)hipFree(res.counter);
   if (stream) (void)hipStreamSynchronize(stream);
   if (last) (void)hipEventSynchronize(last);  // the last engine work, on whichever stream the caller gave
   if (gtab) (void)hipFree(gtab);
@@ -372,6 +346,7 @@ Dev::~Dev() {
   if (buf) (void)hipFree(buf);
   if (pin) (void)hipHostFree(pin);
   if (gate.w) (void)hipHostFree(gate.w);
+  if (vfault) (void)hipHostFree(vfault);
   if (gate.dev) (void)hipFree(gate.dev);
   if (last) (void)hipEventDestroy(last);
   for (int r = 0; r < 2; ++r) {
@@ -386,16 +361,11 @@ Dev::~Dev() {
     (void)hipEventDestroy(ev_join);
     (void)hipFree(ws2);
   }
-  if (hin) (void)hipStreamSynchronize(hin), (void)hipStreamDestroy(hin);
-  if (hout) (void)hipStreamSynchronize(hout), (void)hipStreamDestroy(hout);
-  for (int r = 0; r < 2; ++r) {
-    if (ev_out[r]) (void)hipEventDestroy(ev_out[r]);
-    if (ring[r]) (void)hipHostFree(ring[r]);
-  }
   for (Lane& l : lanes) {
     if (l.stream) (void)hipStreamSynchronize(l.stream);
     if (l.buf) (void)hipFree(l.buf);
     if (l.pin) (void)hipHostFree(l.pin);
+    if (l.vfault) (void)hipHostFree(l.vfault);
     for (int r = 0; r < 2; ++r) {
       if (l.ev_in[r]) (void)hipEventDestroy(l.ev_in[r]);
       if (l.ev_k[r]) (void)hipEventDestroy(l.ev_k[r]);
@@ -427,6 +397,24 @@ struct Serial {
   hipStream_t st;
   Serial(Dev& dev, hipStream_t s) : d(dev), st(s) { (void)hipStreamWaitEvent(st, d.last, 0); }
   ~Serial() { (void)hipEventRecord(d.last, st); }
+};
+
+// Device-wide work (lane-serial and mid-size batches, the device-resident entries, synthesis):
+// counted in d.wide first, so the resident server can be neither handed a job nor relaunched
+// from then on; then the server is stopped (it would otherwise hold CUs the device-wide kernels
+// are sized for) and the device mutex taken.
+struct DeviceWide {
+  Dev& d;
+  std::unique_lock<std::mutex> lk;
+  explicit DeviceWide(Dev& dv) : d(dv) {
+    d.wide.fetch_add(1, std::memory_order_acq_rel);
+    resident_stop(d);
+    lk = std::unique_lock<std::mutex>(d.mu);
+  }
+  ~DeviceWide() {
+    lk.unlock();
+    d.wide.fetch_sub(1, std::memory_order_acq_rel);
+  }
 };
 
 // The device's diagnostic counters and the test-only knobs, on every launch's parameters.
@@ -524,9 +512,9 @@ hipError_t launch_recover_pass(Dev& d, const Route& rt, const RecoverParams& p0,
   RecoverParams p = with_diag(d, p0, rt);
   // the split form (four waves per signature) while the batch leaves SIMDs idle, then the
   // three-wave form, then the narrow form (k_recover_lat.hip FORM_*)
-  // (the three-wave form only while its workgroups and the root helpers fit one generation at
-  // its occupancy of 3 waves per SIMD)
-  const bool tri = p.n <= rt.tri_max && 3 * (size_t)p.n + 2 * ((p.n + 127) / 128) <= (size_t)d.cus * 4 * 3;
+  // (the three-wave form only while its workgroups and the root helpers, three waves each, fit
+  // one generation at its occupancy of 3 waves per SIMD)
+  const bool tri = p.n <= rt.tri_max && 3 * (size_t)p.n + 3 * ((p.n + 127) / 128) <= (size_t)d.cus * 4 * 3;
   p.wide = p.n <= rt.wide_max ? 1u : tri ? 2u : 0u;
   const bool mid = use_mid(d, rt, p.n);
   if (p.wire_raw && !(mid ? mid_bucket(d, rt, p.n) : p.n <= rt.lat_max)) return hipErrorInvalidValue;  // wire_fused() decides
@@ -781,21 +769,8 @@ Region region_for(const HostJob& j, size_t base, size_t m) {
 // compute stream runs chunk i, the copy stream stages chunk i+1's inputs and returns chunk
 // i-1's outputs (host order H2D(i+1), K(i+1), D2H(i): the pageable D2H blocks this thread
 // until K(i) is done, by which time K(i+1) is queued behind it). Synchronous overall.
-int run_host_pipe(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t cnt);
-int resident_block_run(Dev& d, const HostJob& j, size_t off, size_t n);
 int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t cnt) {
   HSTAMP(0);
-  // blocks for the latency kernel's narrow form (above the three-wave form's range): the resident
-  // block server, when it is on and free (no launch, dispatch or completion signal per block)
-  if ((j.kind == HostJob::RECOVER || j.kind == HostJob::SENDER) && cnt <= rt.lat_max &&
-      cnt > std::max<size_t>(rt.wide_max, rt.tri_max)) {
-    const int rc = resident_block_run(d, j, off, cnt);
-    if (rc >= 0) return rc;
-  }
-  // (EGES_HOST_PIPE = 2: tests force the pipeline for any batch larger than its first chunk)
-  if (j.kind != HostJob::SENDER_RAW &&
-      ((rt.host_pipe == 1 && cnt >= 2 * PIPE_MIN) || (rt.host_pipe == 2 && cnt > rt.pipe_first)))
-    return run_host_pipe(d, rt, j, off, cnt);
   DevGuard g(d.id);
   // a shard big enough to pipeline runs as >= 2 chunks (each still a full resident grid)
   size_t c = std::min(CHUNK, cnt);
@@ -810,6 +785,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   const bool small = pinned && cnt <= rt.lat_max;
   Lane* lane = nullptr;
   std::unique_lock<std::mutex> lk;
+  std::unique_ptr<DeviceWide> wide;
   if (small) {
     for (Lane& l : d.lanes) {
       std::unique_lock<std::mutex> t(l.mu, std::try_to_lock);
@@ -828,8 +804,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       lk = std::move(t);
     }
   } else {
-    resident_stop(d);  // device-wide work: the resident server leaves the CUs first
-    lk = std::unique_lock<std::mutex>(d.mu);
+    wide = std::make_unique<DeviceWide>(d);  // device-wide work: the resident server leaves the CUs first
   }
   uint8_t*& dbuf = small ? lane->buf : d.buf;
   uint8_t*& pin = small ? lane->pin : d.pin;
@@ -840,24 +815,18 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   if (rc) return rc;
   // a single chunk has nothing to overlap: one stream, no cross-stream waits (C3 latency)
   hipStream_t st = small ? lane->stream : d.stream, sx = nreg > 1 ? d.copy : st;
-  // EGES_HOST_STREAMS = 2: the chunks' kernels alternate between the device's two compute
-  // streams and workspaces, so one chunk's launch can start in the previous one's tail
-  const bool two = nreg > 1 && rt.host_streams >= 2;
-  if (two && (rc = ensure_aux(d))) return rc;
-  hipStream_t sa = two ? d.aux : st;
   // Every return after this point (errors included) first drains every stream, so the lane /
   // device mutex is never released while kernels or copies of this call still touch its
   // pinned staging or scratch (the next caller writes its inputs there).
   struct Drain {
-    hipStream_t a, b, c;
+    hipStream_t a, b;
     bool armed;
     ~Drain() {
       if (!armed) return;
       (void)hipStreamSynchronize(a);
       if (b != a) (void)hipStreamSynchronize(b);
-      if (c != a) (void)hipStreamSynchronize(c);
     }
-  } drain{st, sx, sa, true};
+  } drain{st, sx, true};
   if (pinned && !pin && hipHostMalloc(&pin, PIN_BYTES, hipHostMallocDefault) != hipSuccess) {
     pin = nullptr;
     return set_err(EGES_E_NOMEM, "hipHostMalloc(%zu) failed", PIN_BYTES);
@@ -868,7 +837,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   // also the guard's destructor, so no return path leaves a launched kernel waiting (declared
   // after `drain`: it runs first).
   Gate& gate = d.gate;  // (the mid-size kernels run above EGES_LAT_MAX: never on a lane)
-  const bool gating = pinned && !small && knob(KNOB_GATE) != 0 &&
+  const bool gating = pinned && !small && rt.gate != 0 &&
                       (j.kind == HostJob::RECOVER || j.kind == HostJob::SENDER || (j.kind == HostJob::SENDER_RAW && !j.decode_only));
   if (gating && !gate.w) {
     if (hipHostMalloc(&gate.w, 64, hipHostMallocCoherent) != hipSuccess) {
@@ -912,10 +881,18 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     gopen.w = gate.w;
     gopen.seq = gate.seq;
   };
+  // VerifySignature: a hand-off fault leaves its item's ok byte 0 and stores 1 into this word
+  uint32_t*& vfault = small ? lane->vfault : d.vfault;
+  if (j.kind == HostJob::VERIFY) {
+    if (!vfault && hipHostMalloc(&vfault, 64, hipHostMallocCoherent) != hipSuccess) {
+      vfault = nullptr;
+      return set_err(EGES_E_NOMEM, "hipHostMalloc(fault word) failed");
+    }
+    __atomic_store_n(vfault, 0u, __ATOMIC_RELAXED);
+  }
   if (!small) {
     HIPCHK(hipStreamWaitEvent(st, d.last, 0));
     HIPCHK(hipStreamWaitEvent(sx, d.last, 0));
-    if (two) HIPCHK(hipStreamWaitEvent(sa, d.last, 0));
   }
   HSTAMP(1);
   // Input staging: each input array goes to its offset in the region, either by its own
@@ -994,8 +971,8 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     const size_t m = std::min(c, off + cnt - base);
     const size_t m_pad = align_up(m, 64);
     const int r = ci % nreg;
-    hipStream_t sk = (two && r) ? sa : st;         // this chunk's compute stream
-    uint32_t* wsk = (two && r) ? d.ws2 : d.ws;     //   and workspace
+    hipStream_t sk = st;  // this chunk's compute stream
+    uint32_t* wsk = d.ws;
     const Region rg = region_for(j, base, m);
     uint8_t* B = dbuf + (size_t)r * worst;
     uint8_t* I = pinned ? pin : B;  // where the kernels read the inputs
@@ -1105,6 +1082,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       VerifyParams p{dp, dl, dm, ds, (uint32_t)m, o_st, d.gtab, wsk};
       verify_scratch_bind(p, B + rg.o_rec, m_pad);
       p = with_diag(d, p, rt);
+      p.fault = vfault;
       // small (lane) calls must not touch the device's shared workspace: latency kernel
       HIPCHK(launch_verify_any(d, rt, p, small, sk));
     }
@@ -1140,7 +1118,6 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   if (!done) {
     HIPCHK(hipStreamSynchronize(sx));
     if (sx != st) HIPCHK(hipStreamSynchronize(st));  // (st's last work is already behind sx's events)
-    if (sa != st) HIPCHK(hipStreamSynchronize(sa));
     if (gated && __atomic_load_n(&gate.w[2], __ATOMIC_ACQUIRE) != gate.seq) {
       (void)hipMemset(gate.dev + 1, 0, 4);  // (the workgroup count, for the next call)
       return set_err(EGES_E_HIP, "a gated launch ended without its completion word");
@@ -1154,6 +1131,8 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   }
   if (pinned && have_prev) unpack(prev);
   HSTAMP(5);
+  if (j.kind == HostJob::VERIFY && __atomic_load_n(vfault, __ATOMIC_ACQUIRE) != 0u)
+    return set_err(EGES_E_HIP, "a kernel hand-off timed out (items read invalid; EGES_DIAG_HANDOFF)");
   // items a kernel marked EGES_ENGINE_FAULT (a wave hand-off timed out, handoff.cuh) have no
   // result: the call fails rather than return them
   if (j.status && !j.decode_only && std::memchr(j.status + off, EGES_ENGINE_FAULT, cnt))
@@ -1295,217 +1274,6 @@ class CopyPool {
   uint64_t gen_ = 0;
   std::atomic<int> active_{0};
 };
-
-// A multi-chunk host-buffer call (RECOVER / SENDER / VERIFY / PRECOMPILE) as a four-stage
-// pipeline over chunks: host copy into a pinned slot (CopyPool) -> DMA to the device (stream
-// hin) -> kernels (two compute streams alternating, each with its own workspace, so one chunk's
-// launch starts while the previous one's last waves drain) -> DMA back into the pinned slot
-// (stream hout) -> host copy into the caller's outputs. Two slots alternate. The first chunk is
-// smaller (EGES_PIPE_FIRST), so the GPU starts after a short copy. Synchronous overall.
-struct PipeArr {
-  const uint8_t* src;
-  uint8_t* dst;
-  size_t w;  // bytes per item
-};
-int run_host_pipe(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t cnt) {
-  DevGuard g(d.id);
-  resident_stop(d);
-  std::unique_lock<std::mutex> lk(d.mu);
-  // chunk schedule: a smaller first chunk, then near-equal chunks of at most rt.pipe_chunk
-  std::vector<std::pair<size_t, size_t>> ch;
-  {
-    const size_t C = std::max<size_t>(64, std::min(rt.pipe_chunk, CHUNK));
-    const size_t f = std::min(cnt, std::max<size_t>(64, std::min(rt.pipe_first, C)));
-    ch.push_back({off, f});
-    const size_t rem = cnt - f;
-    const size_t parts = (rem + C - 1) / C;
-    for (size_t k = 0, b = off + f; k < parts; ++k) {
-      const size_t m = rem / parts + (k < rem % parts ? 1 : 0);
-      ch.push_back({b, m});
-      b += m;
-    }
-  }
-  size_t cmax = 0;
-  for (auto& c : ch) cmax = std::max(cmax, c.second);
-  // per-item inputs and outputs of the kind (in the order the kernels read them from the region)
-  std::vector<PipeArr> in, out;
-  const size_t astride = j.kind == HostJob::PRECOMPILE ? 32 : 20;
-  switch (j.kind) {
-    case HostJob::RECOVER:
-      in = {{j.a, nullptr, 32}, {j.b, nullptr, 65}};
-      break;
-    case HostJob::SENDER:
-      in = {{j.a, nullptr, 32}, {j.b, nullptr, 32}, {j.c, nullptr, 32}, {j.d, nullptr, 32}};
-      if (j.e) in.push_back({j.e, nullptr, 1});
-      break;
-    case HostJob::VERIFY:
-      in = {{j.a, nullptr, 65}, {j.b, nullptr, 1}, {j.c, nullptr, 32}, {j.d, nullptr, 64}};
-      break;
-    case HostJob::PRECOMPILE:
-      in = {{j.a, nullptr, 128}};
-      if (j.inlen) in.push_back({reinterpret_cast<const uint8_t*>(j.inlen), nullptr, 4});
-      break;
-    default:
-      return set_err(EGES_E_INVALID_ARG, "run_host_pipe: unsupported kind");
-  }
-  if (j.pub) out.push_back({nullptr, j.pub, 65});
-  if (j.addr) out.push_back({nullptr, j.addr, astride});
-  out.push_back({nullptr, j.status, 1});
-  size_t in_w = 0, out_w = 0;
-  for (auto& a : in) in_w += a.w;
-  for (auto& a : out) out_w += a.w;
-  // device region per slot: inputs | record / verify scratch | outputs
-  const size_t cpad = align_up(cmax, 64);
-  const size_t rec_bytes = j.kind == HostJob::VERIFY ? verify_scratch_bytes(cpad) : recover_scratch_bytes(cpad);
-  const size_t o_rec = align_up(cmax * in_w + 256 * in.size(), 256);
-  const size_t o_out = o_rec + align_up(rec_bytes, 256);
-  const size_t R = align_up(o_out + cmax * out_w + 256 * out.size(), 256);
-  int rc = dev_ensure_buf(d, 2 * R);
-  if (rc) return rc;
-  if (!d.aux) {
-    HIPCHK(hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&d.ev_fork, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&d.ev_join, hipEventDisableTiming));
-    HIPCHK(hipMalloc(&d.ws2, ws_bytes_per_block() * (size_t)d.ws_blocks));
-  }
-  if (!d.hin) {
-    HIPCHK(hipStreamCreateWithFlags(&d.hin, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&d.hout, hipStreamNonBlocking));
-    for (int r = 0; r < 2; ++r) HIPCHK(hipEventCreateWithFlags(&d.ev_out[r], hipEventDisableTiming));
-  }
-  const size_t slot = align_up(cmax * in_w + 256 * in.size(), 256) + align_up(cmax * out_w + 256 * out.size(), 256);
-  if (slot > d.ring_cap) {
-    for (int r = 0; r < 2; ++r) {
-      if (d.ring[r]) HIPCHK(hipHostFree(d.ring[r]));
-      d.ring[r] = nullptr;
-    }
-    d.ring_cap = 0;
-    for (int r = 0; r < 2; ++r)
-      if (hipHostMalloc(&d.ring[r], slot, hipHostMallocDefault) != hipSuccess)
-        return set_err(EGES_E_NOMEM, "hipHostMalloc(%zu) failed", slot);
-    d.ring_cap = slot;
-  }
-  const size_t pin_out = align_up(cmax * in_w + 256 * in.size(), 256);
-  // One compute stream by default: two lane-serial launches running concurrently double the
-  // per-lane R-table working set past the Infinity Cache (profiles/r04: 78-81 vs 84 M sigs/s);
-  // EGES_PIPE_STREAMS = 2 alternates d.stream / d.aux with their own workspaces (A/B).
-  const bool two = rt.pipe_streams >= 2;
-  hipStream_t cs[2] = {d.stream, two ? d.aux : d.stream};
-  uint32_t* wsr[2] = {d.ws, two ? d.ws2 : d.ws};
-  struct Drain {
-    hipStream_t s[4];
-    bool armed;
-    ~Drain() {
-      if (!armed) return;
-      for (hipStream_t x : s) (void)hipStreamSynchronize(x);
-    }
-  } drain{{d.hin, cs[0], cs[1], d.hout}, true};  // (cs[1] may equal cs[0]: synchronising twice is harmless)
-  for (hipStream_t x : {d.hin, cs[0], cs[1], d.hout}) HIPCHK(hipStreamWaitEvent(x, d.last, 0));
-  // offsets of each array inside a slot's input / output block, for a chunk of m items
-  auto offs = [](const std::vector<PipeArr>& v, size_t m) {
-    std::vector<size_t> o;
-    size_t x = 0;
-    for (const PipeArr& a : v) {
-      o.push_back(x);
-      x = align_up(x + m * a.w, 256);
-    }
-    o.push_back(x);  // total
-    return o;
-  };
-  auto copy_out = [&](size_t ci) {
-    const size_t base = ch[ci].first, m = ch[ci].second;
-    const auto oo = offs(out, m);
-    std::vector<CopyPool::Task> t;
-    for (size_t k = 0; k < out.size(); ++k)
-      t.push_back({out[k].dst + base * out[k].w, d.ring[ci & 1] + pin_out + oo[k], m * out[k].w});
-    CopyPool::get().run(t);
-  };
-  for (size_t ci = 0; ci < ch.size(); ++ci) {
-    const int r = (int)(ci & 1);
-    const size_t base = ch[ci].first, m = ch[ci].second, m_pad = align_up(m, 64);
-    uint8_t* B = d.buf + (size_t)r * R;
-    uint8_t* P = d.ring[r];
-    const auto io = offs(in, m), oo = offs(out, m);
-    // 1. host copy into the pinned slot (free: chunk ci - 2 was copied out in iteration ci - 1)
-    //    and 2. DMA in (after the kernels of chunk ci - 2, same device region), segment by
-    //    segment, so that the copies and the DMA overlap
-    if (ci >= 2) HIPCHK(hipStreamWaitEvent(d.hin, d.ev_k[r], 0));
-    {
-      std::vector<CopyPool::Task> t;
-      for (size_t k = 0; k < in.size(); ++k) t.push_back({P + io[k], in[k].src + base * in[k].w, m * in[k].w});
-      hipError_t e = hipSuccess;
-      CopyPool::get().run_segments(t, rt.pipe_seg, [&](size_t k, size_t o, size_t nb) {
-        if (e == hipSuccess) e = hipMemcpyAsync(B + io[k] + o, P + io[k] + o, nb, hipMemcpyHostToDevice, d.hin);
-      });
-      HIPCHK(e);
-    }
-    HIPCHK(hipEventRecord(d.ev_in[r], d.hin));
-    // 3. kernels on this slot's compute stream and workspace
-    hipStream_t st = cs[r];
-    HIPCHK(hipStreamWaitEvent(st, d.ev_in[r], 0));
-    uint32_t* rec = reinterpret_cast<uint32_t*>(B + o_rec);
-    uint8_t* O = B + o_out;
-    uint8_t* o_pub = nullptr;
-    uint8_t* o_addr = nullptr;
-    uint8_t* o_st = nullptr;
-    {
-      size_t k = 0;
-      if (j.pub) o_pub = O + oo[k++];
-      if (j.addr) o_addr = O + oo[k++];
-      o_st = O + oo[k];
-    }
-    const uint8_t* I[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    for (size_t k = 0; k < in.size(); ++k) I[k] = B + io[k];
-    if (j.kind == HostJob::RECOVER) {
-      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, o_pub, d.gtab, wsr[r]};
-      if (fused_parse(d, rt, m)) {
-        p.raw_msg = I[0];
-        p.raw_sig = I[1];
-      } else {
-        HIPCHK(launch_prep_ecrecover(I[0], I[1], (uint32_t)m, (uint32_t)m_pad, rec, st));
-      }
-      HIPCHK(launch_recover_pass(d, rt, p, st));
-    } else if (j.kind == HostJob::SENDER) {
-      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, wsr[r]};
-      const uint8_t* vf = j.e ? I[4] : nullptr;
-      if (sender_fused(d, rt, m, {I[0], I[1], I[2], I[3]}))
-        bind_sender_rows(p, I[0], I[1], I[2], I[3], vf, j.signer, j.chain_id);
-      else
-        HIPCHK(launch_prep_sender(I[0], I[1], I[2], I[3], vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, st));
-      HIPCHK(launch_recover_pass(d, rt, p, st));
-    } else if (j.kind == HostJob::PRECOMPILE) {
-      HIPCHK(hipMemsetAsync(o_addr, 0, m * 32, st));
-      HIPCHK(launch_prep_precompile(I[0], j.inlen ? reinterpret_cast<const uint32_t*>(I[1]) : nullptr, (uint32_t)m,
-                                    (uint32_t)m_pad, rec, st));
-      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr + 12, nullptr, d.gtab, wsr[r], 32};
-      HIPCHK(launch_recover_pass(d, rt, p, st));
-    } else {
-      VerifyParams p{I[0], I[1], I[2], I[3], (uint32_t)m, o_st, d.gtab, wsr[r]};
-      verify_scratch_bind(p, B + o_rec, m_pad);
-      p = with_diag(d, p, rt);
-      HIPCHK(launch_verify_any(d, rt, p, false, st));
-    }
-    HIPCHK(hipEventRecord(d.ev_k[r], st));
-    // 4. DMA out into the pinned slot
-    HIPCHK(hipStreamWaitEvent(d.hout, d.ev_k[r], 0));
-    HIPCHK(hipMemcpyAsync(P + pin_out, O, oo.back(), hipMemcpyDeviceToHost, d.hout));
-    HIPCHK(hipEventRecord(d.ev_out[r], d.hout));
-    // 5. the previous chunk's outputs into the caller's buffers, while this chunk computes
-    if (ci >= 1) {
-      HIPCHK(hipEventSynchronize(d.ev_out[r ^ 1]));
-      copy_out(ci - 1);
-    }
-  }
-  const size_t last = ch.size() - 1;
-  HIPCHK(hipEventSynchronize(d.ev_out[last & 1]));
-  copy_out(last);
-  for (hipStream_t x : {d.hin, cs[0], cs[1], d.hout}) HIPCHK(hipStreamSynchronize(x));
-  drain.armed = false;
-  HIPCHK(hipEventRecord(d.last, d.hout));
-  if (j.status && std::memchr(j.status + off, EGES_ENGINE_FAULT, cnt))
-    return set_err(EGES_E_HIP, "a kernel hand-off timed out (EGES_ENGINE_FAULT items; EGES_DIAG_HANDOFF)");
-  return EGES_SUCCESS;
-}
 
 // Contiguous index shards across the engine's devices.
 int run_host(const HostJob& j, size_t n) {
@@ -1709,39 +1477,26 @@ void resident_halt(Dev& d, Resident& r) {  // r.mu held
   d.lanes[r.lane].reserved.store(false, std::memory_order_release);
 }
 void resident_stop(Dev& d) {
-  for (Resident* r : {&d.res, &d.res_blk}) {
-    std::lock_guard<std::mutex> lk(r->mu);
-    resident_halt(d, *r);
-  }
+  std::lock_guard<std::mutex> lk(d.res.mu);
+  resident_halt(d, d.res);
 }
 
-// One job on the resident server of device d: fill(data, layout) writes the inputs, read(...)
+// One job on the resident server of device d: fill(data, job) writes the inputs, read(data)
 // takes the outputs. Returns -1 when the server is off, busy or the group too large (the caller
 // takes a lane), else an EGES status.
-// the block server's cap: its grid (helpers + one workgroup per item, two waves each) stays
-// within three quarters of the device's workgroup slots at the narrow form's occupancy (3 waves
-// per SIMD), so the single server and lane kernels still find room beside it
-uint32_t resident_cap(const Dev& d, bool block) {
-  if (!block) return (uint32_t)std::max<long long>(1, std::min<long long>(knob(KNOB_RESIDENT_CAP), 4096));
-  const long long wg_slots = (long long)d.cus * 4 * 3 / 2;
-  return (uint32_t)std::max<long long>(64, std::min<long long>(knob(KNOB_RESIDENT_BLOCK_CAP), wg_slots * 3 / 4 - 16));
-}
-// base (block server only): fills the launch parameters of its kind / outputs / signer / chain
-// id from the server's buffers (called at each launch, after they exist); a job with others
-// first drains the queued launches. The single-call server is one launch that
-// loops over jobs; the block server is one launch per job, the next one enqueued (launch API
-// time overlapped with the GPU's work) while the current job runs, so one is always polling.
+uint32_t resident_cap() { return (uint32_t)std::max<long long>(1, std::min<long long>(knob(KNOB_RESIDENT_CAP), 4096)); }
 template <class Fill, class Read>
-int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& read,
-                 const std::function<void(RecoverParams&)>* base = nullptr,
-                 uint32_t want = 0, uint32_t signer = 0, uint64_t cid = 0) {
-  if (knob(r.block ? KNOB_RESIDENT_BLOCK : KNOB_RESIDENT) == 0 || n == 0 || (r.block && !base)) return -1;
+int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& read) {
+  if (knob(KNOB_RESIDENT) == 0 || n == 0) return -1;
   // the test-only knobs act on launches: their runs take the lanes
   if (knob(KNOB_FORCE_REDO) != 0 || knob(KNOB_TEST_SKIP_FLAG) != 0 || knob(KNOB_ROOT_HELPERS) == 0) return -1;
-  const uint32_t cap = resident_cap(d, r.block);
+  const uint32_t cap = resident_cap();
   if (n > cap) return -1;
   std::unique_lock<std::mutex> lk(r.mu, std::try_to_lock);
   if (!lk.owns_lock()) return -1;
+  // device-wide work running or still queued: the lanes (checked under r.mu, which resident_stop
+  // takes after raising d.wide, so no server starts once a device-wide call has begun)
+  if (d.wide.load(std::memory_order_acquire) != 0 || hipEventQuery(d.last) != hipSuccess) return -1;
   DevGuard g(d.id);
   if (!r.job || r.cap < cap) {
     if (r.running) return -1;  // (a knob raised while it runs: the lanes until it exits)
@@ -1754,49 +1509,32 @@ int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& re
     }
     if (r.data) (void)hipHostFree(r.data);
     r.data = nullptr;
-    const size_t bytes = r.block ? resident_block_layout(cap).total : resident_layout(cap).total;
     // the data area is ordinary (cacheable) pinned memory, like the lanes' staging: uncached
-    // (coherent) memory made the root helpers' scattered row reads one PCIe read per lane. The
-    // servers order it by system-scope fences around each job (k_recover_lat.hip resident_next
-    // / resident_done); only the job word is coherent.
-    if (hipHostMalloc(&r.data, bytes, hipHostMallocDefault) != hipSuccess)
+    // (coherent) memory made scattered reads one PCIe read per lane. The server orders it by
+    // system-scope fences around each job (k_recover_lat.hip resident_next / resident_done);
+    // only the job word is coherent.
+    if (hipHostMalloc(&r.data, resident_layout(cap).total, hipHostMallocDefault) != hipSuccess)
       return set_err(EGES_E_NOMEM, "hipHostMalloc(resident data)");
-    if (r.block) {
-      if (r.scratch) (void)hipFree(r.scratch);
-      HIPCHK(hipMalloc(&r.scratch, recover_scratch_bytes((cap + 63) / 64 * 64)));
-    }
     r.cap = cap;
   }
   const long long idle_ms = std::max<long long>(1, knob(KNOB_RESIDENT_IDLE_MS));
   const auto now = std::chrono::steady_clock::now();
   // a server idle for half its bound may be deciding to exit: restart it rather than race it
-  // (the block server's queued launch instead serves whatever job is pending when it starts)
-  if (!r.block && r.running &&
+  if (r.running &&
       (hipStreamQuery(r.stream) == hipSuccess || now - r.last_use > std::chrono::microseconds(idle_ms * 500)))
-    resident_halt(d, r);
-  if (r.block && r.running &&
-      (r.cfg_kind != (uint32_t)kind || r.cfg_want != want || r.cfg_signer != signer || r.cfg_cid != cid))
     resident_halt(d, r);
   auto launch = [&]() -> int {
     if (!r.running) {  // the lane finishes what it runs and takes no more calls
       std::lock_guard<std::mutex> l0(d.lanes[r.lane].mu);
       d.lanes[r.lane].reserved.store(true, std::memory_order_release);
     }
-    if (!r.block) HIPCHK(hipMemsetAsync(r.counter, 0, RESIDENT_COUNTER_BYTES, r.stream));
+    HIPCHK(hipMemsetAsync(r.counter, 0, RESIDENT_COUNTER_BYTES, r.stream));
     if (++r.inst == 0) r.inst = 1;
-    ResidentParams rp{r.job, r.data, r.scratch, r.cap, __atomic_load_n(&r.job->done, __ATOMIC_ACQUIRE), r.counter,
+    ResidentParams rp{r.job, r.data, r.cap, __atomic_load_n(&r.job->done, __ATOMIC_ACQUIRE), r.counter,
                       (uint64_t)idle_ms * 100000ull, r.inst, d.gtab, d.diag};
     r.wgs = (uint32_t)std::max<long long>(1, std::min<long long>(knob(KNOB_RESIDENT_WGS), 1024));
-    if (!r.data || !r.counter || (r.block && !r.scratch)) return set_err(EGES_E_HIP, "resident server: buffers missing");
-    hipError_t e;
-    if (r.block) {
-      RecoverParams bp{r.scratch, r.cap, (r.cap + 63) / 64 * 64, nullptr, nullptr, nullptr, d.gtab, nullptr};
-      (*base)(bp);
-      e = launch_lat_resident_block(rp, bp, r.stream);
-    } else {
-      e = launch_lat_resident(rp, r.wgs, r.stream);
-    }
-    if (e != hipSuccess) {
+    if (!r.data || !r.counter) return set_err(EGES_E_HIP, "resident server: buffers missing");
+    if (launch_lat_resident(rp, r.wgs, r.stream) != hipSuccess) {
       r.running = false;
       d.lanes[r.lane].reserved.store(false, std::memory_order_release);
       return set_err(EGES_E_HIP, "resident server launch failed");
@@ -1804,28 +1542,20 @@ int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& re
     r.running = true;
     return EGES_SUCCESS;
   };
-  if (!r.running || (r.block && now - r.last_use > std::chrono::microseconds(idle_ms * 500))) {
-    const int rc = launch();  // (block: the queued launch may be about to idle out; this one follows it)
+  if (!r.running) {
+    const int rc = launch();
     if (rc) return rc;
-    r.cfg_kind = (uint32_t)kind;
-    r.cfg_want = want;
-    r.cfg_signer = signer;
-    r.cfg_cid = cid;
   }
   fill(r.data, r.job);
   __atomic_store_n(&r.job->n, (uint32_t)n, __ATOMIC_RELAXED);
   __atomic_store_n(&r.job->kind, (uint32_t)kind, __ATOMIC_RELAXED);
   const uint32_t seq = ++r.seq;
   __atomic_store_n(&r.job->seq, seq, __ATOMIC_RELEASE);
-  if (r.block) {  // the next job's launch, queued behind this one while the GPU works
-    const int rc = launch();
-    if (rc) return rc;
-  }
   const auto t0 = std::chrono::steady_clock::now();
   for (uint64_t spins = 0; __atomic_load_n(&r.job->done, __ATOMIC_ACQUIRE) != seq; ++spins) {
     cpu_relax();
     if ((spins & 1023) != 1023) continue;
-    if (!r.block && hipStreamQuery(r.stream) == hipSuccess && __atomic_load_n(&r.job->done, __ATOMIC_ACQUIRE) != seq) {
+    if (hipStreamQuery(r.stream) == hipSuccess && __atomic_load_n(&r.job->done, __ATOMIC_ACQUIRE) != seq) {
       // the server exited without taking the job (its idle bound): a fresh one takes it (lane 0
       // stays reserved in between)
       const int rc = launch();
@@ -1840,65 +1570,6 @@ int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& re
   r.last_use = std::chrono::steady_clock::now();
   return EGES_SUCCESS;
 }
-// A host-buffer block (ecrecover or types.Sender rows) on the resident block server; -1: not taken.
-int resident_block_run(Dev& d, const HostJob& j, size_t off, size_t n) {
-  const uint32_t cap = resident_cap(d, true);
-  const ResidentBlockLayout L = resident_block_layout(cap);
-  const bool snd = j.kind == HostJob::SENDER;
-  const uint32_t want = snd ? 0u : ((j.pub ? 1u : 0u) | (j.addr ? 2u : 0u));
-  // the block server's launch parameters for this kind (the data area's fixed layout)
-  Resident& r = d.res_blk;
-  const std::function<void(RecoverParams&)> base = [&](RecoverParams& p) {  // (r.data / r.scratch exist)
-    if (snd) {
-      p.status = r.data + L.sstatus;
-      p.addr = r.data + L.saddr;
-      bind_sender_rows(p, r.data + L.sh, r.data + L.sr, r.data + L.ss, r.data + L.sv, r.data + L.sf, j.signer, j.chain_id);
-    } else {
-      p.status = r.data + L.status;
-      p.addr = j.addr ? r.data + L.addr : nullptr;
-      p.pub = j.pub ? r.data + L.pub : nullptr;
-      p.raw_msg = r.data + L.msg;
-      p.raw_sig = r.data + L.sig;
-    }
-    p.wide = 0;  // narrow form
-    p.n_helpers = resident_block_helpers(r.cap);
-    p.diag = d.diag;
-  };
-  bool fault = false;
-  const int rc = resident_job(
-      d, r, snd ? RESIDENT_SENDER : RESIDENT_RECOVER, n,
-      [&](uint8_t* D, ResidentJob* job) {
-        if (snd) {
-          std::memcpy(D + L.sh, j.a + off * 32, n * 32);
-          std::memcpy(D + L.sr, j.b + off * 32, n * 32);
-          std::memcpy(D + L.ss, j.c + off * 32, n * 32);
-          std::memcpy(D + L.sv, j.d + off * 32, n * 32);
-          if (j.e) std::memcpy(D + L.sf, j.e + off, n);
-          else std::memset(D + L.sf, 0, n);
-          job->signer = (uint32_t)j.signer;
-          job->chain_id = j.chain_id;
-        } else {
-          std::memcpy(D + L.msg, j.a + off * 32, n * 32);
-          std::memcpy(D + L.sig, j.b + off * 65, n * 65);
-          job->want = (j.pub ? 1u : 0u) | (j.addr ? 2u : 0u);
-        }
-      },
-      [&](const uint8_t* D) {
-        const uint8_t* st = D + (snd ? L.sstatus : L.status);
-        if (j.status) std::memcpy(j.status + off, st, n);
-        fault = std::memchr(st, EGES_ENGINE_FAULT, n) != nullptr;
-        if (snd) {
-          if (j.addr) std::memcpy(j.addr + off * 20, D + L.saddr, n * 20);
-        } else {
-          if (j.pub) std::memcpy(j.pub + off * 65, D + L.pub, n * 65);
-          if (j.addr) std::memcpy(j.addr + off * 20, D + L.addr, n * 20);
-        }
-      },
-      &base, want, snd ? (uint32_t)j.signer : 0u, snd ? j.chain_id : 0u);
-  if (rc == EGES_SUCCESS && fault)
-    return set_err(EGES_E_HIP, "a kernel hand-off timed out (EGES_ENGINE_FAULT items; EGES_DIAG_HANDOFF)");
-  return rc;
-}
 DevPtr first_dev() {
   std::lock_guard<std::mutex> lk(g_mu);
   return g_devs.empty() ? nullptr : g_devs[0];
@@ -1908,7 +1579,7 @@ void run_group(std::vector<RecoverReq*>& g) {
   const size_t n = g.size();
   if (ensure_init() == EGES_SUCCESS) {
     if (DevPtr d = first_dev()) {
-      const ResidentLayout L = resident_layout(resident_cap(*d, false));
+      const ResidentLayout L = resident_layout(resident_cap());
       const int rc = resident_job(
           *d, d->res, RESIDENT_RECOVER, n,
           [&](uint8_t* D, ResidentJob*) {
@@ -1954,10 +1625,11 @@ void run_group(std::vector<VerifyReq*>& g) {
   const size_t n = g.size();
   if (ensure_init() == EGES_SUCCESS) {
     if (DevPtr d = first_dev()) {
-      const ResidentLayout L = resident_layout(resident_cap(*d, false));
+      const ResidentLayout L = resident_layout(resident_cap());
       const int rc = resident_job(
           *d, d->res, RESIDENT_VERIFY, n,
           [&](uint8_t* D, ResidentJob*) {
+            *reinterpret_cast<uint32_t*>(D + L.vfault) = 0u;
             for (size_t i = 0; i < n; ++i) {
               std::memset(D + L.vpub + i * 65, 0, 65);
               std::memcpy(D + L.vpub + i * 65, g[i]->pub, g[i]->publen);
@@ -1967,9 +1639,8 @@ void run_group(std::vector<VerifyReq*>& g) {
             }
           },
           [&](const uint8_t* D) {
-            bool fault = false;
-            for (size_t i = 0; i < n; ++i) fault = fault || D[L.vok + i] == EGES_ENGINE_FAULT;
-            const int rc2 = fault ? set_err(EGES_E_HIP, "a kernel hand-off timed out (EGES_ENGINE_FAULT items)") : EGES_SUCCESS;
+            const bool fault = *reinterpret_cast<const volatile uint32_t*>(D + L.vfault) != 0u;
+            const int rc2 = fault ? set_err(EGES_E_HIP, "a kernel hand-off timed out (EGES_DIAG_HANDOFF)") : EGES_SUCCESS;
             for (size_t i = 0; i < n; ++i) {
               g[i]->result = (rc2 == EGES_SUCCESS && D[L.vok + i] == 1) ? 1 : 0;
               g[i]->rc = rc2;
@@ -2309,8 +1980,7 @@ int eges_ecrecover_batch_dev(int device, const uint8_t* msg, const uint8_t* sig,
   if (rc) return rc;
   DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
-  resident_stop(*d);
-  std::lock_guard<std::mutex> lk(d->mu);
+  DeviceWide wide(*d);
   DevGuard g(device);
   return run_recover_dev(*d, Route::now(), msg, sig, n, pub_out, addr_out, status, (hipStream_t)stream);
 }
@@ -2325,8 +1995,7 @@ int eges_sender_batch_dev(int device, const uint8_t* sighash, const uint8_t* r, 
   if (rc) return rc;
   DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
-  resident_stop(*d);
-  std::lock_guard<std::mutex> lk(d->mu);
+  DeviceWide wide(*d);
   DevGuard g(device);
   return run_sender_dev(*d, Route::now(), sighash, r, s, v, vflags, n, signer, chain_id, addr_out, status,
                         (hipStream_t)stream);
@@ -2342,8 +2011,7 @@ int eges_sender_raw_batch_dev(int device, const uint8_t* raw, const uint64_t* of
   if (rc) return rc;
   DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
-  resident_stop(*d);
-  std::lock_guard<std::mutex> lk(d->mu);
+  DeviceWide wide(*d);
   DevGuard g(device);
   return run_sender_raw_dev(*d, Route::now(), raw, offsets, n, signer, chain_id, addr_out, status, sighash_out,
                             (hipStream_t)stream);
@@ -2357,8 +2025,7 @@ int eges_ecrecover_precompile_batch_dev(int device, const uint8_t* input, const 
   if (rc) return rc;
   DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
-  resident_stop(*d);
-  std::lock_guard<std::mutex> lk(d->mu);
+  DeviceWide wide(*d);
   DevGuard g(device);
   return run_precompile_dev(*d, Route::now(), input, inlen, n, out32, status, (hipStream_t)stream);
 }
@@ -2371,8 +2038,7 @@ int eges_verify_batch_dev(int device, const uint8_t* pub, const uint8_t* publen,
   if (rc) return rc;
   DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
-  resident_stop(*d);
-  std::lock_guard<std::mutex> lk(d->mu);
+  DeviceWide wide(*d);
   DevGuard g(device);
   return run_verify_dev(*d, Route::now(), pub, publen, msg, sig, n, ok_out, (hipStream_t)stream);
 }
@@ -2383,8 +2049,7 @@ static int synth_common(int device, uint64_t first_index, size_t n, const uint8_
   if (rc) return rc;
   DevPtr d = dev_by_id(device);
   if (!d) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
-  resident_stop(*d);
-  std::lock_guard<std::mutex> lk(d->mu);
+  DeviceWide wide(*d);
   DevGuard g(device);
   hipStream_t st = (hipStream_t)stream;
   Serial ser(*d, st);

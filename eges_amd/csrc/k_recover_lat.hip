@@ -762,6 +762,9 @@ DEV uint32_t* root_area(const RecoverParams& prm) {
 }
 
 DEV void root_helper(const RecoverParams& prm, uint32_t epoch, uint32_t n) {
+  // (the three-wave form's workgroups have 192 threads: the third wave of a helper workgroup
+  // would take the next helper's items)
+  if (threadIdx.x >= ROOT_WG) return;
   const uint32_t j = blockIdx.x * ROOT_WG + threadIdx.x;
   if (j >= n) return;
   LatParse q;
@@ -1089,7 +1092,10 @@ DEV void verify_lat_item(const VerifyParams& prm, uint32_t idx, LatLds& S) {
     }
     eq = fr_equal(Q.x, fr_mul(fe_to_fr(fe_from_u256(rn)), z2));
   }
-  if (lane_id() == 0) prm.ok[idx] = fault ? (uint8_t)ST_ENGINE_FAULT : (ok && eq) ? 1 : 0;
+  if (lane_id() == 0) {  // ok stays 0 / 1 (eges.h): a faulted item reads invalid, the fault word says why
+    prm.ok[idx] = (!fault && ok && eq) ? 1 : 0;
+    if (fault && prm.fault) __hip_atomic_store(prm.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 constexpr int LAT_WG_SPLIT = 256;  // split form: four waves
@@ -1147,11 +1153,10 @@ hipError_t launch_recover_lat(const RecoverParams& p0, hipStream_t st) {
 // after every workgroup's outputs (each releases at system scope before its count).
 // RM_SEQ: one 64-bit word (launch id << 32 | sequence), so a workgroup never pairs this launch's
 // id with an earlier launch's sequence (launch.h RESIDENT_COUNTER_BYTES covers the mirror)
-enum { RM_SEQ = 8, RM_EXIT = 10, RM_N, RM_KIND, RM_SIGNER, RM_WANT, RM_CID_LO, RM_CID_HI, RM_END };
+enum { RM_SEQ = 8, RM_EXIT = 10, RM_N, RM_KIND, RM_END };
 static_assert(RM_END * 4 <= RESIDENT_COUNTER_BYTES, "resident mirror");
 struct ResidentNext {
-  uint32_t seq, n, kind, signer, want, exit;
-  uint64_t cid;
+  uint32_t seq, n, kind, exit;
 };
 // thread 0: the next job (one the host handed over and no launch has served yet: seq > done)
 // after `seen`, or this launch's exit, into J. The mirror entries carry the launch's id, so a
@@ -1181,16 +1186,9 @@ DEV void resident_next(const ResidentParams& rp, uint32_t seen, uint64_t last, R
     J.seq = q;
     J.n = __hip_atomic_load(&rp.job->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     J.kind = __hip_atomic_load(&rp.job->kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    J.signer = __hip_atomic_load(&rp.job->signer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    J.want = __hip_atomic_load(&rp.job->want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    J.cid = __hip_atomic_load(&rp.job->chain_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (gridDim.x > 1) {
       __hip_atomic_store(&M[RM_N], J.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&M[RM_KIND], J.kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&M[RM_SIGNER], J.signer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&M[RM_WANT], J.want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&M[RM_CID_LO], (uint32_t)J.cid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&M[RM_CID_HI], (uint32_t)(J.cid >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(reinterpret_cast<uint64_t*>(M + RM_SEQ), (uint64_t)rp.inst << 32 | q, __ATOMIC_RELEASE,
                          __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -1213,10 +1211,6 @@ DEV void resident_next(const ResidentParams& rp, uint32_t seen, uint64_t last, R
       J.seq = q;
       J.n = __hip_atomic_load(&M[RM_N], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       J.kind = __hip_atomic_load(&M[RM_KIND], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      J.signer = __hip_atomic_load(&M[RM_SIGNER], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      J.want = __hip_atomic_load(&M[RM_WANT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      J.cid = (uint64_t)__hip_atomic_load(&M[RM_CID_LO], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
-              (uint64_t)__hip_atomic_load(&M[RM_CID_HI], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 32;
       return;
     }
     __builtin_amdgcn_s_sleep(8);
@@ -1259,6 +1253,7 @@ __global__ void __launch_bounds__(LAT_WG_SPLIT) lat_resident_kernel(ResidentPara
         VerifyParams v{rp.data + L.vpub, rp.data + L.vpublen, rp.data + L.vmsg, rp.data + L.vsig, n,
                        rp.data + L.vok, rp.gtab, nullptr};
         v.diag = rp.diag;
+        v.fault = reinterpret_cast<uint32_t*>(rp.data + L.vfault);
         verify_lat_item<true>(v, idx, S);
       }
       __syncthreads();  // every wave done with this item's LDS
@@ -1271,37 +1266,6 @@ __global__ void __launch_bounds__(LAT_WG_SPLIT) lat_resident_kernel(ResidentPara
 }
 hipError_t launch_lat_resident(const ResidentParams& p, uint32_t wgs, hipStream_t st) {
   hipLaunchKernelGGL(lat_resident_kernel, dim3(wgs), dim3(LAT_WG_SPLIT), 0, st, p);
-  return hipGetLastError();
-}
-
-// The block server (blocks of EGES_LAT_TRI_MAX + 1 ... cap items, ecrecover or types.Sender
-// rows): the narrow form's launch kept resident. The first ceil(cap / 128) workgroups are the
-// root helpers (their lanes take items j < n), then one workgroup per item; each job's epoch is
-// its sequence number, so root words of an earlier job never match.
-// base: the server's RecoverParams (the layout's pointers for its kind, signer, chain id and
-// outputs fixed per launch: the host relaunches when a job needs others), read from the argument
-// segment as a launch's are. One job per launch: the host enqueues the next instance while this
-// one works, so it is already polling when the next job comes (a loop over jobs inside one
-// launch kept the item's invariants live across jobs and pushed the kernel into spills).
-// Each job supplies n and its sequence number as the epoch of its root words.
-__global__ void __launch_bounds__(LAT_WG) lat_resident_block_kernel(ResidentParams rp, RecoverParams base) {
-  __shared__ LatLds S;
-  __shared__ ResidentNext J;
-  if (threadIdx.x == 0) resident_next(rp, 0u, __builtin_amdgcn_s_memrealtime(), J);
-  __syncthreads();
-  if (J.exit) return;
-  const uint32_t seq = J.seq, n = J.n < rp.cap ? J.n : rp.cap;
-  if (blockIdx.x < base.n_helpers) {
-    root_helper(base, seq, n);
-  } else if (blockIdx.x - base.n_helpers < n) {
-    recover_lat_item<NoStamp, FORM_NARROW>(base, blockIdx.x - base.n_helpers, S, nullptr, seq);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) resident_done(rp, seq);
-}
-hipError_t launch_lat_resident_block(const ResidentParams& p, const RecoverParams& base, hipStream_t st) {
-  const uint32_t grid = base.n_helpers + p.cap;
-  hipLaunchKernelGGL(lat_resident_block_kernel, dim3(grid), dim3(LAT_WG), 0, st, p, base);
   return hipGetLastError();
 }
 

@@ -924,7 +924,10 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
       cy >>= 32;
     }
     eq = eq || (!u256_ge(q.R.v, P_MINUS_N) && fe_equal(Q.x, fe_mul(fe_from_u256(rn), z2)));
-    if (live) prm.v_ok[idx] = fault ? (uint8_t)ST_ENGINE_FAULT : (ok && eq) ? 1 : 0;
+    if (live) {  // ok stays 0 / 1 (eges.h): a faulted item reads invalid, the fault word says why
+      prm.v_ok[idx] = (!fault && ok && eq) ? 1 : 0;
+      if (fault && prm.v_fault) __hip_atomic_store(prm.v_fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     st_.mark(7);
     stamp_out();
     return;
@@ -991,6 +994,7 @@ hipError_t launch_verify_mid(const VerifyParams& v, hipStream_t st) {
   p.v_msg = v.msg;
   p.v_sig = v.sig;
   p.v_ok = v.ok;
+  p.v_fault = v.fault;
   hipLaunchKernelGGL(verify_bkt_kernel, dim3((v.n + MID_L - 1) / MID_L), dim3(MID_WG), 0, st, p);
   return hipGetLastError();
 }

@@ -27,29 +27,20 @@ enum KnobId : int {
   KNOB_COALESCE_SPINNERS,   //   at most this many callers spin at once
   KNOB_SENDER_FUSED,      // 1: sender rows of latency / mid-size batches are classified inside the
                           //   recover kernel (no prep_sender launch); 0: prep_sender_kernel first
-  KNOB_HOST_PIPE,         // 1: multi-chunk host-buffer calls run the pinned-slot pipeline (run_host_pipe;
-                          //   measured slower than 0 at 1M); 0 (default): the chunked
-                          //   pageable-copy path; 2 (tests): any batch above PIPE_FIRST
-  KNOB_PIPE_CHUNK,        //   its chunk size (signatures)
-  KNOB_PIPE_FIRST,        //   and its first, smaller chunk
-  KNOB_PIPE_STREAMS,      //   compute streams the chunks alternate on (1 default, 2 for A/B)
   KNOB_LAT_TRI_MAX,       // latency batches above LAT_WIDE_MAX up to this size: the three-wave form
-  KNOB_PIPE_SEG,          //   host copy / DMA segment of the pipeline (bytes; 8 MB)
   KNOB_HOST_PARTS,        // host-buffer shards of >= 2 * PIPE_MIN items without the pipeline: chunks (8;
                           //   at least PIPE_MIN / 2 signatures each)
   KNOB_TEST_SKIP_FLAG,    // tests: k > 0 makes item 0's workgroup's producer of hand-off flag k - 1
                           //   skip publishing it (handoff.cuh), so its consumers time out
   KNOB_TEST_DELAY_X,      // tests: the bucket form's wave X sleeps k x ~3 us before it reads its
                           //   workgroup's wire stage (the stage / part[0] release)
-  KNOB_HOST_STREAMS,      // the chunked host path's kernels on 1 (default) or 2 alternating compute streams
   KNOB_RESIDENT,          // 1: coalesced single calls go to the resident server (capi.hip Resident)
   KNOB_RESIDENT_WGS,      //   its workgroups (split form, four waves each)
   KNOB_RESIDENT_CAP,      //   the largest group it takes (larger groups launch on a lane)
   KNOB_RESIDENT_IDLE_MS,  //   it exits after this long without a job (restarted on demand)
-  KNOB_RESIDENT_BLOCK,    // 1: latency-kernel blocks above LAT_TRI_MAX go to the resident block server
-  KNOB_RESIDENT_BLOCK_CAP,  //   its largest block (and grid: helpers + one workgroup per item)
-  KNOB_GATE,              // 1: single-chunk host-buffer calls on the latency / mid-size kernels launch first
-                          //   and copy their inputs while the launch is in flight (capi.hip Gate)
+  KNOB_GATE,              // 1: single-chunk host-buffer calls on the mid-size kernels launch first and copy
+                          //   their inputs while the launch is in flight (capi.hip Gate; the latency
+                          //   kernels run ungated)
   KNOB_COUNT
 };
 

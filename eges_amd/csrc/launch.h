@@ -68,6 +68,7 @@ struct RecoverParams {
   // (VerifyParams' pub n x 65, publen, msg n x 32, sig n x 64) and its 0/1 output instead
   const uint8_t *v_pub = nullptr, *v_publen = nullptr, *v_msg = nullptr, *v_sig = nullptr;
   uint8_t* v_ok = nullptr;
+  uint32_t* v_fault = nullptr;  // as VerifyParams::fault
   // mid-size bucket form only: wire-format transactions instead of record rows (tx_rows_kernel
   // and prep_sender_kernel fused in): item i is wire_raw[wire_off[first + i] - wire_off[0],
   // wire_off[first + i + 1] - wire_off[0]); wire_raw 4-byte aligned. wire_sighash: n x 32 or null.
@@ -95,6 +96,9 @@ struct VerifyParams {
   uint32_t* diag = nullptr;   // as RecoverParams
   uint32_t force_redo = 0;
   uint32_t test_skip_flag = 0, test_skip_block = 0;
+  // a wave hand-off of an item timed out (handoff.cuh): its ok byte is 0 and a kernel stores 1
+  // here (system scope: host-buffer calls give a word of coherent pinned memory; nullable)
+  uint32_t* fault = nullptr;
 };
 // Verify scratch: slot rows (P affine, prefix product of s), the order, the two counters.
 constexpr int VERIFY_SLOT_ROWS = 7;
@@ -163,20 +167,17 @@ hipError_t launch_verify_lat(const VerifyParams& p, bool wide, hipStream_t st);
 struct ResidentJob {  // coherent pinned host memory, 128 bytes
   uint32_t seq;   // host: the job's sequence number, stored last (release)
   uint32_t n;     // items (<= the server's cap)
-  uint32_t kind;  // RESIDENT_RECOVER / RESIDENT_VERIFY / RESIDENT_SENDER
+  uint32_t kind;  // RESIDENT_RECOVER / RESIDENT_VERIFY
   uint32_t stop;  // host: exit now
   uint32_t done;  // device: the last finished sequence, stored after every output (release)
-  uint32_t signer;     // RESIDENT_SENDER: types.Sender's signer and chain id
-  uint64_t chain_id;
-  uint32_t want;       // RESIDENT_RECOVER on the block server: bit 0 pub, bit 1 addr
-  uint32_t pad[23];
+  uint32_t pad[27];
 };
-enum { RESIDENT_RECOVER = 0, RESIDENT_VERIFY = 1, RESIDENT_SENDER = 2 };
-// the data area (coherent pinned, cap items): recover msg | sig | pub | status; verify pub |
-// publen | msg | sig | ok (offsets from resident_layout)
+enum { RESIDENT_RECOVER = 0, RESIDENT_VERIFY = 1 };
+// the data area (pinned, cap items): recover msg | sig | pub | status; verify pub | publen | msg |
+// sig | ok | fault word (offsets from resident_layout)
 struct ResidentLayout {
   size_t msg, sig, pub, status;        // recover
-  size_t vpub, vpublen, vmsg, vsig, vok;  // verify
+  size_t vpub, vpublen, vmsg, vsig, vok, vfault;  // verify
   size_t total;
 };
 __host__ __device__ inline ResidentLayout resident_layout(uint32_t cap) {
@@ -191,53 +192,24 @@ __host__ __device__ inline ResidentLayout resident_layout(uint32_t cap) {
   L.vmsg = L.vpublen + c;
   L.vsig = L.vmsg + c * 32;
   L.vok = L.vsig + c * 64;
-  L.total = L.status + c > L.vok + c ? L.status + c : L.vok + c;
+  L.vfault = (L.vok + c + 3) / 4 * 4;
+  L.total = L.status + c > L.vfault + 4 ? L.status + c : L.vfault + 4;
   return L;
 }
-// the block server's data area (narrow form, blocks of up to cap items): recover msg | sig | pub |
-// addr | status; sender rows h | r | s | v | vflags | addr | status (4-byte aligned rows)
-struct ResidentBlockLayout {
-  size_t msg, sig, pub, addr, status;
-  size_t sh, sr, ss, sv, sf, saddr, sstatus;
-  size_t total;
-};
-__host__ __device__ inline ResidentBlockLayout resident_block_layout(uint32_t cap) {
-  ResidentBlockLayout L;
-  const size_t c = ((size_t)cap + 63) / 64 * 64;
-  L.msg = 0;
-  L.sig = L.msg + c * 32;
-  L.pub = L.sig + c * 65;
-  L.addr = L.pub + c * 65;
-  L.status = L.addr + c * 20;
-  L.sh = 0;
-  L.sr = L.sh + c * 32;
-  L.ss = L.sr + c * 32;
-  L.sv = L.ss + c * 32;
-  L.sf = L.sv + c * 32;
-  L.saddr = L.sf + c;
-  L.sstatus = L.saddr + c * 20;
-  const size_t a = L.status + c, b = L.sstatus + c;
-  L.total = a > b ? a : b;
-  return L;
-}
-// bytes of ResidentParams::counter: the completion counters, then the block server's job mirror
+// bytes of ResidentParams::counter: the completion counters, then the job mirror
 constexpr uint32_t RESIDENT_COUNTER_BYTES = 256;
 struct ResidentParams {
   ResidentJob* job;
   uint8_t* data;
-  uint32_t* scratch;     // block server: the narrow form's record / root rows (n_pad = cap padded)
   uint32_t cap;
   uint32_t seen0;        // the last sequence finished before this launch
-  uint32_t* counter;     // device memory, 2 words: zero at launch (single) / left zero by the last WG (block)
+  uint32_t* counter;     // device memory: 2 completion counters (zero at launch), then the job mirror
   uint64_t idle_ticks;   // exit after this long without a job (s_memrealtime, 100 MHz)
   uint32_t inst;         // this launch's id (nonzero): its workgroups' exit mark in the mirror
   const uint32_t* gtab;
   uint32_t* diag;
 };
 hipError_t launch_lat_resident(const ResidentParams& p, uint32_t wgs, hipStream_t st);
-// the block server: ceil(cap / 128) root-helper workgroups, then cap narrow-form workgroups
-hipError_t launch_lat_resident_block(const ResidentParams& p, const RecoverParams& base, hipStream_t st);
-__host__ __device__ inline uint32_t resident_block_helpers(uint32_t cap) { return (cap + 127) / 128; }
 // Blocks the lane-serial kernels may need for a pass of n signatures at a resident grid of
 // max_blocks (grid_for_lane_serial: more than resident when n > max_blocks * WG * MAX_SLOTS).
 int lane_serial_grid(uint32_t n, int max_blocks);

@@ -47,7 +47,9 @@ typedef enum eges_status {
                                      kernel workgroup timed out, and the item got no result (no address
                                      is written). Host-buffer entries then return EGES_E_HIP; *_dev
                                      entries leave it in the status byte (and EGES_DIAG_HANDOFF counts
-                                     it). Never produced by a call that returns EGES_SUCCESS. */
+                                     it). Never produced by a call that returns EGES_SUCCESS. The
+                                     VerifySignature entries never write it: their ok bytes stay 0 / 1
+                                     (a faulted item reads 0, see eges_verify_batch). */
 } eges_status;
 
 /* Call-level return codes. */
@@ -164,7 +166,9 @@ int eges_ecrecover_precompile_batch(const uint8_t *input, const uint32_t *inlen,
 
 /* crypto.VerifySignature over a batch (signature_cgo.go:66 -> secp256.go:126-134).
  * pub: n*65 (each key left-aligned, publen[i] bytes valid: 33 or 65; 0 => false),
- * msg n*32, sig n*64. ok_out n bytes of 0/1. */
+ * msg n*32, sig n*64. ok_out n bytes, always 0 or 1. An item whose in-kernel wave hand-off timed
+ * out reads 0; the call then returns EGES_E_HIP (eges_verify_batch_dev cannot: it returns before
+ * the kernels run, so there EGES_DIAG_HANDOFF is the only report). */
 int eges_verify_batch(const uint8_t *pub, const uint8_t *publen, const uint8_t *msg, const uint8_t *sig,
                       size_t n, uint8_t *ok_out);
 

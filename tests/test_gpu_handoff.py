@@ -146,7 +146,8 @@ def test_verify_split_form_skipped_flag_faults_one_item(engine):
     with knobs(engine, dict(SPLIT, EGES_TEST_SKIP_FLAG=1)):
         rc = _lib.lib.eges_verify_batch(_p(pub), _p(publen), _p(msg), _p(sig), n, _p(ok))
     assert rc == -3
-    assert ok[0] == _lib.ENGINE_FAULT
+    assert "hand-off" in _lib.lib.eges_last_error().decode()
+    assert ok[0] == 0  # (ok stays 0 / 1; the call's error and EGES_DIAG_HANDOFF say why)
     assert np.array_equal(ok[1:], g["ok"][1:n])
     with knobs(engine, SPLIT):
         assert np.array_equal(engine.verify_batch(pub, publen, msg, sig), g["ok"][:n])
@@ -164,6 +165,30 @@ def test_verify_bucket_form_skipped_flag_faults_one_workgroup(engine):
     with knobs(engine, dict(BUCKET, EGES_TEST_SKIP_FLAG=1)):
         rc = _lib.lib.eges_verify_batch(_p(pub), _p(publen), _p(msg), _p(sig), n, _p(ok))
     assert rc == -3
-    assert (ok[:64] == _lib.ENGINE_FAULT).all()
+    assert (ok[:64] == 0).all()
     assert np.array_equal(ok[64:], exp[64:])
     engine.diag_counters(reset=True)
+
+
+@pytest.mark.parametrize("form", ["split", "bucket"])
+def test_verify_dev_fault_is_never_truthy(engine, form):
+    """the device-resident VerifySignature entry returns without a sync, so a faulted
+    item must not reach the caller as a nonzero ok byte: it is 0, and EGES_DIAG_HANDOFF counts it"""
+    import torch
+    g = load_golden("verify.npz")
+    n = 40 if form == "split" else 300
+    rep = -(-n // len(g["pub"]))
+    cols = [np.ascontiguousarray(np.concatenate([g[k]] * rep)[:n]) for k in ("pub", "publen", "msg", "sig", "ok")]
+    pub, publen, msg, sig, exp = cols
+    nf = 1 if form == "split" else 64
+    assert exp[:nf].any()  # some of the faulted items are valid signatures
+    d = [torch.from_numpy(x).cuda() for x in (pub, publen, msg, sig)]
+    ok = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+    engine.diag_counters(reset=True)
+    with knobs(engine, dict(SPLIT if form == "split" else BUCKET, EGES_TEST_SKIP_FLAG=1)):
+        engine.verify_batch_dev(*d, ok=ok)
+        torch.cuda.synchronize()
+    got = ok.cpu().numpy()
+    assert set(np.unique(got).tolist()) <= {0, 1}
+    assert not got[:nf].any() and np.array_equal(got[nf:], exp[nf:])
+    assert engine.diag_counters(reset=True)["handoff"] >= 1

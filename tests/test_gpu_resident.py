@@ -1,10 +1,10 @@
-"""The resident servers (capi.hip Resident, k_recover_lat.hip lat_resident_kernel /
-lat_resident_block_kernel): coalesced eges_ecdsa_recover / eges_ecdsa_verify groups go to
-split-form workgroups, and latency-kernel blocks above the three-wave form's range to a
-narrow-form grid, that stay resident and poll a job word in coherent pinned memory instead of a
-launch per call. Every golden item through them against the fixtures; device-wide calls between
-(the servers stop first and restart on the next call); idle exits and restarts; the servers
-switched off. EGES_DIAG_RESIDENT counts the jobs they served."""
+"""The resident single-call server (capi.hip Resident, k_recover_lat.hip lat_resident_kernel):
+coalesced eges_ecdsa_recover / eges_ecdsa_verify groups go to split-form workgroups that stay
+resident and poll a job word in coherent pinned memory instead of a launch per call. Every golden
+item through it against the fixtures; device-wide calls between (the server stops first and
+restarts on the next call); idle exits and restarts; the server switched off. EGES_DIAG_RESIDENT
+counts the jobs it served. (Round 4's resident block server measured slower and was removed in
+round 5.)"""
 import ctypes
 import time
 
@@ -107,70 +107,3 @@ def test_resident_off_uses_the_lanes(engine):
         rc, pub = _single_recover(g["msg"][i], g["sig"][i])
     assert rc == 1 and pub == g["pub"][i].tobytes()
     assert engine.diag_counters(reset=True)["resident"] == 0
-
-
-# ---- the block server: latency-kernel blocks above the three-wave form's range (narrow form)
-def _sender_block(engine, n, first):
-    import torch
-    from eges_amd import txs
-    h = txs.geec_block(first, n, payload=100)
-    sig_d, exp_d = engine.synth_sign_msg_dev(torch.from_numpy(h).cuda(), first)
-    torch.cuda.synchronize()
-    sig_h, exp = sig_d.cpu().numpy(), exp_d.cpu().numpy()
-    r, s, v = txs.sender_rows(sig_h, txs.GEEC_CHAIN_ID)
-    return h, r, s, v, exp
-
-
-def test_block_server_sender_blocks(engine):
-    """1000-transaction blocks (C3) through eges_sender_batch, one after another, with single calls
-    between them (both servers resident at once)"""
-    from eges_amd import txs
-    g = load_golden("recover.npz")
-    i1 = int(np.nonzero((g["status"] == 0) & (g["sig"][:, 64] < 4))[0][0])
-    engine.diag_counters(reset=True)
-    with knobs(engine, {"EGES_RESIDENT": 1, "EGES_RESIDENT_BLOCK": 1}):
-        for rep, n in enumerate([1000, 1000, 777, 449, 1000]):
-            h, r, s, v, exp = _sender_block(engine, n, 100000 * rep)
-            addr, st = engine.sender_batch(h, r, s, v, None, _lib.SIGNER_EIP155, txs.GEEC_CHAIN_ID)
-            assert (st == 0).all() and np.array_equal(addr, exp), (rep, n)
-            rc, pub = _single_recover(g["msg"][i1], g["sig"][i1])
-            assert rc == 1 and pub == g["pub"][i1].tobytes()
-    assert engine.diag_counters(reset=True)["resident"] >= 10
-
-
-def test_block_server_recover_golden_tiled(engine):
-    """every golden recovery item (all reject classes) in 600-item blocks, pub + address + status"""
-    g = load_golden("recover.npz")
-    n = len(g["msg"])
-    engine.diag_counters(reset=True)
-    with knobs(engine, {"EGES_RESIDENT_BLOCK": 1}):
-        for a in range(0, n, 600):
-            sel = np.arange(a, min(n, a + 600))
-            if len(sel) <= 448:
-                sel = np.arange(a, a + 600) % n
-            pub, addr, st = engine.ecrecover_batch(g["msg"][sel], g["sig"][sel])
-            assert np.array_equal(st, g["status"][sel]) and np.array_equal(pub, g["pub"][sel]), a
-    assert engine.diag_counters(reset=True)["resident"] >= n // 600
-    with knobs(engine, {"EGES_RESIDENT_BLOCK": 0}):
-        sel = np.arange(0, 600)
-        pub0, addr0, st0 = engine.ecrecover_batch(g["msg"][sel], g["sig"][sel])
-    assert engine.diag_counters(reset=True)["resident"] == 0
-    assert np.array_equal(st0, g["status"][sel]) and np.array_equal(pub0, g["pub"][sel])
-
-
-def test_block_server_stops_for_device_work_and_idles_out(engine):
-    from eges_amd import txs
-    g = load_golden("recover.npz")
-    engine.diag_counters(reset=True)
-    with knobs(engine, {"EGES_RESIDENT_BLOCK": 1, "EGES_RESIDENT_IDLE_MS": 4}):
-        for rep in range(6):
-            h, r, s, v, exp = _sender_block(engine, 800, 7000 * rep)
-            addr, st = engine.sender_batch(h, r, s, v, None, _lib.SIGNER_EIP155, txs.GEEC_CHAIN_ID)
-            assert (st == 0).all() and np.array_equal(addr, exp), rep
-            if rep % 2:
-                sel = np.arange(0, 3000) % len(g["msg"])  # a mid-size batch: device-wide work
-                pub, _, st2 = engine.ecrecover_batch(g["msg"][sel], g["sig"][sel])
-                assert np.array_equal(st2, g["status"][sel]) and np.array_equal(pub, g["pub"][sel])
-            else:
-                time.sleep(0.01)  # past the server's idle bound
-    assert engine.diag_counters(reset=True)["resident"] >= 6

@@ -373,20 +373,11 @@ int main(int argc, char** argv) {
     for (size_t n : {1u, 37u, 1000u, 5000u, 70000u}) batch_recover(n);
     single_item_threads(8, 300);
     signed_block(300);
-    // the pipelined host-buffer path (pinned slots, copy threads, DMA streams) forced on ragged
-    // multi-chunk batches of every kind it takes
-    step("host pipeline");
-    eges_test_set_knob("EGES_HOST_PIPE", 2);
-    eges_test_set_knob("EGES_PIPE_FIRST", 1000);
-    eges_test_set_knob("EGES_PIPE_CHUNK", 3001);
-    batch_recover(20011);
-    signed_block(5003);
-    eges_test_set_knob("EGES_HOST_PIPE", 1);
-    eges_test_set_knob("EGES_PIPE_STREAMS", 2);
-    batch_recover(20011);
-    eges_test_set_knob("EGES_PIPE_STREAMS", 1);
-    eges_test_set_knob("EGES_PIPE_FIRST", 262144);
-    eges_test_set_knob("EGES_PIPE_CHUNK", 786432);
+    // the chunked host-buffer path (a shard of >= 512k items in EGES_HOST_PARTS chunks)
+    step("host chunks");
+    eges_test_set_knob("EGES_HOST_PARTS", 5);
+    batch_recover(600011);
+    eges_test_set_knob("EGES_HOST_PARTS", 8);
     block_structure(2000);
     eges_shutdown();
   }
