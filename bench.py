@@ -25,11 +25,18 @@ Metric (BASELINE.json): "secp256k1 ecrecover+address/sec at 1/8 MI355X; % of INT
 --config verify: crypto.VerifySignature throughput (65-byte and 33-byte keys).
 --config c2host: configs[1]'s batch handed over as host (pageable) buffers through
   eges_ecrecover_batch — the PCIe-inclusive rate a Go caller sees (never `value` of the c2 line).
+--config c4host: configs[3]'s batch as host buffers through eges_ecrecover_batch with every
+  visible device open in one process (the library's own multi-device split, capi run_host).
 
-The c2 line also carries a `secondary` object (N = 1, outside the timed region): C3's block
-latency (median / p99 over 50 blocks, from sender rows and from wire bytes), C1's 10k transfers
-from wire bytes, C5 over the same 1M batch (ecrecover and sender statuses, mismatch counts), the
-same 1M batch as host buffers (c2_host) and the single-item seam under concurrent callers.
+The c2 line also carries a `secondary` object (outside the timed region). At every N it holds
+`c4_strong`: configs[3]'s fixed 64M batch split by shard_range over the ranks, every address
+checked, each rank's HIP-event kernel ms and the max/min imbalance, and the strong-scaled rate
+(so the driver's 1/2/4/8 runs of the default line give the configs[3] curve too); at N > 1 also
+`c4_host_all_devices` (rank 0 runs --config c4host as a child, the other ranks wait on a gloo
+barrier). At N = 1 also: C3's block latency (median / p99 over 50 blocks, from sender rows and
+from wire bytes), C1's 10k transfers from wire bytes, C5 over the same 1M batch (ecrecover and
+sender statuses, mismatch counts), the same 1M batch as host buffers (c2_host) and the
+single-item seam under concurrent callers.
 
 Multi-GPU: `--gpus N` without a launcher starts `torch.distributed.run --nproc-per-node N` on this
 script as a child process (no exec) and exits with its code; under a launcher WORLD_SIZE must
@@ -37,7 +44,8 @@ equal N. Every line carries `ranks`: each rank's device index, PCI address and U
 through the process group. `--stub` rehearses the rank logic on the CPU (gloo, a timed sleep as
 the step, no GPU and no libeges): tests/test_shard.py runs it at world size 2.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config c1|c2|c2host|c3|c3raw|c4|c5|verify]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--c4-total T]
+                       [--config c1|c2|c2host|c3|c3raw|c4|c4host|c5|verify]
 """
 import argparse
 import ctypes
@@ -76,11 +84,14 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=None, help="c2: signatures per GPU; c4: total signatures")
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2host", "c3", "c3raw", "c4", "c5", "verify"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2host", "c3", "c3raw", "c4", "c4host", "c5",
+                                                           "verify"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="c2: skip the secondary C1 / C3 / C5 measurements")
     ap.add_argument("--stub", action="store_true", help="CPU rehearsal of the rank logic (gloo, sleep as the step)")
+    ap.add_argument("--c4-total", type=int, default=None,
+                    help="c2: the secondary configs[3] strong-scaled leg's total batch (default 64M; 0 skips it)")
     return ap.parse_args()
 
 
@@ -224,12 +235,17 @@ class Ctx:
         if self.world > 1:
             backend = "gloo" if self.stub else (os.environ.get("EGES_BENCH_BACKEND") or "nccl")
             dist.init_process_group(backend=backend)
+        # host-side collectives (per-rank summaries, the barrier while rank 0's child uses every
+        # GPU): gloo, so no RCCL kernel waits on a device meanwhile
+        self.cpu_group = (dist.new_group(backend="gloo") if backend != "gloo" else dist.group.WORLD) \
+            if self.world > 1 else None
         self.ranks = self.gather_ranks()
         if self.stub:
             return
         import eges_amd
         self.eges = eges_amd
-        eges_amd.init(1 << self.local)
+        # c4host opens every visible device in this one process (the library splits the batch)
+        eges_amd.init(0 if args.config == "c4host" else 1 << self.local)
         self.dev = torch.device("cuda", self.local)
         # a dedicated stream: the engine's kernels and the timing events share it
         self.stream = torch.cuda.Stream(self.dev)
@@ -366,6 +382,15 @@ def run_throughput(c, strong):
                 "dtype": "u32", "data": "stub: rank-logic rehearsal on the CPU (sleep as the step, no GPU)",
                 "config": {"workload": wl, "batch_per_gpu": B, "shards": shards, "total_batch": total,
                            "parallelism": f"index-sharded x{c.world}", "correct": ok}}
+        c4_total = C4_TOTAL if a.c4_total is None else a.c4_total
+        if not strong and not a.no_secondary and c4_total > 0:
+            sec = {"note": "stub legs", "c4_strong": measure_c4_strong(c, c4_total)}
+            if c.world > 1:
+                sec["c4_host_all_devices"] = measure_host_all_devices(c, c4_total)
+            ok = ok and all(v.get("correct", True) for v in sec.values() if isinstance(v, dict))
+            ok = c.reduce_max(0.0 if ok else 1.0)[0] == 0.0
+            line["secondary"] = sec
+            line["config"]["correct"] = ok
         c.finish(line, ok)
         return
     torch = c.torch
@@ -404,9 +429,20 @@ def run_throughput(c, strong):
             "config": {"workload": wl, "batch_per_gpu": B, "shards": shards, "total_batch": total,
                        "parallelism": f"index-sharded x{c.world}", "correct": ok},
             "roofline": roofline(per_gpu_rate, W_RECOVER, B, kern_ms), "cpu_baseline": cpu}
+    sec = {"note": "measured after the timed C2 region, same processes; not part of value"}
+    c4_total = C4_TOTAL if a.c4_total is None else a.c4_total
+    if not strong and not a.no_secondary and c4_total > 0:
+        # configs[3] at every N: the driver's 1/2/4/8 runs of this default line are its curve
+        sec["c4_strong"] = measure_c4_strong(c, c4_total)
+        if c.world > 1:
+            sec["c4_host_all_devices"] = measure_host_all_devices(c, c4_total)
+            if c.rank == 0:
+                line["secondary"] = sec
+                ok = ok and all(v.get("correct", True) for v in sec.values() if isinstance(v, dict))
+                line["config"]["correct"] = ok
+            ok = c.reduce_max(0.0 if ok else 1.0)[0] == 0.0
     if c.world == 1 and not strong and not a.no_secondary:
         # the other configs, after the timed region (about a second): C3 and C1 latency, C5 statuses
-        sec = {"note": "measured after the timed C2 region, same process; not part of value"}
         sec["c3_block"] = measure_block(c, 1000, raw_mode=False, warmup=3, iters=50, cpu=False)
         sec["c3_block_wire"] = measure_block(c, 1000, raw_mode=True, warmup=3, iters=50, cpu=False)
         sec["c1_transfers"] = measure_c1(c, 10000, warmup=3, iters=20, cpu=False)
@@ -416,7 +452,8 @@ def run_throughput(c, strong):
                                       warmup=2)
         # as many synchronous callers as the reference baseline's threads (the box's granted CPUs)
         ref = cpu if cpu and cpu.get("kind") == "reference" else None
-        sec["single"] = measure_single(ref["cores"] if ref else 16, 2000, ref["value"] if ref else None)
+        sec["single"] = measure_single(ref["cores"] if ref else 16, 2000, ref["value"] if ref else None,
+                                       ref_one_call_us(msg.cpu().numpy(), sig.cpu().numpy()))
         line["secondary"] = sec
         ok = ok and all(v.get("correct", True) for v in sec.values() if isinstance(v, dict))
         line["config"]["correct"] = ok
@@ -432,6 +469,118 @@ def run_stub(c, B):
     ok = str(c.rank) != os.environ.get("EGES_BENCH_STUB_BAD_RANK", "")
     elapsed, kern_ms, bad = c.reduce_max(elapsed, kern_ms, 0.0 if ok else 1.0)
     return elapsed, kern_ms, bad == 0.0
+
+
+def with_steps(c, steps, warmup, fn):
+    """fn() with the context's step / warmup counts temporarily replaced (secondary legs)."""
+    saved = (c.args.steps, c.args.warmup)
+    c.args.steps, c.args.warmup = steps, warmup
+    try:
+        return fn()
+    finally:
+        c.args.steps, c.args.warmup = saved
+
+
+def strong_summary(total, shards, steps, per_rank):
+    """The configs[3] leg's numbers from every rank's (elapsed s, kernel ms, ok) triple: the
+    strong-scaled rate (all ranks' items / the slowest rank's elapsed time), each rank's kernel
+    ms from HIP events, and the imbalance max / min over the ranks that hold work."""
+    els = [p[0] for p in per_rank]
+    kms = [p[1] for p in per_rank]
+    busy = [k for k, (lo, hi) in zip(kms, shards) if hi > lo]
+    el = max(els)
+    return {"total_batch": total, "shards": [list(s) for s in shards], "steps": steps,
+            "sigs_per_s": round(total * steps / el, 1), "ms_per_step": round(el * 1e3 / steps, 3),
+            "rank_kernel_ms": [round(k, 4) for k in kms],
+            "rank_elapsed_ms_per_step": [round(e * 1e3 / steps, 3) for e in els],
+            "imbalance_max_over_min": round(max(busy) / min(busy), 4) if busy and min(busy) > 0 else None,
+            "correct": all(bool(p[2]) for p in per_rank), "scaling": "strong"}
+
+
+def measure_c4_strong(c, total, steps=2, warmup=1):
+    """configs[3] inside the default line: the fixed batch of `total`
+    signatures split by shard_range over the ranks, each rank's shard synthesised on its GPU,
+    `steps` timed passes between barriers, every address the timed passes wrote checked against
+    its signer's. Per-rank numbers are all-gathered so rank 0's line shows the imbalance. With
+    --stub the step is a sleep proportional to the shard (the rank logic on the CPU)."""
+    from eges_amd.shard import shard_range
+    shards = [shard_range(total, r, c.world) for r in range(c.world)]
+    lo, hi = shards[c.rank]
+    B = hi - lo
+    if c.stub:
+        unit = max(1, shards[0][1] - shards[0][0])
+
+        def step():
+            time.sleep(0.002 * B / unit)
+        elapsed, kern_ms = with_steps(c, steps, warmup, lambda: c.timed(step))
+        ok = str(c.rank) != os.environ.get("EGES_BENCH_STUB_BAD_RANK", "")
+    else:
+        torch = c.torch
+        from eges_amd._lib import check, lib
+        ok = True
+        elapsed, kern_ms = 0.0, 0.0
+        if B:
+            msg, sig, exp_addr = c.eges.synth_sign_dev(lo, B, c.local, stream=c.sp)
+            addr = torch.empty((B, 20), dtype=torch.uint8, device=c.dev)
+            status = torch.empty((B,), dtype=torch.uint8, device=c.dev)
+            torch.cuda.synchronize()
+
+            def step():
+                check(lib.eges_ecrecover_batch_dev(c.local, ctypes.c_void_p(msg.data_ptr()),
+                                                   ctypes.c_void_p(sig.data_ptr()), B, None,
+                                                   ctypes.c_void_p(addr.data_ptr()), ctypes.c_void_p(status.data_ptr()),
+                                                   ctypes.c_void_p(c.sp)))
+
+            def reset():
+                addr.zero_()
+                status.fill_(0xFF)
+        else:  # an empty shard (total < world): the rank still joins the barriers
+            def step():
+                pass
+            reset = None
+        elapsed, kern_ms = with_steps(c, steps, warmup, lambda: c.timed(step, reset))
+        if B:
+            ok = bool((status == 0).all().item()) and bool(torch.equal(addr, exp_addr))
+            del msg, sig, exp_addr, addr, status
+            torch.cuda.empty_cache()
+    mine = (elapsed, kern_ms, ok)
+    if c.world == 1:
+        per_rank = [mine]
+    else:
+        per_rank = [None] * c.world
+        c.dist.all_gather_object(per_rank, mine, group=c.cpu_group)
+    out = strong_summary(total, shards, steps, per_rank)
+    out["workload"] = ("configs[3]: the fixed batch sharded by index across the ranks (eges_amd.shard.shard_range), "
+                       "device-resident inputs, every address checked")
+    out["kernel_ms_source"] = "HIP events on each rank's launch stream around each timed step"
+    return out
+
+
+def measure_host_all_devices(c, total):
+    """The Go caller's multi-GPU path: rank 0 starts bench.py --config
+    c4host as a child process (no launcher environment) after the ranks' own legs; the child
+    opens every visible device in one process and hands the fixed batch over as host buffers
+    through eges_ecrecover_batch, which splits it over the devices in-library (capi run_host).
+    The other ranks wait at a barrier meanwhile. Returns the child's line (rank 0) or None."""
+    out = None
+    if c.rank == 0:
+        env = {k: v for k, v in os.environ.items()
+               if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                            "ROLE_WORLD_SIZE", "TORCHELASTIC_RUN_ID", "MASTER_PORT")}
+        cmd = [sys.executable, os.path.abspath(__file__), "--config", "c4host", "--batch", str(total),
+               "--steps", "2", "--warmup", "1"] + (["--stub"] if c.stub else [])
+        try:
+            cp = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+            lines = [ln for ln in cp.stdout.splitlines() if ln.startswith("{")]
+            out = json.loads(lines[-1]) if lines else {"note": f"c4host child rc {cp.returncode}: {cp.stderr[-500:]}",
+                                                       "correct": False}
+            if cp.returncode != 0:
+                out["correct"] = False
+        except Exception as e:  # noqa: BLE001
+            out = {"note": f"c4host child failed: {e}", "correct": False}
+    if c.world > 1:
+        c.dist.barrier(group=c.cpu_group)
+    return out
 
 
 # ------------------------------------------------------------------ c3: Geec block latency
@@ -568,7 +717,25 @@ def run_block_latency(c):
 
 
 # ------------------------------------------------------------------ single-item seam
-def measure_single(callers=16, calls=2000, ref_rate=None):
+def ref_one_call_us(msg_h, sig_h, n=4000):
+    """The reference's per-call cost on one host thread: secp256k1_ext_ecdsa_recover (ext.h:30-47,
+    what crypto.Ecrecover reaches through signature_cgo.go:31-44) over n items serially, no
+    Keccak, averaged (oracle/_ref; the cgo call overhead itself is not included)."""
+    try:
+        from oracle import RefLib, have_ref
+        if not have_ref():
+            return None
+        ref = RefLib()
+        ref.ecrecover_batch_mt(msg_h[:200], sig_h[:200], 1, want_addr=False)  # warm
+        t0 = time.perf_counter()
+        _, _, ret = ref.ecrecover_batch_mt(msg_h[:n], sig_h[:n], 1, want_addr=False)
+        dt = time.perf_counter() - t0
+        return round(dt / min(n, len(msg_h)) * 1e6, 2) if (ret == 1).all() else None
+    except Exception:  # noqa: BLE001
+        return None
+
+
+def measure_single(callers=16, calls=2000, ref_rate=None, ref_one_us=None):
     """The per-call cgo seam (eges_ecdsa_recover, replacing ext.h:30-47 under
     crypto.Ecrecover, signature_cgo.go:31-44): tools/single_bench (native threads, built by
     build()) as a child process on the same GPU: one caller's p50 / p99, then `callers` synchronous
@@ -591,6 +758,10 @@ def measure_single(callers=16, calls=2000, ref_rate=None):
     if ref_rate:
         out["reference_same_threads_per_s"] = ref_rate
         out["vs_reference"] = round(m["recoveries_per_s"] / ref_rate, 3)
+    if ref_one_us:
+        # one caller: the reference's serial per-call cost beside this seam's p50
+        out["reference_one_call_us"] = ref_one_us
+        out["one_caller_vs_reference"] = round(ref_one_us / (m["p50_ms_one_caller"] * 1e3), 3)
     return out
 
 
@@ -813,7 +984,7 @@ def run_verify(c):
 
 
 # ------------------------------------------------------------------ c2host: host buffers
-def measure_host(c, msg_h, sig_h, exp_h, steps, warmup):
+def measure_host(c, msg_h, sig_h, exp_h, steps, warmup, fresh_reps=3):
     """configs[1]'s batch as host (pageable) buffers through eges_ecrecover_batch (the cgo path of
     signature_cgo.go:31): H2D + prep + recover + D2H in one synchronous call. The caller's output
     arrays are reused across calls (a buffer pool); fresh arrays cost their first-touch page faults
@@ -837,14 +1008,16 @@ def measure_host(c, msg_h, sig_h, exp_h, steps, warmup):
     elapsed = time.perf_counter() - t0
     _, addr, st = out["r"]
     ok = bool((st == 0).all()) and np.array_equal(addr, exp_h)
-    tf = time.perf_counter()
-    for _ in range(3):
-        step(fresh=True)
-    fresh = B * 3 / (time.perf_counter() - tf)
-    _, addr, st = out["r"]
-    ok = ok and bool((st == 0).all()) and np.array_equal(addr, exp_h)
+    fresh = None
+    if fresh_reps:
+        tf = time.perf_counter()
+        for _ in range(fresh_reps):
+            step(fresh=True)
+        fresh = round(B * fresh_reps / (time.perf_counter() - tf), 1)
+        _, addr, st = out["r"]
+        ok = ok and bool((st == 0).all()) and np.array_equal(addr, exp_h)
     return {"batch": B, "sigs_per_s": round(B * steps / elapsed, 1), "ms_per_call": round(elapsed * 1e3 / steps, 3),
-            "steps": steps, "fresh_outputs_sigs_per_s": round(fresh, 1), "correct": ok}
+            "steps": steps, "fresh_outputs_sigs_per_s": fresh, "correct": ok}
 
 
 def run_host_throughput(c):
@@ -866,12 +1039,61 @@ def run_host_throughput(c):
     c.finish(line, ok)
 
 
+def run_c4host(c):
+    """--config c4host: configs[3]'s fixed batch handed over as host (pageable) buffers through
+    eges_ecrecover_batch with every visible device open in this one process (eges_init(0)): the
+    library splits the batch into contiguous shards, one host thread per device (capi run_host),
+    the path a Go node with several GPUs takes. Inputs are synthesised on each device for its
+    own shard and brought to the host first (untimed); every address is checked."""
+    a = c.args
+    total = a.batch or C4_TOTAL
+    if c.stub:
+        t0 = time.perf_counter()
+        time.sleep(0.002 * a.steps)
+        el = time.perf_counter() - t0
+        line = {"metric": "secp256k1 ecrecover+address/sec, host buffers over every device of one process",
+                "value": round(total * a.steps / el, 1), "unit": "sigs/s", "devices": 0, "steps": a.steps,
+                "data": "stub", "config": {"workload": "c4host stub", "total_batch": total, "correct": True}}
+        c.finish(line, True)
+        return
+    import numpy as np
+    torch = c.torch
+    from eges_amd.shard import shard_range
+    nd = c.eges.device_count()  # every visible gfx950 device (Ctx called eges_init(0))
+    msg_h = np.empty((total, 32), np.uint8)
+    sig_h = np.empty((total, 65), np.uint8)
+    exp_h = np.empty((total, 20), np.uint8)
+    ng = torch.cuda.device_count()  # (the synthesis runs per physical device)
+    for d in range(ng):
+        lo, hi = shard_range(total, d, ng)
+        for s0 in range(lo, hi, 1 << 24):  # 16M-signature pieces bound the device memory used
+            s1 = min(hi, s0 + (1 << 24))
+            with torch.cuda.device(d):
+                m, s, e = c.eges.synth_sign_dev(s0, s1 - s0, d)
+                torch.cuda.synchronize(d)
+                msg_h[s0:s1], sig_h[s0:s1], exp_h[s0:s1] = m.cpu().numpy(), s.cpu().numpy(), e.cpu().numpy()
+                del m, s, e
+    r = measure_host(c, msg_h, sig_h, exp_h, a.steps, a.warmup, fresh_reps=0)
+    line = {"metric": "secp256k1 ecrecover+address/sec, host buffers over every device of one process",
+            "value": r["sigs_per_s"], "unit": "sigs/s", "devices": nd, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": r["ms_per_call"], "higher_is_better": True, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": f"configs[3] batch of {total} signatures through eges_ecrecover_batch: pageable "
+                                   "host msg/sig in, host addresses + statuses out, split over every device in-library "
+                                   "(one host thread per device), reused output arrays",
+                       "total_batch": total, "shards": [list(shard_range(total, d, nd)) for d in range(nd)],
+                       "correct": r["correct"]}}
+    c.finish(line, r["correct"])
+
+
 def main():
     args = parse()
     launch_ranks(args)  # --gpus N: one process per GPU (before anything touches the GPU)
     c = Ctx(args)
-    if args.stub and args.config not in ("c2", "c4"):
-        sys.exit("bench.py: --stub rehearses the c2 / c4 rank logic only")
+    if args.stub and args.config not in ("c2", "c4", "c4host"):
+        sys.exit("bench.py: --stub rehearses the c2 / c4 / c4host rank logic only")
+    if args.config == "c4host":
+        run_c4host(c)
+        return
     if args.config == "c1":
         run_c1(c)
     elif args.config == "c2":

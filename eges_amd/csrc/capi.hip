@@ -305,7 +305,7 @@ int init_device(int id, DevPtr* out) {
   // generation start as the first generation's finish, filling the tail the slowest waves leave
   // (the batch inversions, amortised over 4 instead of 8, cost less than that tail): C2 +2.0 %
   // (99.4 -> 101.3 M sigs/s, 3 reps each, same box), C4 +0.1 %, VerifySignature +1.2 %.
-  const int gm = std::max(1, std::min(4, env_int("EGES_GRID_MULT", 2)));
+  const int gm = std::max(1, std::min(8, env_int("EGES_GRID_MULT", 2)));
   d->mb_recover = occupancy_recover() * d->cus * gm;
   d->mb_verify = occupancy_verify() * d->cus * gm;
   d->mb_synth = occupancy_synth() * d->cus;
@@ -1142,138 +1142,6 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
 #undef FLUSH_IN
 #undef JOIN_IN
 }
-
-// ------------------------------------------------------------------ pipelined host-buffer calls
-// Host memcpy workers (a process-wide pool, created on first use): the caller's pageable buffers
-// are copied into pinned staging by several threads at once, so that the DMA engines then move
-// them at the link's rate (tools/memcpy_probe.cpp). The calling thread takes a share too.
-class CopyPool {
- public:
-  struct Task {
-    uint8_t* dst;
-    const uint8_t* src;
-    size_t n;
-  };
-  static CopyPool& get() {
-    static CopyPool* p = new CopyPool(4);  // never destroyed: detached workers live to process exit
-    return *p;
-  }
-  // The tasks' bytes in segments of about seg bytes (whole pieces, never across tasks): the workers
-  // copy, and the calling thread runs on_seg(task, offset, bytes) for each segment as soon as its
-  // pieces are done, in order (e.g. the segment's DMA, which then overlaps the next copies).
-  template <class F>
-  void run_segments(const std::vector<Task>& tasks, size_t seg, F&& on_seg) {
-    struct Seg {
-      size_t task, off, n, p0, np;
-    };
-    std::vector<Task> pieces;
-    std::vector<Seg> segs;
-    const size_t per = std::max<size_t>(1, seg / PIECE);
-    for (size_t t = 0; t < tasks.size(); ++t)
-      for (size_t o = 0; o < tasks[t].n;) {
-        Seg s{t, o, 0, pieces.size(), 0};
-        for (size_t k = 0; k < per && o < tasks[t].n; ++k, o += PIECE) {
-          const size_t n = std::min(PIECE, tasks[t].n - o);
-          pieces.push_back({tasks[t].dst + o, tasks[t].src + o, n});
-          s.n += n;
-          ++s.np;
-        }
-        segs.push_back(s);
-      }
-    if (pieces.empty()) return;
-    std::lock_guard<std::mutex> one(run_mu_);
-    std::atomic<size_t> next{0};
-    std::unique_ptr<std::atomic<uint32_t>[]> done(new std::atomic<uint32_t>[pieces.size()]);
-    for (size_t k = 0; k < pieces.size(); ++k) done[k].store(0, std::memory_order_relaxed);
-    auto work = [&] {
-      for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
-        std::memcpy(pieces[k].dst, pieces[k].src, pieces[k].n);
-        done[k].store(1, std::memory_order_release);
-      }
-    };
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      job_ = work;
-      ++gen_;
-    }
-    cv_.notify_all();
-    for (const Seg& s : segs) {
-      for (size_t k = s.p0; k < s.p0 + s.np; ++k)
-        while (!done[k].load(std::memory_order_acquire)) {
-          // no worker woke yet (or all are busy elsewhere): copy the next piece here
-          const size_t j = next.fetch_add(1);
-          if (j < pieces.size()) {
-            std::memcpy(pieces[j].dst, pieces[j].src, pieces[j].n);
-            done[j].store(1, std::memory_order_release);
-          } else {
-            cpu_relax();
-          }
-        }
-      on_seg(s.task, s.off, s.n);
-    }
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      job_ = nullptr;
-    }
-    while (active_.load(std::memory_order_acquire) != 0) cpu_relax();
-  }
-  void run(const std::vector<Task>& tasks) {
-    std::vector<Task> pieces;
-    for (const Task& t : tasks)
-      for (size_t o = 0; o < t.n; o += PIECE) pieces.push_back({t.dst + o, t.src + o, std::min(PIECE, t.n - o)});
-    if (pieces.empty()) return;
-    std::lock_guard<std::mutex> one(run_mu_);  // one job at a time (several devices' threads may call)
-    std::atomic<size_t> next{0}, left{pieces.size()};
-    auto work = [&] {
-      for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
-        std::memcpy(pieces[k].dst, pieces[k].src, pieces[k].n);
-        left.fetch_sub(1, std::memory_order_release);
-      }
-    };
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      job_ = work;
-      ++gen_;
-    }
-    cv_.notify_all();
-    work();
-    while (left.load(std::memory_order_acquire) != 0) cpu_relax();
-    {
-      std::lock_guard<std::mutex> lk(mu_);  // workers that wake late find no job ...
-      job_ = nullptr;
-    }
-    // ... and none still inside this one touches its (stack) state after we return
-    while (active_.load(std::memory_order_acquire) != 0) cpu_relax();
-  }
-
- private:
-  static constexpr size_t PIECE = size_t(1) << 20;
-  explicit CopyPool(int n) {
-    for (int i = 0; i < n; ++i) std::thread([this] { loop(); }).detach();
-  }
-  void loop() {
-    uint64_t seen = 0;
-    for (;;) {
-      std::function<void()> job;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
-        job = job_;
-        if (job) active_.fetch_add(1, std::memory_order_relaxed);
-      }
-      if (job) {
-        job();
-        active_.fetch_sub(1, std::memory_order_release);
-      }
-    }
-  }
-  std::mutex mu_, run_mu_;
-  std::condition_variable cv_;
-  std::function<void()> job_;
-  uint64_t gen_ = 0;
-  std::atomic<int> active_{0};
-};
 
 // Contiguous index shards across the engine's devices.
 int run_host(const HostJob& j, size_t n) {

@@ -127,6 +127,7 @@ class RefLib:
         L.eref_pubkey.argtypes = [P, P]
         L.eref_ecrecover_batch_mt.argtypes = [SZ, P, P, P, P, P, I]
         L.eref_sender_batch_mt.argtypes = [SZ, I, ctypes.c_ulonglong, P, P, P, P, P, P, P, I]
+        L.eref_verify_batch_mt.argtypes = [SZ, P, P, P, P, P, I]
         self.L = L
 
     def ecrecover(self, msg: bytes, sig: bytes):
@@ -137,14 +138,17 @@ class RefLib:
         _rec("eref_ecrecover", m, s, r, pub)
         return r, pub.tobytes()
 
-    def ecrecover_batch_mt(self, msg, sig, nthreads):
+    def ecrecover_batch_mt(self, msg, sig, nthreads, want_addr=True):
+        """want_addr=False: the recovery alone (secp256k1_ext_ecdsa_recover per item, no Keccak),
+        addr comes back None."""
         msg = np.ascontiguousarray(msg, np.uint8)
         sig = np.ascontiguousarray(sig, np.uint8)
         n = msg.shape[0]
         pub = np.zeros((n, 65), np.uint8)
-        addr = np.zeros((n, 20), np.uint8)
+        addr = np.zeros((n, 20), np.uint8) if want_addr else None
         ret = np.zeros(n, np.int8)
-        self.L.eref_ecrecover_batch_mt(n, _p(msg), _p(sig), _p(pub), _p(addr), _p(ret), int(nthreads))
+        self.L.eref_ecrecover_batch_mt(n, _p(msg), _p(sig), _p(pub), _p(addr) if want_addr else None, _p(ret),
+                                       int(nthreads))
         _rec("eref_batch_mt", n, msg, sig, int(nthreads), pub, addr, ret)
         return pub, addr, ret
 
@@ -158,3 +162,13 @@ class RefLib:
         self.L.eref_sender_batch_mt(n, int(signer), int(chain_id), _p(sighash), _p(r), _p(s), _p(v), _p(vflags), _p(addr),
                                     _p(st), int(nthreads))
         return addr, st
+
+    def verify_batch_mt(self, pub, publen, msg, sig64, nthreads):
+        """crypto.VerifySignature per item (secp256.go:126-134 over ext.h:58-75): pub [n, 65]
+        (the first publen[i] bytes used), msg [n, 32], sig64 [n, 64] -> ok [n] (1 / 0; 255 = the
+        reference's illegal-argument callback fired)."""
+        pub, publen, msg, sig64 = (np.ascontiguousarray(x, np.uint8) for x in (pub, publen, msg, sig64))
+        n = msg.shape[0]
+        ok = np.zeros(n, np.uint8)
+        self.L.eref_verify_batch_mt(n, _p(pub), _p(publen), _p(msg), _p(sig64), _p(ok), int(nthreads))
+        return ok

@@ -201,3 +201,42 @@ void eref_sender_batch_mt(size_t n, int signer, unsigned long long chain_id, con
     }
     for (t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
 }
+
+/* ---- crypto.VerifySignature over the reference libsecp256k1 (TEST INFRASTRUCTURE) ----
+ * Per item: eref_verify (secp256.go:126-134 -> ext.h:58-75) on pub[65*i .. 65*i+publen[i]),
+ * msg[32*i], sig[64*i]; ok_out[i] = 1 valid, 0 invalid, 255 illegal-arg panic. One pthread per
+ * worker; the GPU tests compare the engine's VerifySignature mode with it item for item. */
+typedef struct {
+    size_t lo, hi;
+    const unsigned char *pub, *publen, *msg, *sig;
+    unsigned char *ok;
+} eref_verify_job;
+
+static void *eref_verify_worker(void *p) {
+    eref_verify_job *j = (eref_verify_job *)p;
+    for (size_t i = j->lo; i < j->hi; ++i) {
+        const int r = eref_verify(j->sig + 64 * i, j->msg + 32 * i, j->pub + 65 * i, j->publen[i]);
+        j->ok[i] = (unsigned char)(r < 0 ? 255 : r);
+    }
+    return NULL;
+}
+
+void eref_verify_batch_mt(size_t n, const unsigned char *pub, const unsigned char *publen, const unsigned char *msg,
+                          const unsigned char *sig, unsigned char *ok_out, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 1024) nthreads = 1024;
+    ctx_get();
+    pthread_t th[1024];
+    eref_verify_job jobs[1024];
+    size_t per = (n + (size_t)nthreads - 1) / (size_t)nthreads;
+    int t;
+    for (t = 0; t < nthreads; ++t) {
+        size_t lo = (size_t)t * per, hi = lo + per;
+        if (lo > n) lo = n;
+        if (hi > n) hi = n;
+        eref_verify_job jb = {lo, hi, pub, publen, msg, sig, ok_out};
+        jobs[t] = jb;
+        pthread_create(&th[t], NULL, eref_verify_worker, &jobs[t]);
+    }
+    for (t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+}

@@ -179,3 +179,15 @@ def test_ref_backed_sender_reproduces_golden():
                                     g["vflags"][sel], 4)
         assert np.array_equal(st, g["status"][sel]), (signer, cid)
         assert np.array_equal(a, g["addr"][sel]), (signer, cid)
+
+
+def test_ref_verify_batch_mt_golden():
+    """oracle/_ref's multi-threaded VerifySignature (the GPU tests' item-for-item checker at
+    size) gives the golden fixtures' results on all 591 items, on 1 and on 7 threads."""
+    from oracle import RefLib, have_ref
+    if not have_ref():
+        pytest.skip("oracle/_ref not built")
+    g = load_golden("verify.npz")
+    for t in (1, 7):
+        ok = RefLib().verify_batch_mt(g["pub"], g["publen"], g["msg"], g["sig"], t)
+        assert np.array_equal(ok, g["ok"]), t

@@ -151,7 +151,7 @@ def test_bench_rank_logic_two_ranks(config):
     shard_range of the fixed total), times between barriers, the max over ranks and the
     correctness reduce come back to rank 0, whose line names both ranks."""
     rc, line, err = _bench(["--stub", "--gpus", "2", "--steps", "3", "--warmup", "1", "--config", config,
-                            "--batch", "1001"])
+                            "--batch", "1001", "--c4-total", "3001"])
     assert rc == 0, err[-2000:]
     assert line["n_gpus"] == 2 and len(line["ranks"]) == 2
     assert sorted(r["rank"] for r in line["ranks"]) == [0, 1]
@@ -167,6 +167,15 @@ def test_bench_rank_logic_two_ranks(config):
     assert abs(line["value"] - line["config"]["total_batch"] * 3 / (line["ms_per_step"] * 3 / 1e3)) \
         <= 1e-3 * line["value"] + 1.0
     assert line["config"]["correct"] is True
+    if config == "c2":
+        # the configs[3] strong-scaled leg every default line carries
+        c4 = line["secondary"]["c4_strong"]
+        assert c4["shards"] == [list(shard_range(3001, r, 2)) for r in range(2)] and c4["scaling"] == "strong"
+        assert len(c4["rank_kernel_ms"]) == 2 and len(c4["rank_elapsed_ms_per_step"]) == 2
+        assert c4["imbalance_max_over_min"] >= 1.0 and c4["correct"] is True
+        assert abs(c4["sigs_per_s"] - 3001 * c4["steps"] / (c4["ms_per_step"] * c4["steps"] / 1e3)) <= 1e-3 * c4["sigs_per_s"] + 1
+        # rank 0's child over every device of one process (stubbed: no GPU here)
+        assert line["secondary"]["c4_host_all_devices"]["config"]["total_batch"] == 3001
 
 
 def test_bench_correctness_reduce_and_world_check():
@@ -174,5 +183,22 @@ def test_bench_correctness_reduce_and_world_check():
     whose WORLD_SIZE differs from --gpus is refused"""
     rc, line, _ = _bench(["--stub", "--gpus", "2", "--steps", "2", "--warmup", "0"], {"EGES_BENCH_STUB_BAD_RANK": "1"})
     assert rc != 0 and line["config"]["correct"] is False
+    assert line["secondary"]["c4_strong"]["correct"] is False  # the bad rank's strong-leg check reaches rank 0
     rc, line, err = _bench(["--stub", "--gpus", "2"], {"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
     assert rc == 2 and line is None and "WORLD_SIZE=3" in err
+
+
+def test_strong_summary_imbalance():
+    """bench.strong_summary: the slowest rank sets the rate, idle (empty) shards are left out of
+    the imbalance, and one rank's failed check fails the leg."""
+    import importlib.util
+    from conftest import ROOT
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    sh = [shard_range(3, r, 4) for r in range(4)]  # [0,1) [1,2) [2,3) [3,3)
+    s = b.strong_summary(3, sh, 2, [(0.2, 10.0, True), (0.4, 20.0, True), (0.3, 15.0, True), (0.1, 0.0, True)])
+    assert s["ms_per_step"] == 200.0 and s["sigs_per_s"] == 15.0
+    assert s["imbalance_max_over_min"] == 2.0 and s["correct"] is True
+    s = b.strong_summary(3, sh, 2, [(0.2, 10.0, True), (0.4, 20.0, False), (0.3, 15.0, True), (0.1, 0.0, True)])
+    assert s["correct"] is False

@@ -1,0 +1,14 @@
+# Round-5 pass a: every GPU test, smoke and the default bench line on the sources after the
+# removal of the measured-slower paths (pinned pipeline, block server).
+set -eo pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+O=gpurun_out/r05_a
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -60 $O/pytest.txt; exit 1; }
+tail -1 $O/pytest.txt
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1
+tail -1 $O/smoke.txt
+timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
+cat $O/bench.json
+echo done rc=0
