@@ -46,7 +46,7 @@ DEV bool ho_failed(const uint32_t* err, const Diag& dg) {
   if (bad) diag_bump(dg, EGES_DIAG_HANDOFF);
   return bad;
 }
-// Host-buffer calls launch before their inputs are in the pinned buffer (capi.hip Gate): the
+// Host-buffer calls launch before their inputs are in the pinned buffer (hostpath.hip Gate): the
 // host copies them while the launch is in flight and then stores the call's sequence into the
 // gate word (coherent pinned memory). Workgroup 0's first wave alone polls that word (a poller
 // per wave over PCIe slowed a 1,000-workgroup launch 2.4x) and mirrors the sequence into a
@@ -80,7 +80,7 @@ DEV void gate_wait(const uint32_t* gate, uint32_t* mirror, uint32_t seq) {
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
-// A gated call's completion (capi.hip run_host_shard): after its last output each workgroup
+// A gated call's completion (hostpath.hip run_host_shard): after its last output each workgroup
 // counts itself done (system-scope release first); the last one stores the call's sequence into
 // gate[2], which the host polls instead of synchronising the stream (the kernel-end signal's
 // path measured ~5 us from the kernel's end to the sync's return). At kernel level, after the

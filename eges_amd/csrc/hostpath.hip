@@ -1,0 +1,882 @@
+// Host-buffer paths (engine.h): the one-launch form of large ecrecover shards, the chunked
+// pipeline of everything else, the multi-device split, the Geec block split and the host Keccak.
+#include "engine.h"
+
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
+
+namespace eges::host {
+
+// Host-side phase stamps of the last host-buffer call (diagnostic build only, tools/block_bench):
+// 0 entry, 1 lane / device acquired, 2 inputs packed, 3 launches enqueued, 4 streams drained,
+// 5 outputs unpacked (steady_clock, ns).
+#ifdef EGES_PHASE_STAMPS
+static int64_t g_hstamp[6];
+#define HSTAMP(k) (g_hstamp[k] = std::chrono::steady_clock::now().time_since_epoch().count())
+extern "C" size_t eges_diag_host_stamps(int64_t* out, size_t n) {
+  for (size_t k = 0; k < n && k < 6; ++k) out[k] = g_hstamp[k];
+  return 6;
+}
+#else
+#define HSTAMP(k) ((void)0)
+#endif
+// ------------------------------------------------------------------ host-buffer pipelines
+
+// Device bytes of one pipeline region for a chunk of m items: inputs | scratch | outputs.
+struct Region {
+  size_t in_bytes = 0, raw_lo = 0, raw_len = 0, o_rec = 0, o_out = 0, total = 0;
+};
+Region region_for(const HostJob& j, size_t base, size_t m) {
+  Region g;
+  const size_t m_pad = align_up(m, 64);
+  switch (j.kind) {
+    case HostJob::RECOVER: g.in_bytes = m * (32 + 65); break;
+    case HostJob::SENDER: g.in_bytes = m * (32 * 4 + 1); break;
+    case HostJob::VERIFY: g.in_bytes = m * (65 + 1 + 32 + 64); break;
+    case HostJob::PRECOMPILE: g.in_bytes = m * (128 + 4); break;
+    case HostJob::SENDER_RAW:
+      g.raw_lo = j.offsets[base] - j.offsets[0];
+      g.raw_len = j.offsets[base + m] - j.offsets[base];
+      g.in_bytes = align_up(g.raw_len, 8) + 8 * (m + 1) + tx_rows_bytes(m);
+      break;
+  }
+  const size_t rec_bytes = (j.kind == HostJob::VERIFY) ? verify_scratch_bytes(m_pad) : recover_scratch_bytes(m_pad);
+  g.o_rec = align_up(g.in_bytes, 256);
+  g.o_out = g.o_rec + align_up(rec_bytes, 256);
+  g.total = align_up(g.o_out + m * (65 + 32 + 1), 256);
+  return g;
+}
+
+// Writes the pieces of a host-buffer launch into pinned staging with several threads: every piece
+// is cut into 1 MB chunks that the threads take in order (work stealing; the calling thread is one
+// of them, so the call never waits for a worker to wake), and the caller publishes piece p (the
+// word the kernel mirrors) as soon as all of its chunks and those of the pieces before it are in
+// place. Each thread fences its own (non-temporal) stores before it counts a chunk done.
+// Copy with non-temporal stores (the bytes go to memory, not into this core's cache), the
+// unaligned head and tail with ordinary stores whose lines are then flushed (EGES_TEST_HOST_ONE
+// bit 2). The caller fences.
+void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+#if defined(__x86_64__)
+  size_t head = (16 - ((uintptr_t)dst & 15)) & 15;
+  if (head > n) head = n;
+  std::memcpy(dst, src, head);
+  size_t i = head;
+  for (; i + 16 <= n; i += 16)
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i)));
+  std::memcpy(dst + i, src + i, n - i);
+  if (head) _mm_clflush(dst);
+  if (i < n) _mm_clflush(dst + i);
+#else
+  std::memcpy(dst, src, n);
+#endif
+}
+
+class Feeder {
+ public:
+  struct Span {
+    uint8_t* dst;
+    const uint8_t* src;
+    size_t n;
+  };
+  static Feeder& get() {
+    static Feeder* f = new Feeder(15);  // never destroyed: detached workers live to process exit
+    return *f;
+  }
+  // pieces[p]: the spans of piece p; publish(p) is called in order by this thread; threads: the
+  // workers joined (0 .. 15) besides the caller
+  template <class F>
+  void run(const std::vector<std::vector<Span>>& pieces, int threads, bool nt, F&& publish) {
+    std::vector<Chunk> chunks;
+    std::vector<uint32_t> per(pieces.size(), 0);
+    for (size_t p = 0; p < pieces.size(); ++p)
+      for (const Span& sp : pieces[p])
+        for (size_t o = 0; o < sp.n; o += CHUNK_BYTES) {
+          chunks.push_back({sp.dst + o, sp.src + o, std::min(CHUNK_BYTES, sp.n - o), (uint32_t)p});
+          ++per[p];
+        }
+    std::unique_ptr<std::atomic<uint32_t>[]> done(new std::atomic<uint32_t>[pieces.size()]);
+    for (size_t p = 0; p < pieces.size(); ++p) done[p].store(0, std::memory_order_relaxed);
+    std::atomic<size_t> next{0};
+    auto take_one = [&]() -> bool {
+      const size_t k = next.fetch_add(1, std::memory_order_relaxed);
+      if (k >= chunks.size()) return false;
+      if (nt) stream_copy(chunks[k].dst, chunks[k].src, chunks[k].n);
+      else std::memcpy(chunks[k].dst, chunks[k].src, chunks[k].n);
+#if defined(__x86_64__)
+      __builtin_ia32_sfence();
+#endif
+      done[chunks[k].piece].fetch_add(1, std::memory_order_release);
+      return true;
+    };
+    std::lock_guard<std::mutex> one(run_mu_);  // one feed at a time (several devices' threads may call)
+    const int want = std::max(0, std::min(threads, (int)nworkers_));
+    if (want > 0 && chunks.size() > 1) {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = [&] { while (take_one()) {} };
+      quota_ = want;
+      ++gen_;
+    }
+    if (want > 0 && chunks.size() > 1) cv_.notify_all();
+    size_t pub = 0;
+    auto flush = [&] {  // publish every complete piece, in order
+      while (pub < pieces.size() && done[pub].load(std::memory_order_acquire) == per[pub]) publish(pub++);
+    };
+    while (take_one()) flush();
+    while (pub < pieces.size()) {
+      flush();
+      cpu_relax();
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);  // workers that wake late find no job ...
+      job_ = nullptr;
+    }
+    // ... and none still inside this one touches its (stack) state after we return
+    while (active_.load(std::memory_order_acquire) != 0) cpu_relax();
+  }
+
+ private:
+  static constexpr size_t CHUNK_BYTES = size_t(1) << 20;
+  struct Chunk {
+    uint8_t* dst;
+    const uint8_t* src;
+    size_t n;
+    uint32_t piece;
+  };
+  explicit Feeder(int n) : nworkers_(n) {
+    for (int i = 0; i < n; ++i) std::thread([this] { loop(); }).detach();
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      std::function<void()> job;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (quota_ <= 0 || !job_) continue;  // (enough workers joined this feed)
+        --quota_;
+        job = job_;
+        active_.fetch_add(1, std::memory_order_relaxed);
+      }
+      job();
+      active_.fetch_sub(1, std::memory_order_release);
+    }
+  }
+  const int nworkers_;
+  std::mutex mu_, run_mu_;
+  std::condition_variable cv_;
+  std::function<void()> job_;
+  int quota_ = 0;
+  uint64_t gen_ = 0;
+  std::atomic<int> active_{0};
+};
+
+// One lane-serial launch over a whole host-buffer ecrecover shard (2 * PIPE_MIN .. CHUNK
+// signatures; the Go caller's large crypto.Ecrecover batches). The chunked pipeline below runs
+// such a shard as several launches of one signature per thread, each ending in a partial
+// generation; this form launches once, with the grid and slots of the device-resident call, and
+// lets the kernel start while this thread is still writing its inputs:
+//  - the inputs go into pinned staging as pieces in the order the waves read them (the first
+//    resident generation's threads slot 0, slot 1, ..., then the next generation's); after each
+//    piece this thread stores the piece count into a coherent word, which block 0 of the launch
+//    mirrors into device memory; a wave waits for its piece before it parses a slot straight
+//    from the staging (k_recover.hip ls_mirror / ls_wait / ls_parse: no copy engine, no prep
+//    launch: a copy engine's small transfers or a blit kernel would wait for CUs the launch holds);
+//  - the kernel writes its outputs into pinned memory, and each block marks its done word after
+//    its stores, so this thread copies a block's outputs to the caller while the others run.
+// The call returns when every block is done and the stream has drained.
+constexpr uint32_t LS_PIECES = 256;  // pieces per call at most (sequence stride)
+constexpr size_t LS_CTL_DONE = 64;   // control words: 0 the host's piece count, 1 the fault word, done from 64
+bool host_one_fits(const Dev& d, const Route& rt, const HostJob& j, size_t cnt) {
+  if (rt.host_one == 0 || j.kind != HostJob::RECOVER || cnt < 2 * PIPE_MIN || cnt > CHUNK) return false;
+  const int grid = lane_serial_grid((uint32_t)cnt, d.mb_recover);
+  const size_t gt = (size_t)grid * threads_per_block(), group = (size_t)d.res_blocks * threads_per_block();
+  if (d.res_blocks <= 0 || grid + 1 > d.ws_blocks) return false;
+  return ((gt + group - 1) / group) * ((cnt + gt - 1) / gt) < LS_PIECES;
+}
+
+template <class T>
+int ensure_pinned(T*& p, size_t& cap, size_t bytes, unsigned flags, hipEvent_t last) {
+  if (bytes <= cap) return EGES_SUCCESS;
+  if (p) {
+    HIPCHK(hipEventSynchronize(last));
+    (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  if (hipHostMalloc(reinterpret_cast<void**>(&p), bytes, flags) != hipSuccess) {
+    p = nullptr;
+    return set_err(EGES_E_NOMEM, "hipHostMalloc(%zu) failed", bytes);
+  }
+  cap = bytes;
+  return EGES_SUCCESS;
+}
+
+int run_host_one(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t cnt) {
+  DevGuard g(d.id);
+  DeviceWide wide(d);
+  const uint32_t n = (uint32_t)cnt;
+  const size_t n_pad = align_up(cnt, 64);
+  const uint32_t wg = (uint32_t)threads_per_block();
+  const int grid = lane_serial_grid(n, d.mb_recover);
+  const uint32_t GT = (uint32_t)grid * wg, group = (uint32_t)d.res_blocks * wg;
+  const uint32_t kmax = (n + GT - 1) / GT, ngroups = (GT + group - 1) / group;
+  int rc = dev_ensure_buf(d, recover_scratch_bytes(n_pad));  // records and slots
+  if (rc) return rc;
+  // pinned: inputs msg | sig, outputs status | addr | pub, control words
+  const size_t o_sig = align_up(cnt * 32, 256);
+  const size_t o_addr = align_up(cnt, 256), o_pub = o_addr + align_up(cnt * 20, 256);
+  if ((rc = ensure_pinned(d.ls_in, d.ls_in_cap, o_sig + cnt * 65, hipHostMallocDefault, d.last))) return rc;
+  const bool coherent_out = (rt.test_host_one & 2u) != 0;
+  if (d.ls_out && d.ls_out_coherent != coherent_out) {  // (a probe switched the memory type)
+    HIPCHK(hipEventSynchronize(d.last));
+    (void)hipHostFree(d.ls_out);
+    d.ls_out = nullptr;
+    d.ls_out_cap = 0;
+  }
+  if ((rc = ensure_pinned(d.ls_out, d.ls_out_cap, o_pub + (j.pub ? cnt * 65 : 0),
+                          coherent_out ? hipHostMallocCoherent : hipHostMallocDefault, d.last)))
+    return rc;
+  d.ls_out_coherent = coherent_out;
+  size_t ctl_bytes = d.ls_ctl_words * 4;
+  if ((rc = ensure_pinned(d.ls_ctl, ctl_bytes, (LS_CTL_DONE + (size_t)d.ws_blocks) * 4, hipHostMallocCoherent, d.last)))
+    return rc;
+  d.ls_ctl_words = ctl_bytes / 4;
+  if (!d.ls_arr) {
+    if (hipMalloc(&d.ls_arr, 256) != hipSuccess) {
+      d.ls_arr = nullptr;
+      return set_err(EGES_E_NOMEM, "hipMalloc(arrival word) failed");
+    }
+    HIPCHK(hipMemset(d.ls_arr, 0, 256));
+  }
+  // the previous call's kernel is done with the staging, outputs and control words
+  HIPCHK(hipEventSynchronize(d.last));
+  uint32_t* host_word = d.ls_ctl;
+  uint32_t* fault = d.ls_ctl + 1;
+  uint32_t* done = d.ls_ctl + LS_CTL_DONE;
+  d.ls_seq += LS_PIECES;
+  const uint32_t seq = d.ls_seq;
+  const uint32_t npieces = ngroups * kmax;
+  std::memset(done, 0, (size_t)grid * 4);
+  __atomic_store_n(fault, 0u, __ATOMIC_RELAXED);
+  __atomic_store_n(host_word, seq, __ATOMIC_RELEASE);  // no piece yet
+  uint8_t* const im = d.ls_in;
+  uint8_t* const is = d.ls_in + o_sig;
+  uint8_t* const o_st = d.ls_out;
+  RecoverParams p{reinterpret_cast<uint32_t*>(d.buf), n, (uint32_t)n_pad, o_st, j.addr ? d.ls_out + o_addr : nullptr,
+                  j.pub ? d.ls_out + o_pub : nullptr, d.gtab, d.ws};
+  p.ls_msg = im;
+  p.ls_sig = is;
+  p.ls_arrived = d.ls_arr;
+  p.ls_host = host_word;
+  p.ls_seq = seq;
+  p.ls_final = seq + npieces;
+  p.ls_group = group;
+  p.ls_kmax = kmax;
+  p.ls_done = done;
+  p.ls_fault = fault;
+  hipStream_t st = d.stream;
+  struct Drain {  // every return waits for the launch first (it reads the staging this call owns)
+    hipStream_t a;
+    uint32_t* word;
+    uint32_t final;
+    bool armed;
+    ~Drain() {
+      if (!armed) return;
+      __atomic_store_n(word, final, __ATOMIC_RELEASE);  // (no wave waits for a piece that will not come)
+      (void)hipStreamSynchronize(a);
+    }
+  } drain{st, host_word, seq + npieces, true};
+  // the pieces in the order the waves read them: generation gi's threads, slot k
+  std::vector<std::vector<Feeder::Span>> pieces(npieces);
+  for (uint32_t gi = 0; gi < ngroups; ++gi)
+    for (uint32_t k = 0; k < kmax; ++k) {
+      const size_t lo = (size_t)k * GT + (size_t)gi * group;
+      const size_t hi = std::min<size_t>({lo + group, (size_t)(k + 1) * GT, cnt});
+      if (lo < hi)
+        pieces[gi * kmax + k] = {{im + lo * 32, j.a + (off + lo) * 32, (hi - lo) * 32},
+                                 {is + lo * 65, j.b + (off + lo) * 65, (hi - lo) * 65}};
+    }
+  HIPCHK(launch_recover_host(with_diag(d, p, rt), grid, d.ws_blocks, st));
+  HIPCHK(hipEventRecord(d.last, st));
+  Feeder::get().run(pieces, (int)rt.feeders - 1, (rt.test_host_one & 4u) != 0,
+                    [&](size_t pc) { publish_u32(host_word, seq + (uint32_t)pc + 1); });
+  // outputs: block by block as their done words appear
+  bool missing = false;
+  for (int b = 0; b < grid && !missing; ++b) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spins = 0; __atomic_load_n(done + b, __ATOMIC_ACQUIRE) != seq; ++spins) {
+      cpu_relax();
+      if ((spins & 1023) == 1023 && (hipStreamQuery(st) == hipSuccess ||
+                                     std::chrono::steady_clock::now() - t0 > std::chrono::seconds(8))) {
+        missing = __atomic_load_n(done + b, __ATOMIC_ACQUIRE) != seq;
+        break;
+      }
+    }
+    for (uint32_t k = 0; k < kmax && !missing; ++k) {
+      const size_t lo = (size_t)k * GT + (size_t)b * wg;
+      if (lo >= cnt) break;
+      const size_t m = std::min<size_t>(wg, cnt - lo);
+      if (j.status) std::memcpy(j.status + off + lo, o_st + lo, m);
+      if (j.addr) std::memcpy(j.addr + (off + lo) * 20, d.ls_out + o_addr + lo * 20, m * 20);
+      if (j.pub) std::memcpy(j.pub + (off + lo) * 65, d.ls_out + o_pub + lo * 65, m * 65);
+    }
+  }
+  drain.armed = false;
+  HIPCHK(hipStreamSynchronize(st));
+  if (__atomic_load_n(fault, __ATOMIC_ACQUIRE) != 0u) return set_err(EGES_E_HIP, "an input piece was not seen in time");
+  if (missing) return set_err(EGES_E_HIP, "a block of the one-launch host form never marked its outputs done");
+  if (rt.test_host_one & 1u) {  // probe: did any block's outputs change after this thread copied them?
+    size_t changed = 0, first = SIZE_MAX;
+    for (size_t i = 0; i < cnt; ++i) {
+      const bool same = (!j.status || j.status[off + i] == o_st[i]) &&
+                        (!j.addr || std::memcmp(j.addr + (off + i) * 20, d.ls_out + o_addr + i * 20, 20) == 0) &&
+                        (!j.pub || std::memcmp(j.pub + (off + i) * 65, d.ls_out + o_pub + i * 65, 65) == 0);
+      if (!same && changed++ == 0) first = i;
+    }
+    if (changed) return set_err(EGES_E_HIP, "recheck: %zu items changed after their block was copied (first %zu)", changed, first);
+  }
+  return EGES_SUCCESS;
+}
+
+// Host-buffer pipeline over chunks of one shard. Two device regions alternate: while the
+// compute stream runs chunk i, the copy stream stages chunk i+1's inputs and returns chunk
+// i-1's outputs (host order H2D(i+1), K(i+1), D2H(i): the pageable D2H blocks this thread
+// until K(i) is done, by which time K(i+1) is queued behind it). Synchronous overall.
+int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t cnt) {
+  if (host_one_fits(d, rt, j, cnt)) return run_host_one(d, rt, j, off, cnt);
+  HSTAMP(0);
+  DevGuard g(d.id);
+  // a shard big enough to pipeline runs as >= 2 chunks (each still a full resident grid)
+  size_t c = std::min(CHUNK, cnt);
+  if (cnt >= 2 * PIPE_MIN && c > cnt / 2)
+    c = std::min(CHUNK, std::max(PIPE_MIN / 2, align_up((cnt + rt.host_parts - 1) / rt.host_parts, 64)));
+  size_t worst = 0;  // region size: SENDER_RAW depends on the bytes of each chunk
+  for (size_t base = off; base < off + cnt; base += c) worst = std::max(worst, region_for(j, base, std::min(c, off + cnt - base)).total);
+  const int nreg = cnt > c ? 2 : 1;
+  const bool pinned = nreg == 1 && worst <= PIN_BYTES;
+  // Small calls on the latency kernel (no shared workspace) run on one of the device's lanes,
+  // concurrently with each other; everything else on the device's main resources, in order.
+  const bool small = pinned && cnt <= rt.lat_max;
+  Lane* lane = nullptr;
+  std::unique_lock<std::mutex> lk;
+  std::unique_ptr<DeviceWide> wide;
+  if (small) {
+    for (Lane& l : d.lanes) {
+      std::unique_lock<std::mutex> t(l.mu, std::try_to_lock);
+      if (t.owns_lock() && !l.reserved.load(std::memory_order_acquire)) {
+        lane = &l;
+        lk = std::move(t);
+        break;
+      }
+    }
+    while (!lane) {
+      static std::atomic<unsigned> rr{0};
+      Lane& l = d.lanes[rr++ % NLANES];
+      std::unique_lock<std::mutex> t(l.mu);
+      if (l.reserved.load(std::memory_order_acquire)) continue;  // (the resident server's)
+      lane = &l;
+      lk = std::move(t);
+    }
+  } else {
+    wide = std::make_unique<DeviceWide>(d);  // device-wide work: the resident server leaves the CUs first
+  }
+  uint8_t*& dbuf = small ? lane->buf : d.buf;
+  uint8_t*& pin = small ? lane->pin : d.pin;
+  hipEvent_t* ev_in = small ? lane->ev_in : d.ev_in;
+  hipEvent_t* ev_k = small ? lane->ev_k : d.ev_k;
+  int rc = small ? ensure_buf(lane->buf, lane->buf_cap, lane->stream, nullptr, worst, size_t(4) << 20)
+                 : dev_ensure_buf(d, worst * nreg);
+  if (rc) return rc;
+  // a single chunk has nothing to overlap: one stream, no cross-stream waits (C3 latency)
+  hipStream_t st = small ? lane->stream : d.stream, sx = nreg > 1 ? d.copy : st;
+  // Every return after this point (errors included) first drains every stream, so the lane /
+  // device mutex is never released while kernels or copies of this call still touch its
+  // pinned staging or scratch (the next caller writes its inputs there).
+  struct Drain {
+    hipStream_t a, b;
+    bool armed;
+    ~Drain() {
+      if (!armed) return;
+      (void)hipStreamSynchronize(a);
+      if (b != a) (void)hipStreamSynchronize(b);
+    }
+  } drain{st, sx, true};
+  if (pinned && !pin && hipHostMalloc(&pin, PIN_BYTES, hipHostMallocDefault) != hipSuccess) {
+    pin = nullptr;
+    return set_err(EGES_E_NOMEM, "hipHostMalloc(%zu) failed", PIN_BYTES);
+  }
+  // A pinned call whose mid-size kernel reads the inputs itself (the fused bucket / windowed forms)
+  // launches first and copies its inputs into the pinned buffer while the launch is in flight:
+  // the kernels wait at the gate (handoff.cuh gate_wait), which opens after the copies. Opening is
+  // also the guard's destructor, so no return path leaves a launched kernel waiting (declared
+  // after `drain`: it runs first).
+  Gate& gate = d.gate;  // (the mid-size kernels run above EGES_LAT_MAX: never on a lane)
+  const bool gating = pinned && !small && rt.gate != 0 &&
+                      (j.kind == HostJob::RECOVER || j.kind == HostJob::SENDER || (j.kind == HostJob::SENDER_RAW && !j.decode_only));
+  if (gating && !gate.w) {
+    if (hipHostMalloc(&gate.w, 64, hipHostMallocCoherent) != hipSuccess) {
+      gate.w = nullptr;
+      return set_err(EGES_E_NOMEM, "hipHostMalloc(gate) failed");
+    }
+    std::memset(gate.w, 0, 64);
+    if (hipMalloc(&gate.dev, 64) != hipSuccess || hipMemset(gate.dev, 0, 64) != hipSuccess) {
+      (void)hipHostFree(gate.w);
+      gate.w = nullptr;
+      gate.dev = nullptr;
+      return set_err(EGES_E_NOMEM, "hipMalloc(gate) failed");
+    }
+  }
+  struct GateOpen {
+    struct Copy {
+      uint8_t* dst;
+      const void* src;
+      size_t n;
+    } q[8];
+    int nq = 0;
+    uint32_t* w = nullptr;  // armed: the kernels wait for sequence `seq`
+    uint32_t seq = 0;
+    void open() {
+      for (int i = 0; i < nq; ++i) std::memcpy(q[i].dst, q[i].src, q[i].n);
+      nq = 0;
+      if (w) publish_u32(w, seq);
+      w = nullptr;
+    }
+    ~GateOpen() { open(); }
+  } gopen;
+  bool defer = false;  // this chunk's inputs wait for gopen.open()
+  bool gated = false;  // a gated mid-size launch ran: its last workgroup stores the sequence into gate.w[2]
+  auto arm = [&](RecoverParams& p) {  // a deferred chunk's kernels wait at the gate
+    if (!defer || p.n == 0) return;
+    if (++gate.seq == 0) gate.seq = 1;
+    gated = true;  // (a mid-size launch: its kernels store the completion word)
+    p.gate = gate.w;
+    p.gate_dev = gate.dev;
+    p.gate_seq = gate.seq;
+    gopen.w = gate.w;
+    gopen.seq = gate.seq;
+  };
+  // VerifySignature: a hand-off fault leaves its item's ok byte 0 and stores 1 into this word
+  uint32_t*& vfault = small ? lane->vfault : d.vfault;
+  if (j.kind == HostJob::VERIFY) {
+    if (!vfault && hipHostMalloc(&vfault, 64, hipHostMallocCoherent) != hipSuccess) {
+      vfault = nullptr;
+      return set_err(EGES_E_NOMEM, "hipHostMalloc(fault word) failed");
+    }
+    __atomic_store_n(vfault, 0u, __ATOMIC_RELAXED);
+  }
+  if (!small) {
+    HIPCHK(hipStreamWaitEvent(st, d.last, 0));
+    HIPCHK(hipStreamWaitEvent(sx, d.last, 0));
+  }
+  HSTAMP(1);
+  // Input staging: each input array goes to its offset in the region, either by its own
+  // (pageable) copy into device memory on the copy stream, or, for a pinned call, packed into
+  // the pinned buffer at the same offset, where the kernels read it directly (zero-copy: no
+  // H2D / D2H operations at all, the outputs are written straight into the pinned buffer too).
+  auto h2d = [&](uint8_t* B, uint8_t* dst, const void* src, size_t bytes) -> int {
+    if (!bytes) return EGES_SUCCESS;
+    if (pinned) {  // dst points into the pinned buffer (see I below)
+      if (defer && gopen.nq < 8) gopen.q[gopen.nq++] = {dst, src, bytes};
+      else std::memcpy(dst, src, bytes);  // (at most 5 inputs per kind: q never fills)
+      return EGES_SUCCESS;
+    }
+    (void)B;
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, sx));
+    return EGES_SUCCESS;
+  };
+  auto flush_in = [&](uint8_t*) -> int { return EGES_SUCCESS; };
+#define H2D(B, dst, src, bytes)                   \
+  do {                                             \
+    int rc_ = h2d((B), (dst), (src), (bytes));     \
+    if (rc_) return rc_;                           \
+  } while (0)
+#define FLUSH_IN(B)                 \
+  do {                              \
+    int rc_ = flush_in(B);          \
+    if (rc_) return rc_;            \
+    HSTAMP(2);                      \
+  } while (0)
+  // the kernels wait for their inputs' copies (a single chunk uses one stream: nothing to join)
+#define JOIN_IN(r)                                      \
+  do {                                                  \
+    if (sx != st) {                                     \
+      HIPCHK(hipEventRecord(ev_in[r], sx));             \
+      HIPCHK(hipStreamWaitEvent(sk, ev_in[r], 0));      \
+    }                                                   \
+  } while (0)
+  struct Pending {
+    size_t base, m;
+    int r;
+    uint8_t* B;
+    Region g;
+  };
+  const size_t astride = j.kind == HostJob::PRECOMPILE ? 32 : 20;
+  auto sighash_off = [&](const Pending& q) { return align_up(q.g.raw_len, 8) + 8 * (q.m + 1); };
+  auto outputs = [&](const Pending& q) -> int {  // D2H of one chunk, on the copy stream
+    uint8_t* o_pub = q.B + q.g.o_out;
+    uint8_t* o_addr = o_pub + q.m * 65;
+    uint8_t* o_st = o_addr + q.m * 32;
+    if (sx != st) HIPCHK(hipStreamWaitEvent(sx, ev_k[q.r], 0));
+    if (pinned) {  // outputs are already in the pinned buffer; the signing hashes are not
+      if (j.kind == HostJob::SENDER_RAW && j.sighash)
+        HIPCHK(hipMemcpyAsync(pin + sighash_off(q), q.B + sighash_off(q), q.m * 32, hipMemcpyDeviceToHost, sx));
+      return EGES_SUCCESS;
+    }
+    if (j.pub) HIPCHK(hipMemcpyAsync(j.pub + q.base * 65, o_pub, q.m * 65, hipMemcpyDeviceToHost, sx));
+    if (j.addr) HIPCHK(hipMemcpyAsync(j.addr + q.base * astride, o_addr, q.m * astride, hipMemcpyDeviceToHost, sx));
+    if (j.status) HIPCHK(hipMemcpyAsync(j.status + q.base, o_st, q.m, hipMemcpyDeviceToHost, sx));
+    if (j.kind == HostJob::SENDER_RAW && j.sighash)
+      HIPCHK(hipMemcpyAsync(j.sighash + q.base * 32, q.B + sighash_off(q), q.m * 32, hipMemcpyDeviceToHost, sx));
+    return EGES_SUCCESS;
+  };
+  auto unpack = [&](const Pending& q) {  // pinned mode, after the sync
+    const uint8_t* o_pub = pin + q.g.o_out;
+    const uint8_t* o_addr = o_pub + q.m * 65;
+    const uint8_t* o_st = o_addr + q.m * 32;
+    if (j.pub) std::memcpy(j.pub + q.base * 65, o_pub, q.m * 65);
+    if (j.addr) std::memcpy(j.addr + q.base * astride, o_addr, q.m * astride);
+    if (j.status) std::memcpy(j.status + q.base, o_st, q.m);
+    if (j.kind == HostJob::SENDER_RAW && j.sighash) std::memcpy(j.sighash + q.base * 32, pin + sighash_off(q), q.m * 32);
+  };
+  Pending prev{};
+  bool have_prev = false;
+  int ci = 0;
+  for (size_t base = off; base < off + cnt; base += c, ++ci) {
+    const size_t m = std::min(c, off + cnt - base);
+    const size_t m_pad = align_up(m, 64);
+    const int r = ci % nreg;
+    hipStream_t sk = st;  // this chunk's compute stream
+    uint32_t* wsk = d.ws;
+    const Region rg = region_for(j, base, m);
+    uint8_t* B = dbuf + (size_t)r * worst;
+    uint8_t* I = pinned ? pin : B;  // where the kernels read the inputs
+    uint8_t* o_pub = (pinned ? pin : B) + rg.o_out;
+    uint8_t* o_addr = o_pub + m * 65;
+    uint8_t* o_st = o_addr + m * 32;
+    uint32_t* rec = reinterpret_cast<uint32_t*>(B + rg.o_rec);
+    // --- inputs (copy stream), then the kernels (compute stream)
+    if (j.kind == HostJob::RECOVER) {
+      uint8_t* dm = I;
+      uint8_t* ds = dm + m * 32;
+      const bool fused = fused_parse(d, rt, m);
+      defer = gating && fused && use_mid(d, rt, m);  // (the latency kernels measured +-0 to +1.5 % slower)
+      H2D(B, dm, j.a + base * 32, m * 32);
+      H2D(B, ds, j.b + base * 65, m * 65);
+      FLUSH_IN(B);
+      JOIN_IN(r);
+      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, j.addr ? o_addr : nullptr, j.pub ? o_pub : nullptr,
+                      d.gtab, wsk};
+      if (fused) {  // the latency / mid-size kernels parse the bytes themselves
+        p.raw_msg = dm;
+        p.raw_sig = ds;
+      } else {
+        HIPCHK(launch_prep_ecrecover(dm, ds, (uint32_t)m, (uint32_t)m_pad, rec, sk));
+      }
+      arm(p);
+      HIPCHK(launch_recover_pass(d, rt, p, sk));
+    } else if (j.kind == HostJob::SENDER) {
+      uint8_t* dh = I;
+      uint8_t* dr = dh + m * 32;
+      uint8_t* dsv = dr + m * 32;
+      uint8_t* dv = dsv + m * 32;
+      uint8_t* df = dv + m * 32;
+      const bool fused = sender_fused(d, rt, m, {dh, dr, dsv, dv});
+      defer = gating && fused && use_mid(d, rt, m);  // (the latency kernels measured +-0 to +1.5 % slower)
+      H2D(B, dh, j.a + base * 32, m * 32);
+      H2D(B, dr, j.b + base * 32, m * 32);
+      H2D(B, dsv, j.c + base * 32, m * 32);
+      H2D(B, dv, j.d + base * 32, m * 32);
+      if (j.e) H2D(B, df, j.e + base, m);
+      FLUSH_IN(B);
+      JOIN_IN(r);
+      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, wsk};
+      if (fused)  // the recover kernel reads the rows itself
+        bind_sender_rows(p, dh, dr, dsv, dv, j.e ? df : nullptr, j.signer, j.chain_id);
+      else
+        HIPCHK(launch_prep_sender(dh, dr, dsv, dv, j.e ? df : nullptr, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id,
+                                  rec, sk));
+      arm(p);
+      HIPCHK(launch_recover_pass(d, rt, p, sk));
+    } else if (j.kind == HostJob::PRECOMPILE) {
+      uint8_t* din = I;
+      uint32_t* dlen = reinterpret_cast<uint32_t*>(din + m * 128);
+      H2D(B, din, j.a + base * 128, m * 128);
+      if (j.inlen) H2D(B, reinterpret_cast<uint8_t*>(dlen), j.inlen + base, m * 4);
+      FLUSH_IN(B);
+      JOIN_IN(r);
+      if (pinned) std::memset(o_addr, 0, m * 32);
+      else HIPCHK(hipMemsetAsync(o_addr, 0, m * 32, sk));
+      HIPCHK(launch_prep_precompile(din, j.inlen ? dlen : nullptr, (uint32_t)m, (uint32_t)m_pad, rec, sk));
+      RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr + 12, nullptr, d.gtab, wsk, 32};
+      HIPCHK(launch_recover_pass(d, rt, p, sk));
+    } else if (j.kind == HostJob::SENDER_RAW) {
+      uint8_t* draw = I;
+      uint64_t* doff = reinterpret_cast<uint64_t*>(draw + align_up(rg.raw_len, 8));
+      uint8_t* hs = B + align_up(rg.raw_len, 8) + 8 * (m + 1);  // decoded rows: device memory
+      uint8_t* rr = hs + m * 32;
+      uint8_t* sr = rr + m * 32;
+      uint8_t* vr = sr + m * 32;
+      uint8_t* vf = vr + m * 32;
+      // (the fused form reads the encodings straight from the pinned buffer: a pipelined host copy
+      // + DMA into device memory measured 0.486-0.508 ms against 0.450 ms for C1, same kernel)
+      const bool fused = !j.decode_only && wire_fused(d, rt, m, draw);
+      defer = gating && fused && use_mid(d, rt, m);  // (the latency kernels measured +-0 to +1.5 % slower)
+      if (rg.raw_len) H2D(B, draw, j.a + rg.raw_lo, rg.raw_len);
+      H2D(B, reinterpret_cast<uint8_t*>(doff), j.offsets + base, 8 * (m + 1));
+      FLUSH_IN(B);
+      JOIN_IN(r);
+      if (j.decode_only) {  // the decoder's flags straight into the status bytes
+        HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, o_st, sk));
+      } else {
+        RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, wsk};
+        if (fused) {
+          p.wire_raw = draw;
+          p.wire_off = doff;
+          p.wire_signer = j.signer;
+          p.wire_chain_id = j.chain_id;
+          p.wire_sighash = j.sighash ? hs : nullptr;
+        } else {
+          HIPCHK(launch_tx_rows(draw, doff, 0, (uint32_t)m, j.signer, j.chain_id, hs, rr, sr, vr, vf, sk));
+          HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, sk));
+        }
+        arm(p);
+        HIPCHK(launch_recover_pass(d, rt, p, sk));
+      }
+    } else {
+      uint8_t* dp = I;
+      uint8_t* dl = dp + m * 65;
+      uint8_t* dm = dl + m;
+      uint8_t* ds = dm + m * 32;
+      H2D(B, dp, j.a + base * 65, m * 65);
+      H2D(B, dl, j.b + base, m);
+      H2D(B, dm, j.c + base * 32, m * 32);
+      H2D(B, ds, j.d + base * 64, m * 64);
+      FLUSH_IN(B);
+      JOIN_IN(r);
+      VerifyParams p{dp, dl, dm, ds, (uint32_t)m, o_st, d.gtab, wsk};
+      verify_scratch_bind(p, B + rg.o_rec, m_pad);
+      p = with_diag(d, p, rt);
+      p.fault = vfault;
+      // small (lane) calls must not touch the device's shared workspace: latency kernel
+      HIPCHK(launch_verify_any(d, rt, p, small, sk));
+    }
+    HSTAMP(3);
+    if (defer) gopen.open();  // the inputs, while the launch is in flight; then the gate
+    defer = false;
+    if (sx != st) HIPCHK(hipEventRecord(ev_k[r], sk));
+    // --- the previous chunk's outputs, while this chunk computes
+    if (have_prev) {
+      rc = outputs(prev);
+      if (rc) return rc;
+    }
+    prev = Pending{base, m, r, B, rg};
+    have_prev = true;
+  }
+  if (have_prev) {
+    rc = outputs(prev);
+    if (rc) return rc;
+  }
+  if (!small) HIPCHK(hipEventRecord(d.last, sx));
+  // a gated single launch with nothing queued behind it: its completion word instead of the
+  // stream's completion signal (handoff.cuh gate_done); later work on the stream stays ordered
+  // after it, and nothing of this call reads the pinned buffer any more once the word is set
+  bool done = false;
+  if (gated && nreg == 1 && !(j.kind == HostJob::SENDER_RAW && j.sighash)) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spins = 0; !(done = __atomic_load_n(&gate.w[2], __ATOMIC_ACQUIRE) == gate.seq); ++spins) {
+      cpu_relax();
+      if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+    }
+    if (done) (void)hipStreamQuery(st);  // (lets the runtime retire the launch)
+  }
+  if (!done) {
+    HIPCHK(hipStreamSynchronize(sx));
+    if (sx != st) HIPCHK(hipStreamSynchronize(st));  // (st's last work is already behind sx's events)
+    if (gated && __atomic_load_n(&gate.w[2], __ATOMIC_ACQUIRE) != gate.seq) {
+      (void)hipMemset(gate.dev + 1, 0, 4);  // (the workgroup count, for the next call)
+      return set_err(EGES_E_HIP, "a gated launch ended without its completion word");
+    }
+  }
+  HSTAMP(4);
+  drain.armed = false;
+  if (gating && __atomic_load_n(&gate.w[1], __ATOMIC_ACQUIRE) != 0u) {
+    __atomic_store_n(&gate.w[1], 0u, __ATOMIC_RELAXED);
+    return set_err(EGES_E_HIP, "a kernel's input gate timed out");
+  }
+  if (pinned && have_prev) unpack(prev);
+  HSTAMP(5);
+  if (j.kind == HostJob::VERIFY && __atomic_load_n(vfault, __ATOMIC_ACQUIRE) != 0u)
+    return set_err(EGES_E_HIP, "a kernel hand-off timed out (items read invalid; EGES_DIAG_HANDOFF)");
+  // items a kernel marked EGES_ENGINE_FAULT (a wave hand-off timed out, handoff.cuh) have no
+  // result: the call fails rather than return them
+  if (j.status && !j.decode_only && std::memchr(j.status + off, EGES_ENGINE_FAULT, cnt))
+    return set_err(EGES_E_HIP, "a kernel hand-off timed out (EGES_ENGINE_FAULT items; EGES_DIAG_HANDOFF)");
+  return EGES_SUCCESS;
+#undef H2D
+#undef FLUSH_IN
+#undef JOIN_IN
+}
+
+// Contiguous index shards across the engine's devices.
+int run_host(const HostJob& j, size_t n) {
+  if (n == 0) return EGES_SUCCESS;
+  int rc = ensure_init();
+  if (rc) return rc;
+  std::vector<DevPtr> devs;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    devs = g_devs;
+  }
+  if (devs.empty()) return set_err(EGES_E_NODEVICE, "no gfx950 device available");
+  const Route rt = Route::now();
+  // small batches stay on one device (a Geec block of 1000 txs is one tile set)
+  size_t ndev = std::min(devs.size(), std::max<size_t>(1, n / 65536));
+  const size_t per = (n + ndev - 1) / ndev;
+  if (ndev == 1) return run_host_shard(*devs[0], rt, j, 0, n);
+  std::vector<int> rcs(ndev, EGES_SUCCESS);
+  std::vector<std::string> errs(ndev);
+  std::vector<std::thread> th;
+  for (size_t i = 0; i < ndev; ++i) {
+    const size_t lo = i * per, hi = std::min(n, lo + per);
+    if (lo >= hi) continue;
+    th.emplace_back([&, i, lo, hi] {
+      rcs[i] = run_host_shard(*devs[i], rt, j, lo, hi - lo);
+      if (rcs[i]) errs[i] = t_err;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (size_t i = 0; i < ndev; ++i)
+    if (rcs[i]) return set_err(rcs[i], "device %d: %s", devs[i]->id, errs[i].c_str());
+  return EGES_SUCCESS;
+}
+
+// Decode-only pass over wire-format transactions (the same GPU decoder as eges_sender_raw_batch,
+// no recovery): *bad = some item fails rlp.DecodeBytes.
+int decode_check_raw(const uint8_t* raw, const uint64_t* offsets, size_t n, int signer, uint64_t chain_id, bool* bad) {
+  *bad = false;
+  if (n == 0) return EGES_SUCCESS;
+  std::vector<uint8_t> vf(n);
+  HostJob j;
+  j.kind = HostJob::SENDER_RAW;
+  j.decode_only = true;
+  j.a = raw;
+  j.offsets = offsets;
+  j.signer = signer;
+  j.chain_id = chain_id;
+  j.status = vf.data();
+  const int rc = run_host(j, n);
+  if (rc) return rc;
+  for (uint8_t f : vf)
+    if (f & VF_DECODE_ERR) *bad = true;
+  return EGES_SUCCESS;
+}
+
+// ------------------------------------------------------------------ Geec block (extblock) split
+// RLP item header at b[p] inside [p, end) (rlp/decode.go readKind :937-990 and the Kind bound
+// checks :874-907): kind 0 = byte, 1 = string, 2 = list; hl = header length, sz = payload size.
+bool rlp_head(const uint8_t* b, size_t p, size_t end, int& kind, size_t& hl, size_t& sz) {
+  if (p >= end) return false;  // EOL / EOF
+  const uint8_t x = b[p];
+  if (x < 0x80) {
+    kind = 0;
+    hl = 1;
+    sz = 0;
+    return true;
+  }
+  size_t ll = 0;
+  if (x < 0xB8) {
+    kind = 1;
+    sz = x - 0x80u;
+  } else if (x < 0xC0) {
+    kind = 1;
+    ll = x - 0xB7u;
+  } else if (x < 0xF8) {
+    kind = 2;
+    sz = x - 0xC0u;
+  } else {
+    kind = 2;
+    ll = x - 0xF7u;
+  }
+  hl = 1 + ll;
+  if (ll) {  // readUint: big-endian length, no leading zero byte, and >= 56 (ErrCanonSize)
+    if (p + 1 + ll > end || b[p + 1] == 0) return false;
+    sz = 0;
+    for (size_t k = 0; k < ll; ++k) sz = (sz << 8) | b[p + 1 + k];
+    if (sz < 56) return false;
+  }
+  return sz <= end - p - hl;  // ErrElemTooLarge / ErrValueTooLarge
+}
+
+// The extblock list (core/types/block.go:188-195: Header, FakeTxs, GeecTxs, Txs, Uncles,
+// Confirm rlp:"nil") of a whole block as rlp.DecodeBytes sees its structure: exactly six
+// elements, the first five lists, the last empty or a list, no trailing bytes. Fills, for
+// the three transaction lists, the item offsets (absolute in b; n_k + 1 each). Header, uncle
+// and confirm-message field contents are not decoded (not on the signature path).
+bool split_extblock(const uint8_t* b, size_t len, std::vector<uint64_t> offs[3]) {
+  int kind;
+  size_t hl, sz;
+  if (!rlp_head(b, 0, len, kind, hl, sz) || kind != 2 || hl + sz != len) return false;
+  size_t p = hl;
+  const size_t end = len;
+  for (int e = 0; e < 6; ++e) {
+    if (!rlp_head(b, p, end, kind, hl, sz)) return false;
+    if (e < 5 && kind != 2) return false;                      // Header, tx lists, Uncles: lists
+    if (e == 5 && !(kind == 2 || (kind == 1 && sz == 0))) return false;  // *ConfirmBlockMsg, rlp:"nil"
+    if (e >= 1 && e <= 3) {                                     // FakeTxs, GeecTxs, Txs
+      std::vector<uint64_t>& o = offs[e - 1];
+      o.clear();
+      size_t q = p + hl;
+      const size_t le = p + hl + sz;
+      o.push_back(q);
+      while (q < le) {
+        int k2;
+        size_t h2, s2;
+        if (!rlp_head(b, q, le, k2, h2, s2)) return false;
+        q += h2 + s2;
+        o.push_back(q);
+      }
+    }
+    p += hl + sz;
+  }
+  return p == end;  // "input list has too many elements"
+}
+
+// ------------------------------------------------------------------ host Keccak-256
+const uint64_t RC[24] = {0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808AULL, 0x8000000080008000ULL,
+                         0x000000000000808BULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
+                         0x000000000000008AULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000AULL,
+                         0x000000008000808BULL, 0x800000000000008BULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
+                         0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800AULL, 0x800000008000000AULL,
+                         0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+// rho offsets in the pi-permuted visiting order of the lane walk x,y -> y,2x+3y
+const int ROTC[24] = {1, 3, 6, 10, 15, 21, 28, 36, 45, 55, 2, 14, 27, 41, 56, 8, 25, 43, 62, 18, 39, 61, 20, 44};
+const int PILN[24] = {10, 7, 11, 17, 18, 3, 5, 16, 8, 21, 24, 4, 15, 23, 19, 13, 12, 2, 20, 14, 22, 9, 6, 1};
+
+inline uint64_t rol(uint64_t x, int s) { return (x << s) | (x >> (64 - s)); }
+
+void keccakf_host(uint64_t st[25]) {
+  for (int round = 0; round < 24; ++round) {
+    uint64_t bc[5];
+    for (int i = 0; i < 5; ++i) bc[i] = st[i] ^ st[i + 5] ^ st[i + 10] ^ st[i + 15] ^ st[i + 20];
+    for (int i = 0; i < 5; ++i) {
+      const uint64_t t = bc[(i + 4) % 5] ^ rol(bc[(i + 1) % 5], 1);
+      for (int j = 0; j < 25; j += 5) st[j + i] ^= t;
+    }
+    uint64_t t = st[1];
+    for (int i = 0; i < 24; ++i) {
+      const int j = PILN[i];
+      const uint64_t tmp = st[j];
+      st[j] = rol(t, ROTC[i]);
+      t = tmp;
+    }
+    for (int j = 0; j < 25; j += 5) {
+      for (int i = 0; i < 5; ++i) bc[i] = st[j + i];
+      for (int i = 0; i < 5; ++i) st[j + i] ^= (~bc[(i + 1) % 5]) & bc[(i + 2) % 5];
+    }
+    st[0] ^= RC[round];
+  }
+}
+
+}  // namespace eges::host

@@ -144,7 +144,7 @@ __global__ void __launch_bounds__(64 * TXW_WAVES) tx_rows_wave_kernel(
 hipError_t launch_tx_rows(const uint8_t* raw, const uint64_t* offsets, uint64_t first, uint32_t n, int signer,
                           uint64_t chain_id, uint8_t* sighash, uint8_t* r, uint8_t* s, uint8_t* v, uint8_t* vflags,
                           hipStream_t st) {
-  // KNOB_TXROWS_WAVE_MAX (default 8192, capi.hip) sets the cut (0: never the wave form)
+  // KNOB_TXROWS_WAVE_MAX (default 8192, engine.hip) sets the cut (0: never the wave form)
   const uint32_t wave_max = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TXROWS_WAVE_MAX), 1u << 30));
   if (n <= wave_max)
     hipLaunchKernelGGL(tx_rows_wave_kernel, dim3((n + TXW_WAVES - 1) / TXW_WAVES), dim3(64 * TXW_WAVES), 0, st, raw,

@@ -4,7 +4,7 @@
 // only through eges_test_set_knob (include/eges.h): no call path after init reads the
 // environment (getenv racing a host application's setenv is undefined behaviour in glibc).
 // The values are atomics, so a test may flip one while other threads run; a call snapshots the
-// routing knobs once at its start (capi.hip Route), so a change takes effect from the next call.
+// routing knobs once at its start (engine.h Route), so a change takes effect from the next call.
 #pragma once
 #include <stdint.h>
 
@@ -34,13 +34,20 @@ enum KnobId : int {
                           //   skip publishing it (handoff.cuh), so its consumers time out
   KNOB_TEST_DELAY_X,      // tests: the bucket form's wave X sleeps k x ~3 us before it reads its
                           //   workgroup's wire stage (the stage / part[0] release)
-  KNOB_RESIDENT,          // 1: coalesced single calls go to the resident server (capi.hip Resident)
+  KNOB_RESIDENT,          // 1: coalesced single calls go to the resident server (single.hip Resident)
   KNOB_RESIDENT_WGS,      //   its workgroups (split form, four waves each)
   KNOB_RESIDENT_CAP,      //   the largest group it takes (larger groups launch on a lane)
   KNOB_RESIDENT_IDLE_MS,  //   it exits after this long without a job (restarted on demand)
   KNOB_GATE,              // 1: single-chunk host-buffer calls on the mid-size kernels launch first and copy
-                          //   their inputs while the launch is in flight (capi.hip Gate; the latency
+                          //   their inputs while the launch is in flight (hostpath.hip Gate; the latency
                           //   kernels run ungated)
+  KNOB_HOST_ONE,          // 1: host-buffer ecrecover shards of 2 * PIPE_MIN .. CHUNK signatures run as ONE
+                          //   lane-serial launch fed piece by piece (hostpath.hip run_host_one); 0: chunked
+  KNOB_HOST_FEEDERS,      //   threads that write its pieces into the pinned staging (the caller included)
+  KNOB_TEST_HOST_ONE,     // tests / probes of run_host_one: bit 0 re-reads the pinned outputs after the
+                          //   stream drained and fails the call if a copied block differs; bit 1 puts
+                          //   the outputs in coherent (uncached) pinned memory; bit 2 writes the
+                          //   staging with non-temporal stores
   KNOB_COUNT
 };
 

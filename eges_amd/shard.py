@@ -4,7 +4,7 @@ Every signature is independent, so a batch of n items splits into contiguous ind
 one per rank: rank g gets [g * ceil(n / G), min(n, (g + 1) * ceil(n / G))). No data-path
 collective is needed; each rank returns its own 21-byte (address, status) records and the
 caller concatenates them in rank order. libeges.so applies the same rule to the devices of
-one process (capi.hip, run_host).
+one process (hostpath.hip, run_host).
 """
 
 

@@ -22,7 +22,7 @@ def tiled_golden(n):
 def small_grid():
     """A device whose resident grid is far below the blocks a full pass needs: a multi-pass
     device batch and a multi-pass verify batch must still be bit-exact (the workspace is sized
-    for the larger grid, capi.hip init_device)."""
+    for the larger grid, engine.hip init_device)."""
     import numpy as np
     import torch
     import eges_amd
@@ -44,7 +44,7 @@ def small_grid():
 
 def logical_devices():
     """Two logical devices on one GPU: run_host splits a host-buffer batch into two contiguous
-    shards on two threads (capi.hip run_host); the result must equal the device-resident
+    shards on two threads (hostpath.hip run_host); the result must equal the device-resident
     single-device result byte for byte, and the synthetic signer's addresses."""
     import numpy as np
     import torch
@@ -97,7 +97,57 @@ def allgather_nccl():
     return {"ok": ok, "backend": backend}
 
 
+def host_one_groups():
+    """run_host_one on a small resident grid (EGES_TEST_MAX_BLOCKS=64: 32 resident blocks, a
+    74-block grid of 32 slots per thread, i.e. 3 generations x 32 slots = 96 pieces): every
+    piece's wait, every block's done word, against the golden fixture tiled to 600,011 items."""
+    import numpy as np
+    import eges_amd
+    from eges_amd._lib import lib
+    eges_amd.init(1)
+    n = 600_011
+    msg, sig, pub, st = tiled_golden(n)
+    p, _, s = eges_amd.ecrecover_batch(msg, sig)
+    ok = bool(np.array_equal(s, st) and np.array_equal(p, pub))
+    eges_amd.set_knob("EGES_HOST_ONE", 0)
+    p0, _, s0 = eges_amd.ecrecover_batch(msg, sig)
+    same = bool(np.array_equal(p0, p) and np.array_equal(s0, s))
+    return {"ok": ok, "same_as_chunked": same, "devices": int(lib.eges_device_count())}
+
+
+def other_process_kernels():
+    """A second process on the same GPU (test_gpu_resident.py): a device-resident 1M batch,
+    timed with HIP events each time a line "go" arrives on stdin; prints one number per launch
+    (ms), then "bye" at EOF. The engine of this process never starts a resident server."""
+    import torch
+    import eges_amd
+    eges_amd.init(1)
+    eges_amd.set_knob("EGES_RESIDENT", 0)
+    n = 1 << 20
+    msg, sig, exp = eges_amd.synth_sign_dev(5 << 30, n, 0)
+    addr = torch.empty((n, 20), dtype=torch.uint8, device=msg.device)
+    st = torch.empty((n,), dtype=torch.uint8, device=msg.device)
+    s = torch.cuda.Stream()
+    for _ in range(2):
+        eges_amd.ecrecover_batch_dev(msg, sig, addr=addr, status=st, stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    print("ready", flush=True)
+    ok = True
+    for line in sys.stdin:
+        if line.strip() != "go":
+            continue
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        eges_amd.ecrecover_batch_dev(msg, sig, addr=addr, status=st, stream=s.cuda_stream)
+        e1.record(s)
+        torch.cuda.synchronize()
+        ok = ok and bool(torch.equal(addr, exp))
+        print(f"{e0.elapsed_time(e1):.4f}", flush=True)
+    return {"ok": ok}
+
+
 if __name__ == "__main__":
     mode = sys.argv[1]
-    out = {"small_grid": small_grid, "logical_devices": logical_devices, "allgather_nccl": allgather_nccl}[mode]()
+    out = {"small_grid": small_grid, "logical_devices": logical_devices, "allgather_nccl": allgather_nccl,
+           "host_one_groups": host_one_groups, "other_process_kernels": other_process_kernels}[mode]()
     print(json.dumps(out), flush=True)

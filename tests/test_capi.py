@@ -87,7 +87,7 @@ def test_knobs_set_and_read_without_gpu():
     # input gate on); round 5 removed the measured-slower pinned pipeline, second host stream and
     # resident block server, so their names are unknown now
     defaults = {"EGES_RESIDENT": 1, "EGES_GATE": 1, "EGES_HOST_PARTS": 8, "EGES_LAT_TRI_MAX": 448,
-                "EGES_SENDER_FUSED": 1}
+                "EGES_SENDER_FUSED": 1, "EGES_HOST_ONE": 0, "EGES_HOST_FEEDERS": 4}
     for name, want in defaults.items():
         assert eges_amd.get_knob(name) == want, name
     for name in ("EGES_RESIDENT_WGS", "EGES_RESIDENT_CAP", "EGES_RESIDENT_IDLE_MS", "EGES_TEST_DELAY_X",
@@ -111,10 +111,11 @@ def test_no_getenv_on_call_paths():
             continue
         src = open(f).read()
         n = len(re.findall(r"getenv\(", src))
-        if os.path.basename(f) == "capi.hip":
+        if os.path.basename(f) == "engine.hip":
             # env_int (init_device / eges_init) and knobs_load_env
             assert n == 2, n
-            for m in re.finditer(r"env_int\(\"(EGES_[A-Z_]+)\"", src):
-                assert m.group(1) in ("EGES_GRID_MULT", "EGES_TEST_MAX_BLOCKS", "EGES_TEST_LOGICAL_DEVICES"), m.group(1)
         else:
             assert n == 0, f
+        for m in re.finditer(r"env_int\(\"(EGES_[A-Z_]+)\"", src):
+            assert os.path.basename(f) in ("engine.hip", "capi.hip"), f
+            assert m.group(1) in ("EGES_GRID_MULT", "EGES_TEST_MAX_BLOCKS", "EGES_TEST_LOGICAL_DEVICES"), m.group(1)

@@ -1,7 +1,7 @@
 """configs[3] (C4) on the GPU: the full 64M-signature batch through the device entry, every
 address checked against the synthetic signer, an oracle sample across every pass boundary and a
 1M random-index sample against the reference libsecp256k1 (oracle/_ref);
-and the in-library multi-device split (capi.hip run_host with ndev > 1) and a small-grid device
+and the in-library multi-device split (hostpath.hip run_host with ndev > 1) and a small-grid device
 run in child processes with the engine's test-only knobs (tests/gpu_child.py)."""
 import json
 import os
@@ -82,3 +82,10 @@ def test_records_all_gather_over_rccl():
     through the "nccl" (RCCL) backend, world size 1, in a child process."""
     out = _child("allgather_nccl", {"EGES_TEST_PORT": str(29000 + os.getpid() % 1000)})
     assert out["ok"] and out["backend"] == "nccl", out
+
+
+def test_host_one_launch_many_groups():
+    """The one-launch host-buffer form with several generations and 32 slots per thread
+    (EGES_TEST_MAX_BLOCKS=64), equal to the fixture and to the chunked path."""
+    out = _child("host_one_groups", {"EGES_TEST_MAX_BLOCKS": "64"})
+    assert out["ok"] and out["same_as_chunked"], out

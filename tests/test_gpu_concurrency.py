@@ -61,7 +61,7 @@ def test_concurrent_batch_and_single_item_callers(engine):
 
 def test_coalesced_single_item_callers(engine):
     """8 threads x 2000 single eges_ecdsa_recover calls (the reference's per-goroutine
-    secp256k1_ext_ecdsa_recover, ext.h:30-47): coalesced into shared batches (capi.hip
+    secp256k1_ext_ecdsa_recover, ext.h:30-47): coalesced into shared batches (single.hip
     Coalescer), every result bit-exact against the golden fixture. Rates printed for the record."""
     import time
     from eges_amd._lib import lib
@@ -112,7 +112,7 @@ def test_coalesced_single_item_callers(engine):
 def test_coalesced_recover_and_verify_many_callers(engine):
     """24 threads at once, 12 through eges_ecdsa_recover and 12 through eges_ecdsa_verify (the
     reference's ext.h:30-47 / :58-75 per-call seams): both coalescers share the device's lanes,
-    more callers than the coalescer lets spin (capi.hip EGES_COALESCE_SPINNERS), so the blocking
+    more callers than the coalescer lets spin (single.hip EGES_COALESCE_SPINNERS), so the blocking
     path runs too. Every result against the golden fixtures (recover.npz, verify.npz)."""
     from eges_amd._lib import lib
     gr = load_golden("recover.npz")

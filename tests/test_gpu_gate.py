@@ -1,5 +1,5 @@
 """Host-buffer calls that launch before their inputs are copied (EGES_GATE = 1, the default:
-capi.hip run_host_shard GateOpen, handoff.cuh gate_wait / gate_done): the fused mid-size kernels
+hostpath.hip run_host_shard GateOpen, handoff.cuh gate_wait / gate_done): the fused mid-size kernels
 (bucket, windowed) wait at the call's gate word while the host copies the inputs into the pinned
 buffer, and their last workgroup stores the completion word the host waits on. The latency forms
 run ungated either way (measured slower gated). Every golden recovery and sender item through

@@ -66,7 +66,7 @@ def test_synth_roundtrip(engine, oracle):
 
 def test_multi_chunk_overlapped_launches(engine, oracle):
     """A device batch larger than one pass (2^21 signatures) runs as launches alternating between
-    two streams with separate workspaces (capi.hip run_recover_dev_overlap). On a caller stream
+    two streams with separate workspaces (route.hip run_recover_dev_overlap). On a caller stream
     that still has queued work, with the pub output: every byte of a ragged 2^21 + 4099 batch
     must equal the same items recovered as single-pass (non-overlapped) calls, and a following
     host-buffer and verify call on the device must still be right (the d.last join)."""

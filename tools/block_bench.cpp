@@ -2,7 +2,7 @@
 // through eges_sender_batch (host buffers, the call the Go block processor makes through cgo;
 // INTEGRATION.md §4), timed around the C call itself (no Python wrapper). Every sender is
 // checked against the synthetic signer's address. Linked against libeges_diag.so (EGES_PHASE_STAMPS)
-// it also prints the host phase split of the call (capi.hip HSTAMP). Prints one JSON line.
+// it also prints the host phase split of the call (hostpath.hip HSTAMP). Prints one JSON line.
 //   build: hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/block_bench.cpp -Iinclude
 //          -Leges_amd -leges -Wl,-rpath,'$ORIGIN/../eges_amd' -ldl -o tools/block_bench
 //   run:   tools/block_bench [txs=1000] [iters=300]

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """C1 (10k wire-format transfers through eges_sender_raw_batch) timed around the C-ABI call, with
-the engine's host phase split (capi.hip HSTAMP: acquire, pack, launch, sync, unpack) from the
+the engine's host phase split (hostpath.hip HSTAMP: acquire, pack, launch, sync, unpack) from the
 stamped diagnostic build. Run with EGES_AB_LIB=eges_amd/libeges_diag.so (the stamped kernels are
 slower; the host phases are what this reads). Prints one JSON line.
 usage: EGES_AB_LIB=$PWD/eges_amd/libeges_diag.so python tools/c1_host_phases.py [n=10000] [iters=100]"""

@@ -1,5 +1,5 @@
 // Host <-> device copies while the lane-serial recover kernel holds the whole GPU (the host-buffer
-// pipeline's situation, capi.hip run_host_shard / run_host_pipe): hipMemcpyAsync (ROCclr picks a
+// pipeline's situation, hostpath.hip run_host_shard / run_host_pipe): hipMemcpyAsync (ROCclr picks a
 // blit kernel, which then waits for free CU slots) against hsa_amd_memory_async_copy (the SDMA
 // engines). Prints one JSON line.
 //   build: hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/copy_overlap_probe.cpp -Iinclude
