@@ -182,7 +182,7 @@ struct Route {
     r.gate = knob(KNOB_GATE);
     r.host_one = knob(KNOB_HOST_ONE);
     r.feeders = std::max<long long>(1, std::min<long long>(knob(KNOB_HOST_FEEDERS), 16));
-    r.test_host_one = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TEST_HOST_ONE), 7));
+    r.test_host_one = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TEST_HOST_ONE), 15));
     r.tri_max = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_LAT_TRI_MAX), 1u << 30));
     r.host_parts = (size_t)std::max<long long>(2, std::min<long long>(knob(KNOB_HOST_PARTS), 64));
     r.force_redo = knob(KNOB_FORCE_REDO) != 0 ? 1u : 0u;

@@ -298,10 +298,15 @@ int run_host_one(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t c
         pieces[gi * kmax + k] = {{im + lo * 32, j.a + (off + lo) * 32, (hi - lo) * 32},
                                  {is + lo * 65, j.b + (off + lo) * 65, (hi - lo) * 65}};
     }
+  auto feed = [&] {
+    Feeder::get().run(pieces, (int)rt.feeders - 1, (rt.test_host_one & 4u) != 0,
+                      [&](size_t pc) { publish_u32(host_word, seq + (uint32_t)pc + 1); });
+  };
+  const bool prefeed = (rt.test_host_one & 8u) != 0;  // probe: every piece in place before the launch
+  if (prefeed) feed();
   HIPCHK(launch_recover_host(with_diag(d, p, rt), grid, d.ws_blocks, st));
   HIPCHK(hipEventRecord(d.last, st));
-  Feeder::get().run(pieces, (int)rt.feeders - 1, (rt.test_host_one & 4u) != 0,
-                    [&](size_t pc) { publish_u32(host_word, seq + (uint32_t)pc + 1); });
+  if (!prefeed) feed();
   // outputs: block by block as their done words appear
   bool missing = false;
   for (int b = 0; b < grid && !missing; ++b) {

@@ -47,7 +47,7 @@ enum KnobId : int {
   KNOB_TEST_HOST_ONE,     // tests / probes of run_host_one: bit 0 re-reads the pinned outputs after the
                           //   stream drained and fails the call if a copied block differs; bit 1 puts
                           //   the outputs in coherent (uncached) pinned memory; bit 2 writes the
-                          //   staging with non-temporal stores
+                          //   staging with non-temporal stores; bit 3 writes every piece before the launch
   KNOB_COUNT
 };
 
