@@ -123,25 +123,12 @@ struct Dev {
   uint32_t* ws = nullptr;
   uint32_t* diag = nullptr;  // DIAG_WORDS counters (eges_diag_counters)
   int mb_recover = 0, mb_verify = 0, mb_synth = 0;
-  int res_blocks = 0;  // lane-serial recover blocks resident at once (one generation)
   int ws_blocks = 0;  // blocks ws (and ws2) hold: every launch's grid is checked against it
   uint8_t* buf = nullptr;  // per-call device scratch, grown on demand
   size_t buf_cap = 0;
   uint8_t* pin = nullptr;  // pinned host staging of single-chunk host-buffer calls (PIN_BYTES)
   Gate gate;               //   and their input gate
   uint32_t* vfault = nullptr;  // coherent pinned: a VerifySignature call's hand-off fault word
-  // one-launch host-buffer form (run_host_one): the copy engine's arrival word (device memory);
-  // coherent pinned control words (the pieces' sequence values, the fault word, one done word per
-  // block); the pinned buffer the kernel writes its outputs into
-  uint32_t* ls_arr = nullptr;
-  uint32_t* ls_ctl = nullptr;
-  size_t ls_ctl_words = 0;
-  uint8_t* ls_in = nullptr;
-  size_t ls_in_cap = 0;
-  uint8_t* ls_out = nullptr;
-  size_t ls_out_cap = 0;
-  bool ls_out_coherent = false;
-  uint32_t ls_seq = 0;
   // overlapped recover launches (EGES_OVERLAP): a second stream, workspace and its events
   hipStream_t aux = nullptr;
   uint32_t* ws2 = nullptr;
@@ -167,9 +154,9 @@ extern std::atomic<long long> g_knob[KNOB_COUNT];
 struct Route {
   size_t lat_max = 0, mid_max = 0;
   uint32_t wide_max = 0, tri_max = 0;
-  long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, gate = 1, host_one = 1, feeders = 4;
+  long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, gate = 1;
   size_t host_parts = EGES_PIPE_PARTS;
-  uint32_t force_redo = 0, skip_flag = 0, delay_x = 0, test_host_one = 0;
+  uint32_t force_redo = 0, skip_flag = 0, delay_x = 0;
   static Route now() {
     Route r;
     r.lat_max = (size_t)std::max<long long>(0, knob(KNOB_LAT_MAX));
@@ -180,9 +167,6 @@ struct Route {
     r.overlap = knob(KNOB_OVERLAP);
     r.sender_fused = knob(KNOB_SENDER_FUSED);
     r.gate = knob(KNOB_GATE);
-    r.host_one = knob(KNOB_HOST_ONE);
-    r.feeders = std::max<long long>(1, std::min<long long>(knob(KNOB_HOST_FEEDERS), 16));
-    r.test_host_one = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TEST_HOST_ONE), 15));
     r.tri_max = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_LAT_TRI_MAX), 1u << 30));
     r.host_parts = (size_t)std::max<long long>(2, std::min<long long>(knob(KNOB_HOST_PARTS), 64));
     r.force_redo = knob(KNOB_FORCE_REDO) != 0 ? 1u : 0u;

@@ -65,9 +65,6 @@ static const KnobDef KNOB_DEFS[] = {
     {"EGES_RESIDENT_CAP", 64},
     {"EGES_RESIDENT_IDLE_MS", 4},
     {"EGES_GATE", 1},
-    {"EGES_HOST_ONE", 0},
-    {"EGES_HOST_FEEDERS", 4},
-    {"EGES_TEST_HOST_ONE", 0},
 };
 static_assert(sizeof(KNOB_DEFS) / sizeof(KNOB_DEFS[0]) == KNOB_COUNT, "a name and default for every knob");
 std::atomic<long long> g_knob[KNOB_COUNT];
@@ -142,9 +139,7 @@ int init_device(int id, DevPtr* out) {
   d->mb_recover = occupancy_recover() * d->cus * gm;
   d->mb_verify = occupancy_verify() * d->cus * gm;
   d->mb_synth = occupancy_synth() * d->cus;
-  d->res_blocks = occupancy_recover() * d->cus;
   if (const int cap = env_int("EGES_TEST_MAX_BLOCKS", 0); cap > 0) {  // tests: a small device
-    d->res_blocks = std::min(d->res_blocks, std::max(1, cap / gm));
     d->mb_recover = std::min(d->mb_recover, cap);
     d->mb_verify = std::min(d->mb_verify, cap);
     d->mb_synth = std::min(d->mb_synth, cap);
@@ -152,9 +147,8 @@ int init_device(int id, DevPtr* out) {
   // A full pass may need more blocks than are resident (grid_for_lane_serial caps the
   // signatures per thread at MAX_SLOTS): the workspace covers the larger of the two.
   const int mb = std::max(d->mb_recover, std::max(d->mb_verify, d->mb_synth));
-  // (+ 1: the host-buffer form's mirror block ahead of a full pass, launch_recover_host)
   d->ws_blocks = std::max(mb, std::max(lane_serial_grid((uint32_t)CHUNK, d->mb_recover),
-                                       lane_serial_grid((uint32_t)CHUNK, d->mb_verify))) + 1;
+                                       lane_serial_grid((uint32_t)CHUNK, d->mb_verify)));
   HIPCHK(hipMalloc(&d->gtab, gtab_bytes()));
   HIPCHK(hipMalloc(&d->ws, ws_bytes_per_block() * (size_t)d->ws_blocks));
   HIPCHK(hipMalloc(&d->diag, DIAG_WORDS * sizeof(uint32_t)));
@@ -184,10 +178,6 @@ Dev::~Dev() {
   if (gate.w) (void)hipHostFree(gate.w);
   if (vfault) (void)hipHostFree(vfault);
   if (gate.dev) (void)hipFree(gate.dev);
-  if (ls_arr) (void)hipFree(ls_arr);
-  if (ls_ctl) (void)hipHostFree(ls_ctl);
-  if (ls_out) (void)hipHostFree(ls_out);
-  if (ls_in) (void)hipHostFree(ls_in);
   if (last) (void)hipEventDestroy(last);
   for (int r = 0; r < 2; ++r) {
     if (ev_in[r]) (void)hipEventDestroy(ev_in[r]);

@@ -1,10 +1,6 @@
-// Host-buffer paths (engine.h): the one-launch form of large ecrecover shards, the chunked
-// pipeline of everything else, the multi-device split, the Geec block split and the host Keccak.
+// Host-buffer paths (engine.h): the chunked pipeline, the multi-device split, the Geec block split
+// and the host Keccak.
 #include "engine.h"
-
-#if defined(__x86_64__)
-#include <immintrin.h>
-#endif
 
 namespace eges::host {
 
@@ -53,304 +49,11 @@ Region region_for(const HostJob& j, size_t base, size_t m) {
 // of them, so the call never waits for a worker to wake), and the caller publishes piece p (the
 // word the kernel mirrors) as soon as all of its chunks and those of the pieces before it are in
 // place. Each thread fences its own (non-temporal) stores before it counts a chunk done.
-// Copy with non-temporal stores (the bytes go to memory, not into this core's cache), the
-// unaligned head and tail with ordinary stores whose lines are then flushed (EGES_TEST_HOST_ONE
-// bit 2). The caller fences.
-void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
-#if defined(__x86_64__)
-  size_t head = (16 - ((uintptr_t)dst & 15)) & 15;
-  if (head > n) head = n;
-  std::memcpy(dst, src, head);
-  size_t i = head;
-  for (; i + 16 <= n; i += 16)
-    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i)));
-  std::memcpy(dst + i, src + i, n - i);
-  if (head) _mm_clflush(dst);
-  if (i < n) _mm_clflush(dst + i);
-#else
-  std::memcpy(dst, src, n);
-#endif
-}
-
-class Feeder {
- public:
-  struct Span {
-    uint8_t* dst;
-    const uint8_t* src;
-    size_t n;
-  };
-  static Feeder& get() {
-    static Feeder* f = new Feeder(15);  // never destroyed: detached workers live to process exit
-    return *f;
-  }
-  // pieces[p]: the spans of piece p; publish(p) is called in order by this thread; threads: the
-  // workers joined (0 .. 15) besides the caller
-  template <class F>
-  void run(const std::vector<std::vector<Span>>& pieces, int threads, bool nt, F&& publish) {
-    std::vector<Chunk> chunks;
-    std::vector<uint32_t> per(pieces.size(), 0);
-    for (size_t p = 0; p < pieces.size(); ++p)
-      for (const Span& sp : pieces[p])
-        for (size_t o = 0; o < sp.n; o += CHUNK_BYTES) {
-          chunks.push_back({sp.dst + o, sp.src + o, std::min(CHUNK_BYTES, sp.n - o), (uint32_t)p});
-          ++per[p];
-        }
-    std::unique_ptr<std::atomic<uint32_t>[]> done(new std::atomic<uint32_t>[pieces.size()]);
-    for (size_t p = 0; p < pieces.size(); ++p) done[p].store(0, std::memory_order_relaxed);
-    std::atomic<size_t> next{0};
-    auto take_one = [&]() -> bool {
-      const size_t k = next.fetch_add(1, std::memory_order_relaxed);
-      if (k >= chunks.size()) return false;
-      if (nt) stream_copy(chunks[k].dst, chunks[k].src, chunks[k].n);
-      else std::memcpy(chunks[k].dst, chunks[k].src, chunks[k].n);
-#if defined(__x86_64__)
-      __builtin_ia32_sfence();
-#endif
-      done[chunks[k].piece].fetch_add(1, std::memory_order_release);
-      return true;
-    };
-    std::lock_guard<std::mutex> one(run_mu_);  // one feed at a time (several devices' threads may call)
-    const int want = std::max(0, std::min(threads, (int)nworkers_));
-    if (want > 0 && chunks.size() > 1) {
-      std::lock_guard<std::mutex> lk(mu_);
-      job_ = [&] { while (take_one()) {} };
-      quota_ = want;
-      ++gen_;
-    }
-    if (want > 0 && chunks.size() > 1) cv_.notify_all();
-    size_t pub = 0;
-    auto flush = [&] {  // publish every complete piece, in order
-      while (pub < pieces.size() && done[pub].load(std::memory_order_acquire) == per[pub]) publish(pub++);
-    };
-    while (take_one()) flush();
-    while (pub < pieces.size()) {
-      flush();
-      cpu_relax();
-    }
-    {
-      std::lock_guard<std::mutex> lk(mu_);  // workers that wake late find no job ...
-      job_ = nullptr;
-    }
-    // ... and none still inside this one touches its (stack) state after we return
-    while (active_.load(std::memory_order_acquire) != 0) cpu_relax();
-  }
-
- private:
-  static constexpr size_t CHUNK_BYTES = size_t(1) << 20;
-  struct Chunk {
-    uint8_t* dst;
-    const uint8_t* src;
-    size_t n;
-    uint32_t piece;
-  };
-  explicit Feeder(int n) : nworkers_(n) {
-    for (int i = 0; i < n; ++i) std::thread([this] { loop(); }).detach();
-  }
-  void loop() {
-    uint64_t seen = 0;
-    for (;;) {
-      std::function<void()> job;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
-        if (quota_ <= 0 || !job_) continue;  // (enough workers joined this feed)
-        --quota_;
-        job = job_;
-        active_.fetch_add(1, std::memory_order_relaxed);
-      }
-      job();
-      active_.fetch_sub(1, std::memory_order_release);
-    }
-  }
-  const int nworkers_;
-  std::mutex mu_, run_mu_;
-  std::condition_variable cv_;
-  std::function<void()> job_;
-  int quota_ = 0;
-  uint64_t gen_ = 0;
-  std::atomic<int> active_{0};
-};
-
-// One lane-serial launch over a whole host-buffer ecrecover shard (2 * PIPE_MIN .. CHUNK
-// signatures; the Go caller's large crypto.Ecrecover batches). The chunked pipeline below runs
-// such a shard as several launches of one signature per thread, each ending in a partial
-// generation; this form launches once, with the grid and slots of the device-resident call, and
-// lets the kernel start while this thread is still writing its inputs:
-//  - the inputs go into pinned staging as pieces in the order the waves read them (the first
-//    resident generation's threads slot 0, slot 1, ..., then the next generation's); after each
-//    piece this thread stores the piece count into a coherent word, which block 0 of the launch
-//    mirrors into device memory; a wave waits for its piece before it parses a slot straight
-//    from the staging (k_recover.hip ls_mirror / ls_wait / ls_parse: no copy engine, no prep
-//    launch: a copy engine's small transfers or a blit kernel would wait for CUs the launch holds);
-//  - the kernel writes its outputs into pinned memory, and each block marks its done word after
-//    its stores, so this thread copies a block's outputs to the caller while the others run.
-// The call returns when every block is done and the stream has drained.
-constexpr uint32_t LS_PIECES = 256;  // pieces per call at most (sequence stride)
-constexpr size_t LS_CTL_DONE = 64;   // control words: 0 the host's piece count, 1 the fault word, done from 64
-bool host_one_fits(const Dev& d, const Route& rt, const HostJob& j, size_t cnt) {
-  if (rt.host_one == 0 || j.kind != HostJob::RECOVER || cnt < 2 * PIPE_MIN || cnt > CHUNK) return false;
-  const int grid = lane_serial_grid((uint32_t)cnt, d.mb_recover);
-  const size_t gt = (size_t)grid * threads_per_block(), group = (size_t)d.res_blocks * threads_per_block();
-  if (d.res_blocks <= 0 || grid + 1 > d.ws_blocks) return false;
-  return ((gt + group - 1) / group) * ((cnt + gt - 1) / gt) < LS_PIECES;
-}
-
-template <class T>
-int ensure_pinned(T*& p, size_t& cap, size_t bytes, unsigned flags, hipEvent_t last) {
-  if (bytes <= cap) return EGES_SUCCESS;
-  if (p) {
-    HIPCHK(hipEventSynchronize(last));
-    (void)hipHostFree(p);
-    p = nullptr;
-    cap = 0;
-  }
-  if (hipHostMalloc(reinterpret_cast<void**>(&p), bytes, flags) != hipSuccess) {
-    p = nullptr;
-    return set_err(EGES_E_NOMEM, "hipHostMalloc(%zu) failed", bytes);
-  }
-  cap = bytes;
-  return EGES_SUCCESS;
-}
-
-int run_host_one(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t cnt) {
-  DevGuard g(d.id);
-  DeviceWide wide(d);
-  const uint32_t n = (uint32_t)cnt;
-  const size_t n_pad = align_up(cnt, 64);
-  const uint32_t wg = (uint32_t)threads_per_block();
-  const int grid = lane_serial_grid(n, d.mb_recover);
-  const uint32_t GT = (uint32_t)grid * wg, group = (uint32_t)d.res_blocks * wg;
-  const uint32_t kmax = (n + GT - 1) / GT, ngroups = (GT + group - 1) / group;
-  int rc = dev_ensure_buf(d, recover_scratch_bytes(n_pad));  // records and slots
-  if (rc) return rc;
-  // pinned: inputs msg | sig, outputs status | addr | pub, control words
-  const size_t o_sig = align_up(cnt * 32, 256);
-  const size_t o_addr = align_up(cnt, 256), o_pub = o_addr + align_up(cnt * 20, 256);
-  if ((rc = ensure_pinned(d.ls_in, d.ls_in_cap, o_sig + cnt * 65, hipHostMallocDefault, d.last))) return rc;
-  const bool coherent_out = (rt.test_host_one & 2u) != 0;
-  if (d.ls_out && d.ls_out_coherent != coherent_out) {  // (a probe switched the memory type)
-    HIPCHK(hipEventSynchronize(d.last));
-    (void)hipHostFree(d.ls_out);
-    d.ls_out = nullptr;
-    d.ls_out_cap = 0;
-  }
-  if ((rc = ensure_pinned(d.ls_out, d.ls_out_cap, o_pub + (j.pub ? cnt * 65 : 0),
-                          coherent_out ? hipHostMallocCoherent : hipHostMallocDefault, d.last)))
-    return rc;
-  d.ls_out_coherent = coherent_out;
-  size_t ctl_bytes = d.ls_ctl_words * 4;
-  if ((rc = ensure_pinned(d.ls_ctl, ctl_bytes, (LS_CTL_DONE + (size_t)d.ws_blocks) * 4, hipHostMallocCoherent, d.last)))
-    return rc;
-  d.ls_ctl_words = ctl_bytes / 4;
-  if (!d.ls_arr) {
-    if (hipMalloc(&d.ls_arr, 256) != hipSuccess) {
-      d.ls_arr = nullptr;
-      return set_err(EGES_E_NOMEM, "hipMalloc(arrival word) failed");
-    }
-    HIPCHK(hipMemset(d.ls_arr, 0, 256));
-  }
-  // the previous call's kernel is done with the staging, outputs and control words
-  HIPCHK(hipEventSynchronize(d.last));
-  uint32_t* host_word = d.ls_ctl;
-  uint32_t* fault = d.ls_ctl + 1;
-  uint32_t* done = d.ls_ctl + LS_CTL_DONE;
-  d.ls_seq += LS_PIECES;
-  const uint32_t seq = d.ls_seq;
-  const uint32_t npieces = ngroups * kmax;
-  std::memset(done, 0, (size_t)grid * 4);
-  __atomic_store_n(fault, 0u, __ATOMIC_RELAXED);
-  __atomic_store_n(host_word, seq, __ATOMIC_RELEASE);  // no piece yet
-  uint8_t* const im = d.ls_in;
-  uint8_t* const is = d.ls_in + o_sig;
-  uint8_t* const o_st = d.ls_out;
-  RecoverParams p{reinterpret_cast<uint32_t*>(d.buf), n, (uint32_t)n_pad, o_st, j.addr ? d.ls_out + o_addr : nullptr,
-                  j.pub ? d.ls_out + o_pub : nullptr, d.gtab, d.ws};
-  p.ls_msg = im;
-  p.ls_sig = is;
-  p.ls_arrived = d.ls_arr;
-  p.ls_host = host_word;
-  p.ls_seq = seq;
-  p.ls_final = seq + npieces;
-  p.ls_group = group;
-  p.ls_kmax = kmax;
-  p.ls_done = done;
-  p.ls_fault = fault;
-  hipStream_t st = d.stream;
-  struct Drain {  // every return waits for the launch first (it reads the staging this call owns)
-    hipStream_t a;
-    uint32_t* word;
-    uint32_t final;
-    bool armed;
-    ~Drain() {
-      if (!armed) return;
-      __atomic_store_n(word, final, __ATOMIC_RELEASE);  // (no wave waits for a piece that will not come)
-      (void)hipStreamSynchronize(a);
-    }
-  } drain{st, host_word, seq + npieces, true};
-  // the pieces in the order the waves read them: generation gi's threads, slot k
-  std::vector<std::vector<Feeder::Span>> pieces(npieces);
-  for (uint32_t gi = 0; gi < ngroups; ++gi)
-    for (uint32_t k = 0; k < kmax; ++k) {
-      const size_t lo = (size_t)k * GT + (size_t)gi * group;
-      const size_t hi = std::min<size_t>({lo + group, (size_t)(k + 1) * GT, cnt});
-      if (lo < hi)
-        pieces[gi * kmax + k] = {{im + lo * 32, j.a + (off + lo) * 32, (hi - lo) * 32},
-                                 {is + lo * 65, j.b + (off + lo) * 65, (hi - lo) * 65}};
-    }
-  auto feed = [&] {
-    Feeder::get().run(pieces, (int)rt.feeders - 1, (rt.test_host_one & 4u) != 0,
-                      [&](size_t pc) { publish_u32(host_word, seq + (uint32_t)pc + 1); });
-  };
-  const bool prefeed = (rt.test_host_one & 8u) != 0;  // probe: every piece in place before the launch
-  if (prefeed) feed();
-  HIPCHK(launch_recover_host(with_diag(d, p, rt), grid, d.ws_blocks, st));
-  HIPCHK(hipEventRecord(d.last, st));
-  if (!prefeed) feed();
-  // outputs: block by block as their done words appear
-  bool missing = false;
-  for (int b = 0; b < grid && !missing; ++b) {
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint64_t spins = 0; __atomic_load_n(done + b, __ATOMIC_ACQUIRE) != seq; ++spins) {
-      cpu_relax();
-      if ((spins & 1023) == 1023 && (hipStreamQuery(st) == hipSuccess ||
-                                     std::chrono::steady_clock::now() - t0 > std::chrono::seconds(8))) {
-        missing = __atomic_load_n(done + b, __ATOMIC_ACQUIRE) != seq;
-        break;
-      }
-    }
-    for (uint32_t k = 0; k < kmax && !missing; ++k) {
-      const size_t lo = (size_t)k * GT + (size_t)b * wg;
-      if (lo >= cnt) break;
-      const size_t m = std::min<size_t>(wg, cnt - lo);
-      if (j.status) std::memcpy(j.status + off + lo, o_st + lo, m);
-      if (j.addr) std::memcpy(j.addr + (off + lo) * 20, d.ls_out + o_addr + lo * 20, m * 20);
-      if (j.pub) std::memcpy(j.pub + (off + lo) * 65, d.ls_out + o_pub + lo * 65, m * 65);
-    }
-  }
-  drain.armed = false;
-  HIPCHK(hipStreamSynchronize(st));
-  if (__atomic_load_n(fault, __ATOMIC_ACQUIRE) != 0u) return set_err(EGES_E_HIP, "an input piece was not seen in time");
-  if (missing) return set_err(EGES_E_HIP, "a block of the one-launch host form never marked its outputs done");
-  if (rt.test_host_one & 1u) {  // probe: did any block's outputs change after this thread copied them?
-    size_t changed = 0, first = SIZE_MAX;
-    for (size_t i = 0; i < cnt; ++i) {
-      const bool same = (!j.status || j.status[off + i] == o_st[i]) &&
-                        (!j.addr || std::memcmp(j.addr + (off + i) * 20, d.ls_out + o_addr + i * 20, 20) == 0) &&
-                        (!j.pub || std::memcmp(j.pub + (off + i) * 65, d.ls_out + o_pub + i * 65, 65) == 0);
-      if (!same && changed++ == 0) first = i;
-    }
-    if (changed) return set_err(EGES_E_HIP, "recheck: %zu items changed after their block was copied (first %zu)", changed, first);
-  }
-  return EGES_SUCCESS;
-}
-
 // Host-buffer pipeline over chunks of one shard. Two device regions alternate: while the
 // compute stream runs chunk i, the copy stream stages chunk i+1's inputs and returns chunk
 // i-1's outputs (host order H2D(i+1), K(i+1), D2H(i): the pageable D2H blocks this thread
 // until K(i) is done, by which time K(i+1) is queued behind it). Synchronous overall.
 int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t cnt) {
-  if (host_one_fits(d, rt, j, cnt)) return run_host_one(d, rt, j, off, cnt);
   HSTAMP(0);
   DevGuard g(d.id);
   // a shard big enough to pipeline runs as >= 2 chunks (each still a full resident grid)

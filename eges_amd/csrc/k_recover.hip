@@ -9,72 +9,6 @@
 
 namespace eges {
 
-// ------------------------------------------------------------------ host-buffer form
-// Block 0 of a host-buffer launch (RecoverParams::ls_host): one wave copies the host's piece count
-// into the device word the signature waves poll, until the last piece (or 4 s). A single poller
-// of the bus word: every wave polling it over PCIe would flood the link.
-DEV void ls_mirror(const RecoverParams& prm) {
-  if (threadIdx.x >= 64) return;
-  uint32_t* h = const_cast<uint32_t*>(prm.ls_host);
-  constexpr uint64_t BOUND = 400000000ull;  // s_memrealtime ticks (100 MHz): 4 s
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  uint32_t last = prm.ls_seq;
-#pragma unroll 1
-  for (;;) {
-    const uint32_t v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-    if (v != last) {
-      if (threadIdx.x == 0) __hip_atomic_store(prm.ls_arrived, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = v;
-    }
-    if ((int32_t)(v - prm.ls_final) >= 0) return;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > BOUND) {
-      if (threadIdx.x == 0) {
-        __hip_atomic_store(prm.ls_fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(prm.ls_arrived, prm.ls_final, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // release the waves
-      }
-      return;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
-// Wait until piece `piece` has been written (RecoverParams::ls_arrived, mirrored by block 0). The
-// piece is wave-uniform; the inputs are read only after it (no line of them was read before in
-// this launch, whose start invalidated the caches).
-DEV void ls_wait(const RecoverParams& prm, uint32_t piece) {
-  const uint32_t want = prm.ls_seq + piece + 1u;
-  constexpr uint64_t BOUND = 500000000ull;  // s_memrealtime ticks (100 MHz): 5 s (the mirror gives up at 4)
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-#pragma unroll 1
-  while ((int32_t)(__builtin_amdgcn_readfirstlane(
-                       __hip_atomic_load(prm.ls_arrived, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - want) < 0) {
-    if (__builtin_amdgcn_s_memrealtime() - t0 > BOUND) {
-      if ((threadIdx.x & 63) == 0) __hip_atomic_store(prm.ls_fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(8);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-// prep_ecrecover_kernel's parse (k_prep.hip) of item idx from the bytes, into its record rows
-DEV void ls_parse(const RecoverParams& prm, uint32_t idx, uint32_t rl[8], uint32_t sl[8], uint32_t& meta) {
-  const uint32_t np = prm.n_pad;
-  uint32_t* rec = const_cast<uint32_t*>(prm.rec);
-  const uint8_t* sg = prm.ls_sig + (size_t)idx * 65;
-  uint32_t zl[8];
-  limbs_from_be32(zl, prm.ls_msg + (size_t)idx * 32);
-  limbs_from_be32(rl, sg);
-  limbs_from_be32(sl, sg + 32);
-  const uint32_t v = sg[64];
-  meta = v >= 4 ? (ST_INVALID_RECOVERY_ID << 8) : v;  // checkSignature (secp256.go:171-179)
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    rec[(size_t)k * np + idx] = zl[k];
-    rec[(size_t)(8 + k) * np + idx] = rl[k];
-    rec[(size_t)(16 + k) * np + idx] = sl[k];
-  }
-  rec[(size_t)24 * np + idx] = meta;
-}
-
 // ------------------------------------------------------------------ recover kernel
 // Lane-serial layout: the grid has GT = gridDim.x * WG threads and thread g owns the
 // signatures idx = k * GT + g, k < K_g (K_g <= MAX_SLOTS). Each thread runs Montgomery's
@@ -93,9 +27,8 @@ DEV void recover_body(const RecoverParams& prm, uint64_t* stamps) {
   ST* st = &st_;
   uint4* const slot = recover_slots(prm.rec, prm.n_pad);
   const uint32_t np = prm.n_pad;
-  const uint32_t bias = prm.ls_host ? 1u : 0u;  // host-buffer form: block 0 is the mirror
-  const uint32_t GT = (gridDim.x - bias) * WG;
-  const uint32_t g = (blockIdx.x - bias) * WG + threadIdx.x;
+  const uint32_t GT = gridDim.x * WG;
+  const uint32_t g = blockIdx.x * WG + threadIdx.x;
   const uint32_t K = g < prm.n ? (prm.n - g + GT - 1) / GT : 0;  // my signatures
   uint32_t okm = 0;
   const uint32_t units = 5u * K;
@@ -105,26 +38,20 @@ DEV void recover_body(const RecoverParams& prm, uint64_t* stamps) {
   for (uint32_t k = 0; k < K; ++k) {
     balance_prio(k, units);
     const uint32_t idx = k * GT + g;
-    uint32_t rl[8], meta;
-    bool ok, ovr, ovs;
-    sc R;
+    uint32_t rl[8];
+    rec_get(prm, 8, idx, rl);
+    const uint32_t meta = prm.rec[(size_t)24 * np + idx];
+    const uint32_t recid = meta & 3u;
+    bool ok = ((meta >> 8) & 0xffu) == ST_OK;
+    // parse_compact: r, s >= n => failure (recovery/main_impl.h:38-58)
+    bool ovr, ovs;
+    sc R = sc_from_limbs(rl, ovr);
     {
       uint32_t sl[8];
-      if (prm.ls_msg) {  // host-buffer form: this slot's piece has arrived, then the parse
-        ls_wait(prm, (g / prm.ls_group) * prm.ls_kmax + k);
-        ls_parse(prm, idx, rl, sl, meta);
-      } else {
-        rec_get(prm, 8, idx, rl);
-        rec_get(prm, 16, idx, sl);
-        meta = prm.rec[(size_t)24 * np + idx];
-      }
-      ok = ((meta >> 8) & 0xffu) == ST_OK;
-      // parse_compact: r, s >= n => failure (recovery/main_impl.h:38-58)
-      R = sc_from_limbs(rl, ovr);
+      rec_get(prm, 16, idx, sl);
       const sc S = sc_from_limbs(sl, ovs);
       ok = ok && !ovr && !ovs && !sc_is_zero(R) && !sc_is_zero(S);
     }
-    const uint32_t recid = meta & 3u;
     // x = r (+ n)  (main_impl.h:101-109)
     uint32_t xr[8];
 #pragma unroll
@@ -236,14 +163,6 @@ DEV void recover_body(const RecoverParams& prm, uint64_t* stamps) {
     }
   }
   st->mark(6);
-  if (prm.ls_done) {  // host-buffer form: this workgroup's outputs are complete
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores acknowledged
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      __hip_atomic_store(prm.ls_done + (blockIdx.x - bias), prm.ls_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
   if constexpr (!std::is_same<ST, NoStamp>::value) {
     if ((threadIdx.x & 63) == 0) {
       const uint32_t w = blockIdx.x * (WG / 64) + (threadIdx.x >> 6);
@@ -256,13 +175,7 @@ DEV void recover_body(const RecoverParams& prm, uint64_t* stamps) {
 #ifndef EGES_RECOVER_WAVES
 #define EGES_RECOVER_WAVES 2
 #endif
-__global__ void __launch_bounds__(WG, EGES_RECOVER_WAVES) recover_kernel(RecoverParams prm) {
-  if (prm.ls_host && blockIdx.x == 0) {
-    ls_mirror(prm);
-    return;
-  }
-  recover_body<NoStamp>(prm, nullptr);
-}
+__global__ void __launch_bounds__(WG, EGES_RECOVER_WAVES) recover_kernel(RecoverParams prm) { recover_body<NoStamp>(prm, nullptr); }
 
 #ifdef EGES_PHASE_STAMPS
 __global__ void __launch_bounds__(WG, 2) recover_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
@@ -288,13 +201,6 @@ hipError_t launch_recover_stamped(const RecoverParams& p, int max_blocks, int ws
   return hipGetLastError();
 }
 #endif
-
-hipError_t launch_recover_host(const RecoverParams& p, int grid, int ws_blocks, hipStream_t st) {
-  if (p.n == 0) return hipSuccess;
-  if (!p.ls_host || grid + 1 > ws_blocks || (uint64_t)grid * WG * MAX_SLOTS < p.n) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(recover_kernel, dim3(grid + 1), dim3(WG), 0, st, p);
-  return hipGetLastError();
-}
 
 int lane_serial_grid(uint32_t n, int max_blocks) { return grid_for_lane_serial(n, max_blocks); }
 

@@ -41,13 +41,6 @@ enum KnobId : int {
   KNOB_GATE,              // 1: single-chunk host-buffer calls on the mid-size kernels launch first and copy
                           //   their inputs while the launch is in flight (hostpath.hip Gate; the latency
                           //   kernels run ungated)
-  KNOB_HOST_ONE,          // 1: host-buffer ecrecover shards of 2 * PIPE_MIN .. CHUNK signatures run as ONE
-                          //   lane-serial launch fed piece by piece (hostpath.hip run_host_one); 0: chunked
-  KNOB_HOST_FEEDERS,      //   threads that write its pieces into the pinned staging (the caller included)
-  KNOB_TEST_HOST_ONE,     // tests / probes of run_host_one: bit 0 re-reads the pinned outputs after the
-                          //   stream drained and fails the call if a copied block differs; bit 1 puts
-                          //   the outputs in coherent (uncached) pinned memory; bit 2 writes the
-                          //   staging with non-temporal stores; bit 3 writes every piece before the launch
   KNOB_COUNT
 };
 

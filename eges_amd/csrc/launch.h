@@ -78,23 +78,6 @@ struct RecoverParams {
   int wire_signer = 0;
   uint64_t wire_chain_id = 0;
   uint8_t* wire_sighash = nullptr;
-  // lane-serial kernel, host-buffer form (hostpath.hip run_host_one: one launch over a whole shard
-  // while the host is still writing its inputs). Phase A parses ls_msg / ls_sig (n x 32, n x 65,
-  // pinned host memory) into the record rows itself; before thread g reads slot k it waits until
-  // the device word *ls_arrived reaches ls_seq + piece + 1, piece = (g / ls_group) * ls_kmax + k
-  // (ls_group a multiple of WG). Block 0 of the launch is the mirror: it copies the host's
-  // coherent word *ls_host (the pieces written so far) into *ls_arrived until it reaches
-  // ls_final, so the other waves poll device memory, not the bus; the signature blocks are
-  // 1 .. grid (launch_recover_host). A wait that runs out stores 1 into *ls_fault (coherent
-  // pinned). After its stores every signature block b stores ls_seq into ls_done[b - 1]
-  // (coherent pinned): the host copies that block's outputs out while the others run.
-  const uint8_t* ls_msg = nullptr;
-  const uint8_t* ls_sig = nullptr;
-  uint32_t* ls_arrived = nullptr;
-  const uint32_t* ls_host = nullptr;
-  uint32_t ls_seq = 0, ls_final = 0, ls_group = 0, ls_kmax = 0;
-  uint32_t* ls_done = nullptr;
-  uint32_t* ls_fault = nullptr;
 };
 
 struct VerifyParams {
@@ -159,9 +142,6 @@ size_t lat_waves(uint32_t n);
 // max_blocks: the resident grid; ws_blocks: blocks the workspace p.ws was allocated for. A
 // launch whose grid would exceed ws_blocks is refused (hipErrorInvalidValue), never run.
 hipError_t launch_recover(const RecoverParams& p, int max_blocks, int ws_blocks, hipStream_t st);
-// The host-buffer form (RecoverParams::ls_*): `grid` signature blocks after the mirror block 0
-// (grid + 1 blocks, each indexing ws by its blockIdx: refused unless grid + 1 <= ws_blocks).
-hipError_t launch_recover_host(const RecoverParams& p, int grid, int ws_blocks, hipStream_t st);
 // Small batches: one signature per 16-lane row, limb-parallel field arithmetic (k_recover_lat.hip).
 // Same inputs (prep records) and outputs as launch_recover; no workspace.
 hipError_t launch_recover_lat(const RecoverParams& p, hipStream_t st);

@@ -97,24 +97,6 @@ def allgather_nccl():
     return {"ok": ok, "backend": backend}
 
 
-def host_one_groups():
-    """run_host_one on a small resident grid (EGES_TEST_MAX_BLOCKS=64: 32 resident blocks, a
-    74-block grid of 32 slots per thread, i.e. 3 generations x 32 slots = 96 pieces): every
-    piece's wait, every block's done word, against the golden fixture tiled to 600,011 items."""
-    import numpy as np
-    import eges_amd
-    from eges_amd._lib import lib
-    eges_amd.init(1)
-    n = 600_011
-    msg, sig, pub, st = tiled_golden(n)
-    p, _, s = eges_amd.ecrecover_batch(msg, sig)
-    ok = bool(np.array_equal(s, st) and np.array_equal(p, pub))
-    eges_amd.set_knob("EGES_HOST_ONE", 0)
-    p0, _, s0 = eges_amd.ecrecover_batch(msg, sig)
-    same = bool(np.array_equal(p0, p) and np.array_equal(s0, s))
-    return {"ok": ok, "same_as_chunked": same, "devices": int(lib.eges_device_count())}
-
-
 def other_process_kernels():
     """A second process on the same GPU (test_gpu_resident.py): a device-resident 1M batch,
     timed with HIP events each time a line "go" arrives on stdin; prints one number per launch
@@ -149,5 +131,5 @@ def other_process_kernels():
 if __name__ == "__main__":
     mode = sys.argv[1]
     out = {"small_grid": small_grid, "logical_devices": logical_devices, "allgather_nccl": allgather_nccl,
-           "host_one_groups": host_one_groups, "other_process_kernels": other_process_kernels}[mode]()
+           "other_process_kernels": other_process_kernels}[mode]()
     print(json.dumps(out), flush=True)

@@ -87,14 +87,14 @@ def test_knobs_set_and_read_without_gpu():
     # input gate on); round 5 removed the measured-slower pinned pipeline, second host stream and
     # resident block server, so their names are unknown now
     defaults = {"EGES_RESIDENT": 1, "EGES_GATE": 1, "EGES_HOST_PARTS": 8, "EGES_LAT_TRI_MAX": 448,
-                "EGES_SENDER_FUSED": 1, "EGES_HOST_ONE": 0, "EGES_HOST_FEEDERS": 4}
+                "EGES_SENDER_FUSED": 1}
     for name, want in defaults.items():
         assert eges_amd.get_knob(name) == want, name
     for name in ("EGES_RESIDENT_WGS", "EGES_RESIDENT_CAP", "EGES_RESIDENT_IDLE_MS", "EGES_TEST_DELAY_X",
                  "EGES_TEST_SKIP_FLAG"):
         eges_amd.get_knob(name)
     for gone in ("EGES_HOST_PIPE", "EGES_PIPE_SEG", "EGES_HOST_STREAMS", "EGES_RESIDENT_BLOCK",
-                 "EGES_RESIDENT_BLOCK_CAP"):
+                 "EGES_RESIDENT_BLOCK_CAP", "EGES_HOST_ONE", "EGES_HOST_FEEDERS", "EGES_TEST_HOST_ONE"):
         assert lib.eges_test_set_knob(gone.encode(), 1) == EGES_E_INVALID_ARG, gone
     assert lib.eges_test_set_knob(b"EGES_NO_SUCH_KNOB", 1) == EGES_E_INVALID_ARG
     with pytest.raises(EgesError):

@@ -83,9 +83,3 @@ def test_records_all_gather_over_rccl():
     out = _child("allgather_nccl", {"EGES_TEST_PORT": str(29000 + os.getpid() % 1000)})
     assert out["ok"] and out["backend"] == "nccl", out
 
-
-def test_host_one_launch_many_groups():
-    """The one-launch host-buffer form with several generations and 32 slots per thread
-    (EGES_TEST_MAX_BLOCKS=64), equal to the fixture and to the chunked path."""
-    out = _child("host_one_groups", {"EGES_TEST_MAX_BLOCKS": "64"})
-    assert out["ok"] and out["same_as_chunked"], out

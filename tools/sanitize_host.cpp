@@ -373,16 +373,11 @@ int main(int argc, char** argv) {
     for (size_t n : {1u, 37u, 1000u, 5000u, 70000u}) batch_recover(n);
     single_item_threads(8, 300);
     signed_block(300);
-    // the one-launch host-buffer form (a shard of 512k .. 2M items), then the chunked path
-    // (EGES_HOST_PARTS chunks)
-    step("host one launch");
-    batch_recover(600011);
+    // the chunked host-buffer path (a shard of >= 512k items in EGES_HOST_PARTS chunks)
     step("host chunks");
-    eges_test_set_knob("EGES_HOST_ONE", 0);
     eges_test_set_knob("EGES_HOST_PARTS", 5);
     batch_recover(600011);
     eges_test_set_knob("EGES_HOST_PARTS", 8);
-    eges_test_set_knob("EGES_HOST_ONE", 1);
     block_structure(2000);
     eges_shutdown();
   }
