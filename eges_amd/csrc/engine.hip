@@ -65,6 +65,7 @@ static const KnobDef KNOB_DEFS[] = {
     {"EGES_RESIDENT_CAP", 64},
     {"EGES_RESIDENT_IDLE_MS", 4},
     {"EGES_GATE", 1},
+    {"EGES_GATE_STEP", 0},
 };
 static_assert(sizeof(KNOB_DEFS) / sizeof(KNOB_DEFS[0]) == KNOB_COUNT, "a name and default for every knob");
 std::atomic<long long> g_knob[KNOB_COUNT];

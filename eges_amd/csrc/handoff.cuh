@@ -47,34 +47,49 @@ DEV bool ho_failed(const uint32_t* err, const Diag& dg) {
   return bad;
 }
 // Host-buffer calls launch before their inputs are in the pinned buffer (hostpath.hip Gate): the
-// host copies them while the launch is in flight and then stores the call's sequence into the
-// gate word (coherent pinned memory). Workgroup 0's first wave alone polls that word (a poller
-// per wave over PCIe slowed a 1,000-workgroup launch 2.4x) and mirrors the sequence into a
-// device word that every wave waits for here before reading an input. No input line can be
-// cached on the device before that (the launch invalidated the caches, and nothing reads the
-// inputs before the gate), so no system-scope cache invalidation follows. A wait that runs out
-// (4 s; the host opens the gate on every path, microseconds after its launch) marks gate[1], and
-// the host fails the call rather than return results from stale inputs.
+// host copies them while the launch is in flight and stores its progress into the gate word
+// (coherent pinned memory) piece by piece, in workgroup order. Workgroup 0's first wave alone
+// polls that word (a poller per wave over PCIe slowed a 1,000-workgroup launch 2.4x) and mirrors
+// every new value into a device word, until the last piece; every other wave waits there for the
+// piece its own workgroup reads (gate_step workgroups per piece), so the first workgroups start
+// while the host still copies the last ones' inputs and their reads over the bus are spread out
+// instead of all at once. No input line can be cached on the device before its piece is open
+// (the launch invalidated the caches, and nothing reads an input before its gate), so no
+// system-scope cache invalidation follows. A wait that runs out (4 s; the host opens every piece
+// on every path, microseconds after its launch) marks gate[1], and the host fails the call rather
+// than return results from stale inputs.
 DEV bool seq_before(uint32_t have, uint32_t want) { return (int32_t)(have - want) < 0; }
-DEV void gate_wait(const uint32_t* gate, uint32_t* mirror, uint32_t seq) {
-  if (!gate) return;
+template <class P>
+DEV void gate_wait(const P& prm) {
+  if (!prm.gate) return;
   constexpr uint64_t BOUND = 400000000ull;  // s_memrealtime ticks (100 MHz): 4 s
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const uint32_t want = prm.gate_step ? prm.gate_seq - prm.gate_pieces + blockIdx.x / prm.gate_step + 1u : prm.gate_seq;
   if (blockIdx.x == 0 && threadIdx.x < 64) {
-    uint32_t* g = const_cast<uint32_t*>(gate);
+    uint32_t* g = const_cast<uint32_t*>(prm.gate);
+    uint32_t last = prm.gate_seq - prm.gate_pieces;  // (no piece open yet)
 #pragma unroll 1
-    while (seq_before(__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), seq)) {
+    for (;;) {
+      const uint32_t v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+      if (v != last && !seq_before(v, last)) {
+        if (threadIdx.x == 0) __hip_atomic_store(prm.gate_dev, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = v;
+      }
+      if (!seq_before(v, prm.gate_seq)) break;
       if (__builtin_amdgcn_s_memrealtime() - t0 > BOUND) {
-        if (threadIdx.x == 0) __hip_atomic_store(g + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (threadIdx.x == 0) {
+          __hip_atomic_store(g + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(prm.gate_dev, prm.gate_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // release the waves
+        }
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    if (threadIdx.x == 0) __hip_atomic_store(mirror, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     return;
   }
 #pragma unroll 1
-  while (seq_before(__hip_atomic_load(mirror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), seq)) {
+  while (seq_before(__hip_atomic_load(prm.gate_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), want)) {
     if (__builtin_amdgcn_s_memrealtime() - t0 > BOUND + BOUND / 4) break;  // (workgroup 0 marks the failure)
     __builtin_amdgcn_s_sleep(2);
   }

@@ -136,17 +136,46 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       return set_err(EGES_E_NOMEM, "hipMalloc(gate) failed");
     }
   }
+  // The deferred copies of a gated chunk, opened in pieces of `per` items in item order (the
+  // mid-size kernels' workgroup order): each queued array knows its item stride (0: the wire bytes,
+  // cut at the offsets; -1: the offsets array itself, n + 1 entries) so a piece copies only its
+  // items' bytes, then publishes base + piece + 1 (handoff.cuh gate_wait).
   struct GateOpen {
     struct Copy {
       uint8_t* dst;
-      const void* src;
+      const uint8_t* src;
       size_t n;
+      long stride;
     } q[8];
     int nq = 0;
-    uint32_t* w = nullptr;  // armed: the kernels wait for sequence `seq`
-    uint32_t seq = 0;
+    const uint64_t* offs = nullptr;  // the wire form's host offsets of this chunk (stride 0)
+    size_t items = 0, per = 0;
+    uint32_t* w = nullptr;  // armed: the kernels wait for sequence `seq` (the last piece)
+    uint32_t seq = 0, pieces = 1;
+    void copy_range(const Copy& c, size_t lo, size_t hi) const {
+      size_t a, b;
+      if (c.stride > 0) {
+        a = lo * (size_t)c.stride;
+        b = hi * (size_t)c.stride;
+      } else if (c.stride == 0) {
+        a = offs[lo] - offs[0];
+        b = offs[hi] - offs[0];
+      } else {  // entries lo .. hi: item hi - 1 ends at entry hi (the next piece copies it again)
+        a = lo * 8;
+        b = (hi + 1) * 8;
+      }
+      if (b > c.n) b = c.n;
+      if (b > a) std::memcpy(c.dst + a, c.src + a, b - a);
+    }
     void open() {
-      for (int i = 0; i < nq; ++i) std::memcpy(q[i].dst, q[i].src, q[i].n);
+      if (nq) {
+        const size_t step = pieces > 1 ? per : items;
+        for (uint32_t p = 0; p < pieces; ++p) {
+          const size_t lo = (size_t)p * step, hi = std::min(items, lo + step);
+          for (int i = 0; i < nq; ++i) copy_range(q[i], lo, hi);
+          if (w) publish_u32(w, seq - pieces + p + 1);
+        }
+      }
       nq = 0;
       if (w) publish_u32(w, seq);
       w = nullptr;
@@ -157,13 +186,22 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   bool gated = false;  // a gated mid-size launch ran: its last workgroup stores the sequence into gate.w[2]
   auto arm = [&](RecoverParams& p) {  // a deferred chunk's kernels wait at the gate
     if (!defer || p.n == 0) return;
-    if (++gate.seq == 0) gate.seq = 1;
+    // pieces of GATE_STEP workgroups (64 items each) when the grid has several of them
+    const uint32_t wgs = (p.n + MID_SIGS_PER_BLOCK - 1) / MID_SIGS_PER_BLOCK;
+    const uint32_t step = rt.gate_step > 0 ? (uint32_t)rt.gate_step : wgs;
+    const uint32_t pieces = (wgs + step - 1) / step;
+    gate.seq += pieces;  // (wraps harmlessly: every comparison is a sequence difference)
     gated = true;  // (a mid-size launch: its kernels store the completion word)
     p.gate = gate.w;
     p.gate_dev = gate.dev;
     p.gate_seq = gate.seq;
+    p.gate_step = pieces > 1 ? step : 0u;
+    p.gate_pieces = pieces;
     gopen.w = gate.w;
     gopen.seq = gate.seq;
+    gopen.pieces = pieces;
+    gopen.items = p.n;
+    gopen.per = (size_t)step * MID_SIGS_PER_BLOCK;
   };
   // VerifySignature: a hand-off fault leaves its item's ok byte 0 and stores 1 into this word
   uint32_t*& vfault = small ? lane->vfault : d.vfault;
@@ -183,10 +221,10 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   // (pageable) copy into device memory on the copy stream, or, for a pinned call, packed into
   // the pinned buffer at the same offset, where the kernels read it directly (zero-copy: no
   // H2D / D2H operations at all, the outputs are written straight into the pinned buffer too).
-  auto h2d = [&](uint8_t* B, uint8_t* dst, const void* src, size_t bytes) -> int {
+  auto h2d = [&](uint8_t* B, uint8_t* dst, const void* src, size_t bytes, long stride) -> int {
     if (!bytes) return EGES_SUCCESS;
     if (pinned) {  // dst points into the pinned buffer (see I below)
-      if (defer && gopen.nq < 8) gopen.q[gopen.nq++] = {dst, src, bytes};
+      if (defer && gopen.nq < 8) gopen.q[gopen.nq++] = {dst, static_cast<const uint8_t*>(src), bytes, stride};
       else std::memcpy(dst, src, bytes);  // (at most 5 inputs per kind: q never fills)
       return EGES_SUCCESS;
     }
@@ -195,10 +233,10 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     return EGES_SUCCESS;
   };
   auto flush_in = [&](uint8_t*) -> int { return EGES_SUCCESS; };
-#define H2D(B, dst, src, bytes)                   \
-  do {                                             \
-    int rc_ = h2d((B), (dst), (src), (bytes));     \
-    if (rc_) return rc_;                           \
+#define H2D(B, dst, src, bytes, stride)                   \
+  do {                                                     \
+    int rc_ = h2d((B), (dst), (src), (bytes), (stride));   \
+    if (rc_) return rc_;                                   \
   } while (0)
 #define FLUSH_IN(B)                 \
   do {                              \
@@ -270,8 +308,8 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       uint8_t* ds = dm + m * 32;
       const bool fused = fused_parse(d, rt, m);
       defer = gating && fused && use_mid(d, rt, m);  // (the latency kernels measured +-0 to +1.5 % slower)
-      H2D(B, dm, j.a + base * 32, m * 32);
-      H2D(B, ds, j.b + base * 65, m * 65);
+      H2D(B, dm, j.a + base * 32, m * 32, 32);
+      H2D(B, ds, j.b + base * 65, m * 65, 65);
       FLUSH_IN(B);
       JOIN_IN(r);
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, j.addr ? o_addr : nullptr, j.pub ? o_pub : nullptr,
@@ -292,11 +330,11 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       uint8_t* df = dv + m * 32;
       const bool fused = sender_fused(d, rt, m, {dh, dr, dsv, dv});
       defer = gating && fused && use_mid(d, rt, m);  // (the latency kernels measured +-0 to +1.5 % slower)
-      H2D(B, dh, j.a + base * 32, m * 32);
-      H2D(B, dr, j.b + base * 32, m * 32);
-      H2D(B, dsv, j.c + base * 32, m * 32);
-      H2D(B, dv, j.d + base * 32, m * 32);
-      if (j.e) H2D(B, df, j.e + base, m);
+      H2D(B, dh, j.a + base * 32, m * 32, 32);
+      H2D(B, dr, j.b + base * 32, m * 32, 32);
+      H2D(B, dsv, j.c + base * 32, m * 32, 32);
+      H2D(B, dv, j.d + base * 32, m * 32, 32);
+      if (j.e) H2D(B, df, j.e + base, m, 1);
       FLUSH_IN(B);
       JOIN_IN(r);
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr, nullptr, d.gtab, wsk};
@@ -310,8 +348,8 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     } else if (j.kind == HostJob::PRECOMPILE) {
       uint8_t* din = I;
       uint32_t* dlen = reinterpret_cast<uint32_t*>(din + m * 128);
-      H2D(B, din, j.a + base * 128, m * 128);
-      if (j.inlen) H2D(B, reinterpret_cast<uint8_t*>(dlen), j.inlen + base, m * 4);
+      H2D(B, din, j.a + base * 128, m * 128, 128);
+      if (j.inlen) H2D(B, reinterpret_cast<uint8_t*>(dlen), j.inlen + base, m * 4, 4);
       FLUSH_IN(B);
       JOIN_IN(r);
       if (pinned) std::memset(o_addr, 0, m * 32);
@@ -331,8 +369,9 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       // + DMA into device memory measured 0.486-0.508 ms against 0.450 ms for C1, same kernel)
       const bool fused = !j.decode_only && wire_fused(d, rt, m, draw);
       defer = gating && fused && use_mid(d, rt, m);  // (the latency kernels measured +-0 to +1.5 % slower)
-      if (rg.raw_len) H2D(B, draw, j.a + rg.raw_lo, rg.raw_len);
-      H2D(B, reinterpret_cast<uint8_t*>(doff), j.offsets + base, 8 * (m + 1));
+      if (defer) gopen.offs = j.offsets + base;  // (the raw bytes open at these offsets, piece by piece)
+      if (rg.raw_len) H2D(B, draw, j.a + rg.raw_lo, rg.raw_len, 0);
+      H2D(B, reinterpret_cast<uint8_t*>(doff), j.offsets + base, 8 * (m + 1), -1);
       FLUSH_IN(B);
       JOIN_IN(r);
       if (j.decode_only) {  // the decoder's flags straight into the status bytes
@@ -357,10 +396,10 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       uint8_t* dl = dp + m * 65;
       uint8_t* dm = dl + m;
       uint8_t* ds = dm + m * 32;
-      H2D(B, dp, j.a + base * 65, m * 65);
-      H2D(B, dl, j.b + base, m);
-      H2D(B, dm, j.c + base * 32, m * 32);
-      H2D(B, ds, j.d + base * 64, m * 64);
+      H2D(B, dp, j.a + base * 65, m * 65, 65);
+      H2D(B, dl, j.b + base, m, 1);
+      H2D(B, dm, j.c + base * 32, m * 32, 32);
+      H2D(B, ds, j.d + base * 64, m * 64, 64);
       FLUSH_IN(B);
       JOIN_IN(r);
       VerifyParams p{dp, dl, dm, ds, (uint32_t)m, o_st, d.gtab, wsk};

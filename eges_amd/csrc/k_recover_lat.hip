@@ -841,7 +841,7 @@ template <class ST, int FORM>
 DEV void recover_lat_body(const RecoverParams& prm, uint64_t* stamps) {
   constexpr bool SPLIT = FORM == FORM_SPLIT;
   __shared__ LatLds S;
-  gate_wait(prm.gate, prm.gate_dev, prm.gate_seq);
+  gate_wait(prm);
   if (!SPLIT && blockIdx.x < prm.n_helpers) {  // narrow / three-wave forms: the lane-serial roots
     root_helper(prm, prm.epoch, prm.n);
     return;

@@ -277,7 +277,7 @@ DEV void recode_mid(const glv_half& h, int8_t (*lo)[MID_L], int8_t (*hi)[MID_L],
 
 template <class ST>
 DEV void recover_mid_body(const RecoverParams& prm, uint64_t* stamps) {
-  gate_wait(prm.gate, prm.gate_dev, prm.gate_seq);
+  gate_wait(prm);
   __shared__ MidLds S;
   ST st_;
   const Diag dg = diag_of(prm);
@@ -675,7 +675,7 @@ DEV void verify_parse_lane(const RecoverParams& prm, uint32_t idx, LatParse& q, 
 
 template <class ST, bool VERIFY = false>
 DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
-  gate_wait(prm.gate, prm.gate_dev, prm.gate_seq);
+  gate_wait(prm);
   __shared__ BktLds S;
   ST st_;
   const Diag dg = diag_of(prm);

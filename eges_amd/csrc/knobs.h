@@ -41,6 +41,8 @@ enum KnobId : int {
   KNOB_GATE,              // 1: single-chunk host-buffer calls on the mid-size kernels launch first and copy
                           //   their inputs while the launch is in flight (hostpath.hip Gate; the latency
                           //   kernels run ungated)
+  KNOB_GATE_STEP,         //   mid-size workgroups per gate piece (the host opens the inputs piece by piece;
+                          //   0: one piece)
   KNOB_COUNT
 };
 

@@ -51,6 +51,10 @@ struct RecoverParams {
   const uint32_t* gate = nullptr;
   uint32_t* gate_dev = nullptr;  // its device-memory mirror (workgroup 0 copies the sequence there)
   uint32_t gate_seq = 0;
+  // progressive gate (the mid-size kernels): the host opens the inputs in gate_pieces pieces of
+  // gate_step workgroups each (the word reaches gate_seq - gate_pieces + p + 1 once piece p is
+  // in place); workgroup b waits for its own piece b / gate_step only. gate_step 0: one gate.
+  uint32_t gate_step = 0, gate_pieces = 1;
   // tests only (KNOB_FORCE_REDO): run every exact-redo pass as if an accumulator was poisoned
   uint32_t force_redo = 0;
   // tests only (KNOB_TEST_SKIP_FLAG, handoff.cuh): workgroup test_skip_block's producer of hand-off

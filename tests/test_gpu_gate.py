@@ -62,3 +62,49 @@ def test_gate_back_to_back_sizes(engine):
             sel = (np.arange(n) + rep * 131) % n_all
             pub, addr, st = engine.ecrecover_batch(g["msg"][sel], g["sig"][sel])
             assert np.array_equal(st, g["status"][sel]) and np.array_equal(pub, g["pub"][sel]), (rep, n)
+
+
+def _c1_batch(engine, first, n):
+    """n C1-shaped transfers (nonce first + i) signed by the GPU synthetic signer,
+    as wire bytes, with their signers' addresses"""
+    import torch
+    from eges_amd import txs
+    sighash = txs.c1_sighashes(first, n)
+    sig_d, exp_d = engine.synth_sign_msg_dev(torch.from_numpy(sighash).cuda(), first)
+    torch.cuda.synchronize()
+    sig, exp = sig_d.cpu().numpy(), exp_d.cpu().numpy()
+    return txs.c1_raw(first, sig), exp
+
+
+@pytest.mark.parametrize("step", [1, 3, 16, 0])
+def test_gate_pieces_wire_and_golden(engine, step):
+    """The progressive gate (EGES_GATE_STEP workgroups per piece; 0 = one piece): the host opens
+    the inputs piece by piece in workgroup order while each mid-size workgroup waits for its own
+    piece only. Two different 10k wire-format batches alternate (a workgroup that read its
+    inputs before its piece was copied would return the other batch's sender), and the golden
+    recovery and sender fixtures tiled to 7,000 items go through the bucket and windowed forms."""
+    from eges_amd import txs
+    from eges_amd._lib import SIGNER_EIP155
+    batches = [_c1_batch(engine, first, 10000) for first in (0, 50000)]
+    with knobs(engine, {"EGES_GATE": 1, "EGES_GATE_STEP": step, "EGES_RESIDENT": 0}):
+        for rep in range(6):
+            raws, exp = batches[rep % 2]
+            addr, st, _ = engine.sender_raw_batch(raws, SIGNER_EIP155, txs.GEEC_CHAIN_ID)
+            bad = np.nonzero((st != 0) | (addr != exp).any(axis=1))[0]
+            assert bad.size == 0, (step, rep, bad[:10].tolist())
+    g = load_golden("recover.npz")
+    gs = load_golden("sender.npz")
+    n = 7000
+    idx = [np.arange(n) % len(g["msg"]), (np.arange(n) * 7 + 3) % len(g["msg"])]
+    sel = np.nonzero((gs["signer"] == 2) & (gs["chain_id"] == 930412))[0]
+    sidx = [sel[np.arange(n) % len(sel)], sel[(np.arange(n) * 5 + 1) % len(sel)]]
+    for form in ("bucket", "windowed"):
+        with knobs(engine, dict(FORMS[form], EGES_GATE=1, EGES_GATE_STEP=step, EGES_RESIDENT=0)):
+            for rep in range(4):
+                i = idx[rep % 2]
+                pub, _, st = engine.ecrecover_batch(g["msg"][i], g["sig"][i])
+                assert np.array_equal(st, g["status"][i]) and np.array_equal(pub, g["pub"][i]), (form, step, rep)
+                k = sidx[rep % 2]
+                a, s_ = engine.sender_batch(gs["sighash"][k], gs["r"][k], gs["s"][k], gs["v"][k], gs["vflags"][k], 2,
+                                            930412)
+                assert np.array_equal(s_, gs["status"][k]) and np.array_equal(a, gs["addr"][k]), (form, step, rep)
