@@ -123,6 +123,7 @@ struct Dev {
   uint32_t* ws = nullptr;
   uint32_t* diag = nullptr;  // DIAG_WORDS counters (eges_diag_counters)
   int mb_recover = 0, mb_verify = 0, mb_synth = 0;
+  int gm = 1;  // resident generations of a lane-serial grid (EGES_GRID_MULT)
   int ws_blocks = 0;  // blocks ws (and ws2) hold: every launch's grid is checked against it
   uint8_t* buf = nullptr;  // per-call device scratch, grown on demand
   size_t buf_cap = 0;
@@ -154,9 +155,10 @@ extern std::atomic<long long> g_knob[KNOB_COUNT];
 struct Route {
   size_t lat_max = 0, mid_max = 0;
   uint32_t wide_max = 0, tri_max = 0;
-  long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, gate = 1, gate_step = 0;
+  long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, gate = 1, gate_step = 8;
   size_t host_parts = EGES_PIPE_PARTS;
   uint32_t force_redo = 0, skip_flag = 0, delay_x = 0;
+  int host_gens = 0;
   static Route now() {
     Route r;
     r.lat_max = (size_t)std::max<long long>(0, knob(KNOB_LAT_MAX));
@@ -168,6 +170,7 @@ struct Route {
     r.sender_fused = knob(KNOB_SENDER_FUSED);
     r.gate = knob(KNOB_GATE);
     r.gate_step = std::max<long long>(0, std::min<long long>(knob(KNOB_GATE_STEP), 1 << 20));
+    r.host_gens = (int)std::max<long long>(0, std::min<long long>(knob(KNOB_HOST_GENS), 8));
     r.tri_max = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_LAT_TRI_MAX), 1u << 30));
     r.host_parts = (size_t)std::max<long long>(2, std::min<long long>(knob(KNOB_HOST_PARTS), 64));
     r.force_redo = knob(KNOB_FORCE_REDO) != 0 ? 1u : 0u;
@@ -257,7 +260,9 @@ bool fused_parse(const Dev& d, const Route& rt, size_t n);
 bool sender_fused(const Dev& d, const Route& rt, size_t n, std::initializer_list<const void*> rows);
 void bind_sender_rows(RecoverParams& p, const uint8_t* h, const uint8_t* r, const uint8_t* s, const uint8_t* v,
                       const uint8_t* f, int signer, uint64_t chain_id);
-hipError_t launch_recover_pass(Dev& d, const Route& rt, const RecoverParams& p0, hipStream_t st);
+// gens > 0: a lane-serial launch covers at most `gens` resident generations (host-buffer chunks,
+// EGES_HOST_GENS) instead of the device's EGES_GRID_MULT
+hipError_t launch_recover_pass(Dev& d, const Route& rt, const RecoverParams& p0, hipStream_t st, int gens = 0);
 // wire-format rows after the recovery records (tx_rows_kernel's decode)
 inline size_t tx_rows_bytes(size_t m) { return align_up(m * (4 * 32 + 1), 256); }
 bool wire_fused(const Dev& d, const Route& rt, size_t m, const uint8_t* raw);

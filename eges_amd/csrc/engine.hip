@@ -65,7 +65,8 @@ static const KnobDef KNOB_DEFS[] = {
     {"EGES_RESIDENT_CAP", 64},
     {"EGES_RESIDENT_IDLE_MS", 4},
     {"EGES_GATE", 1},
-    {"EGES_GATE_STEP", 0},
+    {"EGES_GATE_STEP", 8},
+    {"EGES_HOST_GENS", 0},
 };
 static_assert(sizeof(KNOB_DEFS) / sizeof(KNOB_DEFS[0]) == KNOB_COUNT, "a name and default for every knob");
 std::atomic<long long> g_knob[KNOB_COUNT];
@@ -137,6 +138,7 @@ int init_device(int id, DevPtr* out) {
   // (the batch inversions, amortised over 4 instead of 8, cost less than that tail): C2 +2.0 %
   // (99.4 -> 101.3 M sigs/s, 3 reps each, same box), C4 +0.1 %, VerifySignature +1.2 %.
   const int gm = std::max(1, std::min(8, env_int("EGES_GRID_MULT", 2)));
+  d->gm = gm;
   d->mb_recover = occupancy_recover() * d->cus * gm;
   d->mb_verify = occupancy_verify() * d->cus * gm;
   d->mb_synth = occupancy_synth() * d->cus;

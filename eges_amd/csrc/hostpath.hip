@@ -23,18 +23,23 @@ extern "C" size_t eges_diag_host_stamps(int64_t* out, size_t n) {
 struct Region {
   size_t in_bytes = 0, raw_lo = 0, raw_len = 0, o_rec = 0, o_out = 0, total = 0;
 };
+// Every input array of a region starts on a 128-byte line (LINE): a gated call opens its inputs
+// piece by piece, and no line may hold bytes of two arrays, one of which a workgroup reads before
+// the piece holding the other's bytes is open (that line would then sit in L2 with stale bytes).
+constexpr size_t LINE = 128;
 Region region_for(const HostJob& j, size_t base, size_t m) {
   Region g;
   const size_t m_pad = align_up(m, 64);
+  const size_t a32 = align_up(m * 32, LINE);
   switch (j.kind) {
-    case HostJob::RECOVER: g.in_bytes = m * (32 + 65); break;
-    case HostJob::SENDER: g.in_bytes = m * (32 * 4 + 1); break;
-    case HostJob::VERIFY: g.in_bytes = m * (65 + 1 + 32 + 64); break;
-    case HostJob::PRECOMPILE: g.in_bytes = m * (128 + 4); break;
+    case HostJob::RECOVER: g.in_bytes = a32 + align_up(m * 65, LINE); break;
+    case HostJob::SENDER: g.in_bytes = 4 * a32 + align_up(m, LINE); break;
+    case HostJob::VERIFY: g.in_bytes = align_up(m * 65, LINE) + align_up(m, LINE) + a32 + align_up(m * 64, LINE); break;
+    case HostJob::PRECOMPILE: g.in_bytes = align_up(m * 128, LINE) + align_up(m * 4, LINE); break;
     case HostJob::SENDER_RAW:
       g.raw_lo = j.offsets[base] - j.offsets[0];
       g.raw_len = j.offsets[base + m] - j.offsets[base];
-      g.in_bytes = align_up(g.raw_len, 8) + 8 * (m + 1) + tx_rows_bytes(m);
+      g.in_bytes = align_up(g.raw_len, LINE) + align_up(8 * (m + 1), LINE) + tx_rows_bytes(m);
       break;
   }
   const size_t rec_bytes = (j.kind == HostJob::VERIFY) ? verify_scratch_bytes(m_pad) : recover_scratch_bytes(m_pad);
@@ -44,11 +49,6 @@ Region region_for(const HostJob& j, size_t base, size_t m) {
   return g;
 }
 
-// Writes the pieces of a host-buffer launch into pinned staging with several threads: every piece
-// is cut into 1 MB chunks that the threads take in order (work stealing; the calling thread is one
-// of them, so the call never waits for a worker to wake), and the caller publishes piece p (the
-// word the kernel mirrors) as soon as all of its chunks and those of the pieces before it are in
-// place. Each thread fences its own (non-temporal) stores before it counts a chunk done.
 // Host-buffer pipeline over chunks of one shard. Two device regions alternate: while the
 // compute stream runs chunk i, the copy stream stages chunk i+1's inputs and returns chunk
 // i-1's outputs (host order H2D(i+1), K(i+1), D2H(i): the pageable D2H blocks this thread
@@ -164,7 +164,10 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
         a = lo * 8;
         b = (hi + 1) * 8;
       }
-      if (b > c.n) b = c.n;
+      // (to the end of the line the piece's last bytes, and a dword read past them, fall in: a
+      // workgroup of this piece may bring that line into L2, so it must hold the next piece's
+      // first bytes already; they are the same bytes, copied again with that piece)
+      b = std::min(c.n, align_up(b + 4, LINE));
       if (b > a) std::memcpy(c.dst + a, c.src + a, b - a);
     }
     void open() {
@@ -259,7 +262,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     Region g;
   };
   const size_t astride = j.kind == HostJob::PRECOMPILE ? 32 : 20;
-  auto sighash_off = [&](const Pending& q) { return align_up(q.g.raw_len, 8) + 8 * (q.m + 1); };
+  auto sighash_off = [&](const Pending& q) { return align_up(q.g.raw_len, LINE) + align_up(8 * (q.m + 1), LINE); };
   auto outputs = [&](const Pending& q) -> int {  // D2H of one chunk, on the copy stream
     uint8_t* o_pub = q.B + q.g.o_out;
     uint8_t* o_addr = o_pub + q.m * 65;
@@ -305,7 +308,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     // --- inputs (copy stream), then the kernels (compute stream)
     if (j.kind == HostJob::RECOVER) {
       uint8_t* dm = I;
-      uint8_t* ds = dm + m * 32;
+      uint8_t* ds = dm + align_up(m * 32, LINE);
       const bool fused = fused_parse(d, rt, m);
       defer = gating && fused && use_mid(d, rt, m);  // (the latency kernels measured +-0 to +1.5 % slower)
       H2D(B, dm, j.a + base * 32, m * 32, 32);
@@ -321,13 +324,14 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
         HIPCHK(launch_prep_ecrecover(dm, ds, (uint32_t)m, (uint32_t)m_pad, rec, sk));
       }
       arm(p);
-      HIPCHK(launch_recover_pass(d, rt, p, sk));
+      HIPCHK(launch_recover_pass(d, rt, p, sk, rt.host_gens));
     } else if (j.kind == HostJob::SENDER) {
+      const size_t a32 = align_up(m * 32, LINE);
       uint8_t* dh = I;
-      uint8_t* dr = dh + m * 32;
-      uint8_t* dsv = dr + m * 32;
-      uint8_t* dv = dsv + m * 32;
-      uint8_t* df = dv + m * 32;
+      uint8_t* dr = dh + a32;
+      uint8_t* dsv = dr + a32;
+      uint8_t* dv = dsv + a32;
+      uint8_t* df = dv + a32;
       const bool fused = sender_fused(d, rt, m, {dh, dr, dsv, dv});
       defer = gating && fused && use_mid(d, rt, m);  // (the latency kernels measured +-0 to +1.5 % slower)
       H2D(B, dh, j.a + base * 32, m * 32, 32);
@@ -344,10 +348,10 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
         HIPCHK(launch_prep_sender(dh, dr, dsv, dv, j.e ? df : nullptr, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id,
                                   rec, sk));
       arm(p);
-      HIPCHK(launch_recover_pass(d, rt, p, sk));
+      HIPCHK(launch_recover_pass(d, rt, p, sk, rt.host_gens));
     } else if (j.kind == HostJob::PRECOMPILE) {
       uint8_t* din = I;
-      uint32_t* dlen = reinterpret_cast<uint32_t*>(din + m * 128);
+      uint32_t* dlen = reinterpret_cast<uint32_t*>(din + align_up(m * 128, LINE));
       H2D(B, din, j.a + base * 128, m * 128, 128);
       if (j.inlen) H2D(B, reinterpret_cast<uint8_t*>(dlen), j.inlen + base, m * 4, 4);
       FLUSH_IN(B);
@@ -356,11 +360,11 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
       else HIPCHK(hipMemsetAsync(o_addr, 0, m * 32, sk));
       HIPCHK(launch_prep_precompile(din, j.inlen ? dlen : nullptr, (uint32_t)m, (uint32_t)m_pad, rec, sk));
       RecoverParams p{rec, (uint32_t)m, (uint32_t)m_pad, o_st, o_addr + 12, nullptr, d.gtab, wsk, 32};
-      HIPCHK(launch_recover_pass(d, rt, p, sk));
+      HIPCHK(launch_recover_pass(d, rt, p, sk, rt.host_gens));
     } else if (j.kind == HostJob::SENDER_RAW) {
       uint8_t* draw = I;
-      uint64_t* doff = reinterpret_cast<uint64_t*>(draw + align_up(rg.raw_len, 8));
-      uint8_t* hs = B + align_up(rg.raw_len, 8) + 8 * (m + 1);  // decoded rows: device memory
+      uint64_t* doff = reinterpret_cast<uint64_t*>(draw + align_up(rg.raw_len, LINE));
+      uint8_t* hs = B + align_up(rg.raw_len, LINE) + align_up(8 * (m + 1), LINE);  // decoded rows: device memory
       uint8_t* rr = hs + m * 32;
       uint8_t* sr = rr + m * 32;
       uint8_t* vr = sr + m * 32;
@@ -389,13 +393,13 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
           HIPCHK(launch_prep_sender(hs, rr, sr, vr, vf, (uint32_t)m, (uint32_t)m_pad, j.signer, j.chain_id, rec, sk));
         }
         arm(p);
-        HIPCHK(launch_recover_pass(d, rt, p, sk));
+        HIPCHK(launch_recover_pass(d, rt, p, sk, rt.host_gens));
       }
     } else {
       uint8_t* dp = I;
-      uint8_t* dl = dp + m * 65;
-      uint8_t* dm = dl + m;
-      uint8_t* ds = dm + m * 32;
+      uint8_t* dl = dp + align_up(m * 65, LINE);
+      uint8_t* dm = dl + align_up(m, LINE);
+      uint8_t* ds = dm + align_up(m * 32, LINE);
       H2D(B, dp, j.a + base * 65, m * 65, 65);
       H2D(B, dl, j.b + base, m, 1);
       H2D(B, dm, j.c + base * 32, m * 32, 32);

@@ -41,8 +41,11 @@ enum KnobId : int {
   KNOB_GATE,              // 1: single-chunk host-buffer calls on the mid-size kernels launch first and copy
                           //   their inputs while the launch is in flight (hostpath.hip Gate; the latency
                           //   kernels run ungated)
-  KNOB_GATE_STEP,         //   mid-size workgroups per gate piece (the host opens the inputs piece by piece;
-                          //   0: one piece)
+  KNOB_GATE_STEP,         //   mid-size workgroups per gate piece (8: the host opens the inputs piece by piece
+                          //   and each workgroup waits for its own; 0: one piece). C1 0.413-0.415 ->
+                          //   0.399-0.400 ms (profiles/r05/gate_step_hostgens_gm_r05_h.txt)
+  KNOB_HOST_GENS,         // host-buffer chunks on the lane-serial kernel: resident generations per launch
+                          //   (0: the device's EGES_GRID_MULT; fewer generations, more signatures per thread)
   KNOB_COUNT
 };
 

@@ -67,7 +67,7 @@ void bind_sender_rows(RecoverParams& p, const uint8_t* h, const uint8_t* r, cons
   p.snd_chain_id = chain_id;
 }
 
-hipError_t launch_recover_pass(Dev& d, const Route& rt, const RecoverParams& p0, hipStream_t st) {
+hipError_t launch_recover_pass(Dev& d, const Route& rt, const RecoverParams& p0, hipStream_t st, int gens) {
   RecoverParams p = with_diag(d, p0, rt);
   // the split form (four waves per signature) while the batch leaves SIMDs idle, then the
   // three-wave form, then the narrow form (k_recover_lat.hip FORM_*)
@@ -91,7 +91,8 @@ hipError_t launch_recover_pass(Dev& d, const Route& rt, const RecoverParams& p0,
 #endif
   if (mid) return launch_recover_mid(p, mid_bucket(d, rt, p.n), dev_ws_bytes(d), st);
   if (p.n <= rt.lat_max || p.raw_sig) return launch_recover_lat(p, st);
-  return launch_recover(p, d.mb_recover, d.ws_blocks, st);
+  const int mb = gens > 0 ? std::max(1, d.mb_recover / d.gm * gens) : d.mb_recover;
+  return launch_recover(p, mb, d.ws_blocks, st);
 }
 
 // ------------------------------------------------------------------ device-side pipelines

@@ -15,6 +15,13 @@ for i in 1 2 3; do
     python -c "import json; a=json.load(open('$O/c1_step${st}_$i.json')); print('c1 step=$st', a['ms_per_batch'], a['p99_ms'], a['roofline']['kernel_ms'], a['config']['correct'])"
   done
 done
+for i in 1 2; do
+  for v in 8_0 4_1 4_0 2_1; do
+    IFS=_ read pt gs <<< "$v"
+    EGES_HOST_PARTS=$pt EGES_HOST_GENS=$gs timeout -k 10 120 python bench.py --config c2host --steps 8 --warmup 2 > $O/c2host_${v}_$i.json 2> $O/c2host_${v}_$i.err
+    python -c "import json; a=json.load(open('$O/c2host_${v}_$i.json')); print('c2host parts_gens=$v', a['value'], a['ms_per_step'], a['config']['correct'])"
+  done
+done
 run() {  # name env...
   local name=$1; shift
   env "$@" timeout -k 10 120 python bench.py --steps 10 --warmup 2 --no-secondary --no-cpu-baseline --c4-total 0 > $O/$name.json 2> $O/$name.err
