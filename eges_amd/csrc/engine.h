@@ -266,6 +266,8 @@ hipError_t launch_recover_pass(Dev& d, const Route& rt, const RecoverParams& p0,
 // wire-format rows after the recovery records (tx_rows_kernel's decode)
 inline size_t tx_rows_bytes(size_t m) { return align_up(m * (4 * 32 + 1), 256); }
 bool wire_fused(const Dev& d, const Route& rt, size_t m, const uint8_t* raw);
+// the device's second compute stream and workspace (overlapped launches), created on first use
+int ensure_aux(Dev& d);
 // device-resident pipelines: all pointers device pointers, d.mu held by the caller
 int run_recover_dev(Dev& d, const Route& rt, const uint8_t* msg, const uint8_t* sig, size_t n, uint8_t* pub,
                     uint8_t* addr, uint8_t* status, hipStream_t st);
