@@ -158,7 +158,7 @@ struct Route {
   long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, gate = 1, gate_step = 8;
   size_t host_parts = EGES_PIPE_PARTS;
   uint32_t force_redo = 0, skip_flag = 0, delay_x = 0;
-  int host_gens = 0;
+  int host_gens = 0, verify_mid_gens = 1;
   static Route now() {
     Route r;
     r.lat_max = (size_t)std::max<long long>(0, knob(KNOB_LAT_MAX));
@@ -171,6 +171,7 @@ struct Route {
     r.gate = knob(KNOB_GATE);
     r.gate_step = std::max<long long>(0, std::min<long long>(knob(KNOB_GATE_STEP), 1 << 20));
     r.host_gens = (int)std::max<long long>(0, std::min<long long>(knob(KNOB_HOST_GENS), 8));
+    r.verify_mid_gens = (int)std::max<long long>(0, std::min<long long>(knob(KNOB_VERIFY_MID_GENS), 64));
     r.tri_max = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_LAT_TRI_MAX), 1u << 30));
     r.host_parts = (size_t)std::max<long long>(2, std::min<long long>(knob(KNOB_HOST_PARTS), 64));
     r.force_redo = knob(KNOB_FORCE_REDO) != 0 ? 1u : 0u;

@@ -48,6 +48,9 @@ enum KnobId : int {
                           //   0.399-0.400 ms (profiles/r05/gate_step_hostgens_gm_r05_h.txt)
   KNOB_HOST_GENS,         // host-buffer chunks on the lane-serial kernel: resident generations per launch
                           //   (0: the device's EGES_GRID_MULT; fewer generations, more signatures per thread)
+  KNOB_VERIFY_MID_GENS,   // VerifySignature batches above LAT_MAX take the bucket form's verify mode while
+                          //   its grid is at most this many generations of one workgroup per CU (2: 20k-32k
+                          //   items 0.78 -> 0.66-0.67 ms; profiles/r05/formcurve_verify_gens_r05_m.jsonl)
   KNOB_COUNT
 };
 

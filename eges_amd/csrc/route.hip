@@ -36,11 +36,12 @@ bool use_mid(const Dev& d, const Route& rt, size_t n) {
   if (n <= rt.lat_max || n > rt.mid_max) return false;
   return mid_bucket(d, rt, n) || (n + 63) / 64 * mid_ws_bytes_per_block() <= dev_ws_bytes(d);
 }
-// VerifySignature batches above LAT_MAX that the bucket form's verify mode takes (one generation of
-// workgroups: n <= 64 x CUs), instead of the lane-serial verify kernel's fixed chain
+// VerifySignature batches above LAT_MAX that the bucket form's verify mode takes (EGES_VERIFY_MID_GENS
+// generations of workgroups: n <= 64 x CUs x gens), instead of the lane-serial verify kernel's fixed
+// chain (one generation 0.35 ms, two 0.66 ms, the lane-serial kernel 0.78-0.82 ms up to 65k items)
 bool verify_mid(const Dev& d, const Route& rt, size_t n) {
   return rt.mid_form != 0 && n > rt.lat_max && n <= rt.mid_max &&
-         (n + MID_SIGS_PER_BLOCK - 1) / MID_SIGS_PER_BLOCK <= (size_t)d.cus;
+         (n + MID_SIGS_PER_BLOCK - 1) / MID_SIGS_PER_BLOCK <= (size_t)d.cus * (size_t)rt.verify_mid_gens;
 }
 hipError_t launch_verify_any(Dev& d, const Route& rt, const VerifyParams& p, bool small, hipStream_t st) {
   if (small || p.n <= rt.lat_max) return launch_verify_lat(p, p.n <= rt.wide_max, st);

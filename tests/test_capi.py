@@ -86,8 +86,8 @@ def test_knobs_set_and_read_without_gpu():
     # the defaults DESIGN.md documents (measured choices: the resident single-call server and the
     # input gate on); round 5 removed the measured-slower pinned pipeline, second host stream and
     # resident block server, so their names are unknown now
-    defaults = {"EGES_RESIDENT": 1, "EGES_GATE": 1, "EGES_GATE_STEP": 8, "EGES_HOST_PARTS": 8, "EGES_LAT_TRI_MAX": 448,
-                "EGES_SENDER_FUSED": 1}
+    defaults = {"EGES_RESIDENT": 1, "EGES_GATE": 1, "EGES_GATE_STEP": 8, "EGES_VERIFY_MID_GENS": 2, "EGES_HOST_PARTS": 8,
+                "EGES_LAT_TRI_MAX": 448, "EGES_SENDER_FUSED": 1}
     for name, want in defaults.items():
         assert eges_amd.get_knob(name) == want, name
     for name in ("EGES_RESIDENT_WGS", "EGES_RESIDENT_CAP", "EGES_RESIDENT_IDLE_MS", "EGES_TEST_DELAY_X",

@@ -88,3 +88,26 @@ def test_verify_bucket_synthetic_mix(engine):
         ok_l = engine.verify_batch(pub_h, publen, msg_h, sig_h)
     assert np.array_equal(ok_b, ok_l)
     assert ok_b.sum() > n * 8 // 10 and ok_b[::10].sum() == 0
+
+
+def test_verify_bucket_two_generations(engine):
+    """EGES_VERIFY_MID_GENS = 2 routes a batch of up to 2 x 64 x CUs items to the bucket form (two
+    generations of workgroups) instead of the lane-serial kernel: with the forced redo only the
+    mid-size kernel bumps mid_redo, so the counters show which form ran; the golden set tiled past
+    one generation (ragged last workgroup) equals the fixtures under both routings"""
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    g = load_golden("verify.npz")
+    n = 64 * cus + 64 * (cus // 2) + 37  # 1.5 generations
+    rep = -(-n // len(g["pub"]))
+    cols = {k: np.ascontiguousarray(np.concatenate([g[k]] * rep)[:n]) for k in ("pub", "publen", "msg", "sig", "ok")}
+    dev = {k: torch.from_numpy(cols[k]).cuda() for k in ("pub", "publen", "msg", "sig")}
+    for gens, form in ((2, "mid_redo"), (1, "ls_redo")):
+        engine.diag_counters(reset=True)
+        with knobs(engine, {"EGES_VERIFY_MID_GENS": gens, "EGES_TEST_FORCE_REDO": 1}):
+            ok = engine.verify_batch_dev(dev["pub"], dev["publen"], dev["msg"], dev["sig"])
+            torch.cuda.synchronize()
+        d = engine.diag_counters(reset=True)
+        assert np.array_equal(ok.cpu().numpy(), cols["ok"]), gens
+        assert d[form] > 0, (gens, d)
+        assert d["mid_redo" if form == "ls_redo" else "ls_redo"] == 0, (gens, d)

@@ -20,6 +20,7 @@ sys.path.insert(0, ROOT)
 
 FORMS = {
     "auto": {},
+    "auto2": {"EGES_VERIFY_MID_GENS": 2},  # the bucket form for up to two generations of workgroups
     "lat": {"EGES_LAT_MAX": 1 << 20},
     "bucket": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2},
     "lane": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 0},
@@ -50,7 +51,10 @@ def main():
     stream = torch.cuda.Stream()
     out = []
     for n in sizes:
+        only = os.environ.get("FORMCURVE_FORMS")
         for form, kv in FORMS.items():
+            if only and form not in only.split(","):
+                continue
             if form == "lat" and n > lat_cap:
                 continue
             old = {k: eges_amd.get_knob(k) for k in kv}
