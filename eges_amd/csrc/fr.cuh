@@ -93,7 +93,15 @@ DEV fr fr_neg(fr a) { return fr_sub<M>(fr_zero(), a); }
 DEV fr fr_mul_small(fr a, uint32_t k) { return fr{a.v * k}; }
 DEV fr fr_select(bool c, fr a, fr b) { return fr{c ? a.v : b.v}; }
 
-// One parallel carry round: limbs < 2^32 -> magnitude 1 (limb 0 <= 2^29 + 2^18).
+// EGES_FR_LEAN (default 1): the row-form carry chains with fewer dependent steps (round 5; a lone
+// wave waits on each dependent instruction's latency). 0: the round-4 code, kept
+// for same-box A/Bs. Same field values either way (a lane-level model of both reductions, checked
+// on worst-case and random magnitudes, and the GPU field tests).
+#ifndef EGES_FR_LEAN
+#define EGES_FR_LEAN 1
+#endif
+// One parallel carry round: limbs < 2^32 -> magnitude 1 (limb 0 <= 2^29 + 2^18). (A four-step form
+// that keeps limb 8's carry out of lane 9 instead of masking at the end measured no faster.)
 DEV fr fr_normalize_weak(fr a) {
   const uint32_t c = a.v >> 29;
   const uint32_t e8 = bcast<8>(c);
@@ -111,6 +119,71 @@ DEV void mac(uint64_t& acc, uint32_t a, uint32_t b) {
 }
 }  // namespace frdetail
 
+#if EGES_FR_LEAN
+// Shorter dependent chains (the same values as the EGES_FR_LEAN=0 code below): carry rounds 1
+// and 2 replaced by one split of every column into 29 + 29 + 6 bits added into its own and the
+// next two lanes (one level of independent shifts and masks, then one three-way add) before the
+// fold and carry round 3; column 16's product takes its carries as the addend; the three MAD
+// chains start from an inline 0 (no zeroed accumulators). Same-box A/Bs, profiles/r05/fr_*:
+// C3 kernel 0.1683-0.1703 -> 0.1610-0.1622 ms, single recover p50 0.1124-0.1143 -> 0.108-0.110 ms.
+DEV void fr_cols(uint64_t& col, uint32_t& a8, uint32_t& b8, fr a, fr b) {
+  uint64_t c1, c2;
+  col = mad64(bcast<0>(a.v), b.v, col);
+  c1 = mad64(bcast<1>(a.v), shr<1>(b.v), 0);
+  c2 = mad64(bcast<2>(a.v), shr<2>(b.v), 0);
+  asm volatile("" : "+v"(c1), "+v"(c2));
+  frdetail::mac<3>(col, a.v, b.v);
+  frdetail::mac<4>(c1, a.v, b.v);
+  frdetail::mac<5>(c2, a.v, b.v);
+  frdetail::mac<6>(col, a.v, b.v);
+  frdetail::mac<7>(c1, a.v, b.v);
+  a8 = bcast<8>(a.v);
+  b8 = bcast<8>(b.v);
+  c2 = mad64(a8, shr<8>(b.v), c2);
+  asm volatile("" : "+v"(c1), "+v"(c2));
+  col += c1 + c2;
+}
+// columns (lane L = column L, < 2^63.9) + a_8 b_8 (column 16) -> reduced row element, magnitude 1
+// (limbs < 2^29 + 2^26, limb 0 < 2^29)
+DEV fr fr_reduce(uint64_t col, uint32_t a8, uint32_t b8) {
+  const uint32_t L = row_lane();
+  const uint32_t lo = (uint32_t)col, hi = (uint32_t)(col >> 32);
+  const uint32_t p0 = lo & M29;
+  const uint32_t p1 = __builtin_amdgcn_alignbit(hi, lo, 29) & M29;
+  const uint32_t p2 = hi >> 26;  // col >> 58, < 2^6
+  // n_L = p0_L + p1_(L-1) + p2_(L-2) < 2^30.01; column 16 = a8 b8 + p1_15 + p2_14, column 17 gets p2_15
+  const uint32_t n = p0 + shr<1>(p1) + shr<2>(p2);
+  const uint32_t s16 = p1 + shr<1>(p2);
+  const uint64_t T = mad64(a8, b8, (uint64_t)bcast<15>(s16));  // < 2^60.8
+  const uint32_t t16 = (uint32_t)T & M29, t17 = (uint32_t)(T >> 29) + bcast<15>(p2);  // t17 < 2^32
+  // fold columns 9..17 into 0..8 as the EGES_FR_LEAN=0 reduction (a fold with the tail's terms
+  // summed first and no lane selects measured no better: the tail path then sets the pace)
+  uint32_t X = shl<9>(n);
+  X = L == 7 ? t16 : X;
+  uint32_t Y = shl<8>(n);
+  Y = L == 0 ? 0u : Y;
+  Y = L == 8 ? t16 : Y;
+  const uint32_t c17 = lane_pick(L, 0, FOLD0 * 256u, 1, 65536u) + (L == 8 ? FOLD0 : 0u);
+  const uint64_t R = mad64(Y, opaque_u32(256u), mad64(X, FOLD0, mad64(c17, t17, (uint64_t)n)));  // < 2^55.01
+  // carry round 3, limb 8's carry (< 2^18.01) folded into lanes 0 and 1
+  const uint32_t e = (uint32_t)(R >> 29);  // < 2^26.01
+  const uint64_t z = mad64(bcast<8>(e), cfold(), (uint64_t)((uint32_t)R & M29));  // < 2^33.01
+  const uint32_t zc = (uint32_t)(z >> 29);
+  return fr{low9(((uint32_t)z & M29) + shr<1>(e + zc))};
+}
+DEV fr fr_mul_col(fr a, fr b, uint64_t col) {
+  uint32_t a8, b8;
+  fr_cols(col, a8, b8, a, b);
+  return fr_reduce(col, a8, b8);
+}
+DEV fr fr_mul(fr a, fr b) { return fr_mul_col(a, b, 0); }
+DEV fr fr_sqr(fr a) { return fr_mul(a, a); }
+template <int M, int SH = 0>
+DEV fr fr_mul_sub(fr a, fr b, fr c) {
+  static_assert(M >= 1 && M <= 3 && SH >= 0 && SH <= 3, "fr_mul_sub");
+  return fr_mul_col(a, b, (uint64_t)(kconst<M>() - c.v) << SH);
+}
+#else
 // columns 0..15 of a * b (lane L = column L) on top of `col`; tail = column 16 = a_8 b_8.
 // Three independent MAD chains (the asm barriers keep the compiler from re-associating them
 // into one 9-deep dependent chain: at one wave per SIMD the kernel is latency-bound).
@@ -186,6 +259,7 @@ DEV fr fr_mul_sub(fr a, fr b, fr c) {
   fr_cols(col, tail, a, b);
   return fr_reduce(col, tail);
 }
+#endif
 template <int M, int SH = 0>
 DEV fr fr_sqr_sub(fr a, fr c) { return fr_mul_sub<M, SH>(a, a, c); }
 
