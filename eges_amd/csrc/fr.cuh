@@ -165,11 +165,14 @@ DEV fr fr_reduce(uint64_t col, uint32_t a8, uint32_t b8) {
   Y = L == 8 ? t16 : Y;
   const uint32_t c17 = lane_pick(L, 0, FOLD0 * 256u, 1, 65536u) + (L == 8 ? FOLD0 : 0u);
   const uint64_t R = mad64(Y, opaque_u32(256u), mad64(X, FOLD0, mad64(c17, t17, (uint64_t)n)));  // < 2^55.01
-  // carry round 3, limb 8's carry (< 2^18.01) folded into lanes 0 and 1
+  // carry round 3, limb 8's carry (< 2^18.01) folded into lanes 0 and 1. Lanes 9..15 hold the
+  // folded columns' leftovers: masked out of r and of the carries that move up (no final mask)
   const uint32_t e = (uint32_t)(R >> 29);  // < 2^26.01
-  const uint64_t z = mad64(bcast<8>(e), cfold(), (uint64_t)((uint32_t)R & M29));  // < 2^33.01
-  const uint32_t zc = (uint32_t)(z >> 29);
-  return fr{low9(((uint32_t)z & M29) + shr<1>(e + zc))};
+  const uint32_t r = (uint32_t)R & (L <= 8 ? M29 : 0u);
+  const uint32_t e7 = L <= 7 ? e : 0u;  // (limb 8's carry goes to lanes 0 and 1 instead)
+  const uint64_t z = mad64(bcast<8>(e), cfold(), (uint64_t)r);  // < 2^33.01
+  const uint32_t zc = (uint32_t)(z >> 29);  // 0 outside lanes 0, 1
+  return fr{((uint32_t)z & M29) + shr<1>(e7 + zc)};
 }
 DEV fr fr_mul_col(fr a, fr b, uint64_t col) {
   uint32_t a8, b8;
