@@ -10,7 +10,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # EGES_LIB: another build of the library in this directory (same-box A/B runs); default libeges.so
 LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ.get("EGES_LIB", "libeges.so")))
-# Same-box A/B tooling only (tools/gpu_*.sh): another build of the same sources, e.g. with one
+# Same-box A/B tooling only (tools/passes/gpu_*.sh): another build of the same sources, e.g. with one
 # optimisation compiled out, in place of the product library.
 if os.environ.get("EGES_AB_LIB"):
     LIB_PATH = os.path.abspath(os.environ["EGES_AB_LIB"])

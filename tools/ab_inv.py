@@ -1,4 +1,4 @@
-"""Same-box A/B of the row-form inversion latency (tools/gpu_r04_c.sh): the product selftest
+"""Same-box A/B of the row-form inversion latency (tools/passes/gpu_r04_c.sh): the product selftest
 library (scalar-ALU divsteps in assembly, EGES_DIVSTEPS_ASM=1) against tools/abbase's build of
 the compiled C loop (EGES_DIVSTEPS_ASM=0), alternating; mean s_memtime cycles per inversion at
 one wave per CU. Prints one JSON line."""

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Whole-call and kernel time by batch size for each recover form (latency / mid-size /
-lane-serial), selected with engine knobs in one process (tools/gpu_formcurve.sh).
+lane-serial), selected with engine knobs in one process (tools/passes/gpu_formcurve.sh).
 
   whole  C1-shaped wire-format transfers through eges_sender_raw_batch (pageable host buffers:
          H2D + decode + sighash + recovery + D2H), median of REPS calls

@@ -1,5 +1,5 @@
 """Host copy cost of a C1-sized wire batch into pinned memory (single-threaded memmove, as the
-engine's pinned staging does), median of 50 (tools/gpu_c1k.sh)."""
+engine's pinned staging does), median of 50 (tools/passes/gpu_c1k.sh)."""
 import ctypes
 import time
 

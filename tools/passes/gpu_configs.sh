@@ -1,4 +1,4 @@
-# All bench configs on one GPU (run via gpurun after tools/gpu_check.sh).
+# All bench configs on one GPU (run via gpurun after tools/passes/gpu_check.sh).
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp

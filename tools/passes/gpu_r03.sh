@@ -1,5 +1,5 @@
 # Round-3 GPU pass: parity tests, the default bench line (c2 + secondary), optional extra configs.
-# Usage (via gpurun, from the repo root): bash tools/gpu_r03.sh TAG [extra bench configs...]
+# Usage (via gpurun, from the repo root): bash tools/passes/gpu_r03.sh TAG [extra bench configs...]
 set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp

@@ -12,7 +12,7 @@ cat gpurun_out/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline > gpurun_out/prof.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python bench.py --config c3 --no-cpu-baseline > gpurun_out/prof_c3.log 2>&1
 bash tools/pmc.sh
-bash tools/gpu_configs.sh
+bash tools/passes/gpu_configs.sh
 timeout -k 10 200 python bench.py --config c3raw > gpurun_out/bench_c3raw.json 2> gpurun_out/bench_c3raw.err
 timeout -k 10 200 python bench.py --config c1 > gpurun_out/bench_c1.json 2> gpurun_out/bench_c1.err
 timeout -k 10 200 tools/single_bench 8 2000 > gpurun_out/single.json 2> gpurun_out/single.err

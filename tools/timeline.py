@@ -1,5 +1,5 @@
 """GPU timeline of host-buffer calls from a rocprofv3 --kernel-trace --memory-copy-trace run
-(tools/gpu_r05_i.sh): the recover_kernel launches and the copies between them, grouped into calls
+(tools/passes/gpu_r05_i.sh): the recover_kernel launches and the copies between them, grouped into calls
 (a gap of more than 1 ms between GPU operations starts a new call). Prints per call: its span from
 the first copy to the last, the kernels' summed time, the idle time between kernels, and the copy
 time not hidden behind a kernel (before the first and after the last)."""
