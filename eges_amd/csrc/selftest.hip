@@ -308,6 +308,8 @@ enum : int {
   FR_INV = 9,      // fr_inv_var (row-parallel safegcd): out = a^-1
   FR_GADD = 10,    // gejq_add of lift(a, even) on Z = c and lift(b, parity of c) on Z = c^2: x of the sum
   FR_SCINV = 11,   // sc_inv_row_var (row-parallel safegcd mod n) of a < n: out = a^-1 mod n
+  FR_MULSUB_MAX = 12,  // (a + 2p') * (2b) - 8 (5c), 2p' = kconst<1> (limbs ~2^30, == 0 mod p): magnitudes
+                       // 3 x 2 with the largest preset (M = 3, SH = 3), columns near their 2^64 bound
 };
 __global__ void fr_selftest_kernel(int op, uint32_t n, const uint32_t* A, const uint32_t* B, const uint32_t* C,
                                    uint32_t* out) {
@@ -322,6 +324,12 @@ __global__ void fr_selftest_kernel(int op, uint32_t n, const uint32_t* A, const 
     case FR_MUL: r = fr_mul(a, b); break;
     case FR_SQR: r = fr_sqr(a); break;
     case FR_MULSUB: r = fr_mul_sub<1, 2>(a, b, c); break;
+    case FR_MULSUB_MAX: {
+      const fr a3 = fr{a.v + kconst<1>()}, b2 = fr_add(b, b);
+      const fr c5 = fr_add(c, fr_add(fr_add(c, c), fr_add(c, c)));
+      r = fr_mul_sub<3, 3>(a3, b2, c5);
+      break;
+    }
     case FR_SUB: r = fr_sub<1>(a, b); break;
     case FR_LAZY: {
       const fr a2 = fr_add(a, a);

@@ -14,7 +14,8 @@ from conftest import ROOT
 from test_gpu_field import P, dec, enc, samples
 
 pytestmark = pytest.mark.gpu
-FR = dict(MUL=0, SQR=1, MULSUB=2, SUB=3, LAZY=4, NORMW=5, CHAIN=6, QUAD=7, QUAD2=8, INV=9, GADD=10, SCINV=11)
+FR = dict(MUL=0, SQR=1, MULSUB=2, SUB=3, LAZY=4, NORMW=5, CHAIN=6, QUAD=7, QUAD2=8, INV=9, GADD=10, SCINV=11,
+          MULSUB_MAX=12)
 N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
 
 
@@ -44,6 +45,8 @@ def expect(op, a, b, c):
         return a * a % P
     if op == "MULSUB":
         return (a * b - 4 * c) % P
+    if op == "MULSUB_MAX":  # magnitudes 3 x 2 with the M = 3, SH = 3 preset (fr.cuh's bounds)
+        return (2 * a * b - 40 * c) % P
     if op == "SUB":
         return (a - b) % P
     if op == "LAZY":
