@@ -20,6 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 FORMS = {
+    "auto": {},  # the product routing (latency / mid-size / lane-serial by batch size)
     "lat": {"EGES_LAT_MAX": 1 << 20, "EGES_MID_MAX": 0},
     "mid": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2},
     "midw": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 0},
