@@ -34,7 +34,13 @@ bool mid_bucket(const Dev& d, const Route& rt, size_t n) {
 }
 bool use_mid(const Dev& d, const Route& rt, size_t n) {
   if (n <= rt.lat_max || n > rt.mid_max) return false;
-  return mid_bucket(d, rt, n) || (n + 63) / 64 * mid_ws_bytes_per_block() <= dev_ws_bytes(d);
+  if (mid_bucket(d, rt, n)) return true;
+  // the windowed form: in auto mode only while its grid is one generation (two workgroups per
+  // CU); a second, partial one costs more than the lane-serial kernel's one chain (36k-40k
+  // signatures 0.98 against 0.80 ms, profiles/r05/formcurve_cut_r05_zb.jsonl)
+  const size_t wgs = (n + MID_SIGS_PER_BLOCK - 1) / MID_SIGS_PER_BLOCK;
+  if (rt.mid_form == 1 && wgs > 2 * (size_t)d.cus) return false;
+  return wgs * mid_ws_bytes_per_block() <= dev_ws_bytes(d);
 }
 // VerifySignature batches above LAT_MAX that the bucket form's verify mode takes (EGES_VERIFY_MID_GENS
 // generations of workgroups: n <= 64 x CUs x gens), instead of the lane-serial verify kernel's fixed
