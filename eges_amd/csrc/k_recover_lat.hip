@@ -67,10 +67,7 @@ static_assert(SPLIT_W0 > 0 && SPLIT_W0 < RWIN, "split point");
 // the high part (bits from RBITS * SPLIT_W0 up, < 2^(130 - RBITS SPLIT_W0) with the recoding
 // carry) in signed 4-bit windows against an 8-entry table of D: half the table build of a
 // 16-entry one for a few more additions on the high waves' chain
-#ifndef EGES_HBITS
-#define EGES_HBITS 4
-#endif
-constexpr int HBITS = EGES_HBITS;
+constexpr int HBITS = 4;
 constexpr int HTAB = 1 << (HBITS - 1);
 constexpr int HWIN = (130 - RBITS * SPLIT_W0 + HBITS) / HBITS;
 // Three-wave form: windows [0, TRI_W0) of both halves on wave 0, the rest of both halves on
