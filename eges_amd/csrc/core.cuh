@@ -33,18 +33,12 @@ constexpr int WG = 256;
 constexpr int NWAVES = WG / 64;
 // R / lambda R: signed windows of RBITS bits over a GLV half (|k| < 2^129, plus one bit for
 // the recoding carry) against the per-lane table {1..2^(RBITS-1)}*R.
-#ifndef EGES_RBITS
-#define EGES_RBITS 5
-#endif
-constexpr int RBITS = EGES_RBITS;
+constexpr int RBITS = 5;
 constexpr int RWIN = (130 + RBITS - 1) / RBITS;  // 26 windows of 5 bits (33 of 4)
 constexpr int PTAB = 1 << (RBITS - 1);           // {1..16}*R per lane
 // Fixed base: u_g = lo + 2^128 hi (libsecp's split_128, ecmult_impl.h:349), signed windows of
 // GBITS bits over each 128-bit half against the tables {1..GTAB}*G and {1..GTAB}*2^128*G.
-#ifndef EGES_GBITS
-#define EGES_GBITS 20
-#endif
-constexpr int GBITS = EGES_GBITS;                 // multiple of RBITS: aligned with the R windows
+constexpr int GBITS = 20;                 // multiple of RBITS: aligned with the R windows
 constexpr int GSTEP = GBITS / RBITS;              // R windows per G window
 constexpr int GWIN = (RWIN + GSTEP - 1) / GSTEP;  // G windows
 constexpr int GTAB = 1 << (GBITS - 1);
@@ -336,17 +330,11 @@ DEV ge neg_if(const ge& p, bool neg) {  // y magnitude <= 2 afterwards
   return r;
 }
 
-#ifndef EGES_PF
-#define EGES_PF 0  // measured ±0 % (DESIGN.md §6 "tried"); kept as an A/B knob
-#endif
 struct CoreLds {
   int8_t rdig[2][RWIN][WG];    // R / lambda R digits
   gdig_t gdig[2][GWIN][WG];    // G / 2^128 G digits
   uint32_t inv_scratch[2 * NWAVES * 10];
   uint32_t zeta[FE_LIMBS][WG];  // per-lane global Z of the R table
-#if EGES_PF
-  uint4 pf[2][PT_WORDS / 4][WG];  // the next window's two R-table entries (LDS-DMA prefetch)
-#endif
 };
 
 template <int N>
@@ -425,48 +413,12 @@ struct Stamper {
   }
 };
 
-#if EGES_PF
-// LDS-DMA prefetch of one R-table entry per lane (global_load_lds_dwordx4, no VGPRs in flight):
-// part q of the entry lands at pf[q][tid], written by the lane's own wave (wave-uniform LDS base
-// + lane x 16 B), so only the wave's own vmcnt orders it. Issued after a window's additions for
-// the next window, it is in flight during the 5 doublings between them.
-DEV void pf_issue(const uint32_t* src, uint4 (*pf)[WG]) {
-  const int wave_base = threadIdx.x & ~63;
-#pragma unroll
-  for (int q = 0; q < PT_WORDS / 4; ++q)
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 4 * q),
-                                     (__attribute__((address_space(3))) void*)&pf[q][wave_base], 16, 0, 0);
-}
-DEV ge pf_read(const uint4 (*pf)[WG]) {
-  uint32_t w[PT_WORDS];
-#pragma unroll
-  for (int q = 0; q < PT_WORDS / 4; ++q) {
-    const uint4 u = pf[q][threadIdx.x];
-    w[4 * q] = u.x;
-    w[4 * q + 1] = u.y;
-    w[4 * q + 2] = u.z;
-    w[4 * q + 3] = u.w;
-  }
-  ge p;
-  pt_unpack(w, p.x, p.y);
-  return p;
-}
-DEV int rdig_entry(const CoreLds& L, int j, int w) {
-  const int d = L.rdig[j][w][threadIdx.x];
-  const int a = d < 0 ? -d : d;
-  return a > 0 ? a - 1 : 0;
-}
-#endif
 
 // Strauss-Shamir over the digits in L and the tables (per-lane R table at `base`, G / lambda G
 // in gtab): acc = sum of the window contributions on the R table's isomorphic curve.
 template <bool CHECKED>
 DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab, CoreLds& L, const Diag& dg) {
   const int tid = threadIdx.x;
-#if EGES_PF
-#pragma unroll
-  for (int j = 0; j < 2; ++j) pf_issue(base + (size_t)(rdig_entry(L, j, RWIN - 1) * WG + tid) * PT_WORDS, L.pf[j]);
-#endif
   // RWIN windows of RBITS bits (R, lambda R) interleaved with GWIN windows of GBITS bits
   // (G, 2^128 G) every GSTEP-th window.
   inf = true;
@@ -480,9 +432,6 @@ DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab
       for (int k = 0; k < RBITS; ++k) acc = gej_double(acc);
     }
     const int nadd = (w % GSTEP) == 0 ? 4 : 2;
-#if EGES_PF
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this window's prefetched entries
-#endif
 #pragma unroll 1
     for (int j = 0; j < nadd; ++j) {
       int d;
@@ -491,11 +440,7 @@ DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab
       const int a = d < 0 ? -d : d;
       const int e = a > 0 ? a - 1 : 0;
       ge p;
-#if EGES_PF
-      if (j < 2) p = pf_read(L.pf[j]);
-#else
       if (j < 2) p = load_pt(base + (size_t)(e * WG + tid) * PT_WORDS);
-#endif
       else p = load_pt(gtab + ((size_t)(j - 2) * GTAB + e) * PT_WORDS);
       if (j == 1) p.x = fe_mul(p.x, fe_const(FE_BETA));
       if (j < 2) {
@@ -508,13 +453,6 @@ DEV void strauss(gej& acc, bool& inf, const uint32_t* base, const uint32_t* gtab
         else add_step_zinv_fast(acc, inf, neg_if(p, d < 0), d != 0, z);
       }
     }
-#if EGES_PF
-    if (w > 0) {  // the next window's entries; this window's LDS reads have completed
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int j = 0; j < 2; ++j) pf_issue(base + (size_t)(rdig_entry(L, j, w - 1) * WG + tid) * PT_WORDS, L.pf[j]);
-    }
-#endif
   }
 }
 
@@ -646,7 +584,6 @@ DEV void rec_get(const RecoverParams& prm, int row, uint32_t idx, uint32_t out[8
 // as it advances (units: 1 per lift, 4 per ecmult), so lagging waves catch up and the SIMD
 // keeps two waves busy to the end. p must be wave-uniform.
 DEV void balance_prio(uint32_t done, uint32_t total) {
-#ifndef EGES_NO_PRIO
   const uint32_t q = __builtin_amdgcn_readfirstlane(total ? (4u * done) / total : 0u);
   switch (q) {
     case 0: __builtin_amdgcn_s_setprio(3); break;
@@ -654,7 +591,6 @@ DEV void balance_prio(uint32_t done, uint32_t total) {
     case 2: __builtin_amdgcn_s_setprio(1); break;
     default: __builtin_amdgcn_s_setprio(0); break;
   }
-#endif
 }
 
 

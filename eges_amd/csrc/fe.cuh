@@ -91,50 +91,27 @@ DEV void fe_to_u256(uint32_t x[8], const fe& a) {
 
 // ------------------------------------------------------------------ reduction of 17 columns
 // S[0..16]: column sums (each < 2^63.9). Returns magnitude-1 limbs (limb 2 carries < 2^15 slack).
-#ifndef EGES_FOLD
-#define EGES_FOLD 1
-#endif
 DEV fe fe_reduce_cols(uint64_t S[17]) {
   const uint32_t f8 = opaque_u32(1u << 8), f3 = opaque_u32(1u << 3);
   // Fold columns 9..16 into 0..8 with 2^261 == 2^37 + 31264 (mod p). S_k = hi 2^32 + lo:
   //   lo 2^(29k) = lo 2^(29(k-9)) (2^37 + 31264): two MADs into columns k-9, k-8;
   //   hi 2^32 2^(29k) either folds the same way (hi 8 31264 into k-8, hi 2^11 into k-7: two
   //   MADs) or moves up as 8 hi into column k+1 (one MAD) before that column is folded.
-  // EGES_FOLD 1 (default) pushes up from every column: 26 MADs, measured 6 % faster end to end
-  // than EGES_FOLD 0 (32 MADs, every hi folded down) and 2.5 % faster than EGES_FOLD 2 (push
-  // from odd columns only: 29 MADs) on the same box — the serial chain costs nothing visible.
+  // Every column pushes its hi up: 26 MADs, measured 6 % faster end to end than folding every hi
+  // down (32 MADs) and 2.5 % faster than pushing from odd columns only (29 MADs) on the same box
+  // — the serial chain costs nothing visible (both variants: profiles/r06/removed_ab_branches_r06.diff).
   // (The same push in the carry pass below, one MAD + 32-bit carry-in instead of a 64-bit
   // shift + add, measured 1 % slower; carries in two independent rounds instead of the serial
   // pass, for a single wave per SIMD, measured 12 % slower on the mid-size kernel's doubling
   // chain, r03: the chain is bound by issue, not by its dependences.)
   // Column 9 holds 8 products (< 2^63.7), so every pushed 8 hi < 2^35 keeps columns < 2^64.
-#if EGES_FOLD == 0
 #pragma unroll
-  for (int k = 16; k >= 9; --k) {
-    const uint32_t lo = (uint32_t)S[k];
-    const uint32_t hi = (uint32_t)(S[k] >> 32);
-    S[k - 9] = mad64(lo, FOLD0, S[k - 9]);
-    S[k - 8] = mad64(lo, f8, S[k - 8]);
-    S[k - 8] = mad64(hi, opaque_u32(FOLD0 << 3), S[k - 8]);
-    S[k - 7] = mad64(hi, opaque_u32(1u << 11), S[k - 7]);
-  }
-#else
-#pragma unroll
-  for (int k = 9; k <= 15; ++k) {
-    if (EGES_FOLD == 1 || (k & 1)) {  // push hi up
-      S[k + 1] = mad64((uint32_t)(S[k] >> 32), f3, S[k + 1]);
-    }
-  }
+  for (int k = 9; k <= 15; ++k) S[k + 1] = mad64((uint32_t)(S[k] >> 32), f3, S[k + 1]);  // push hi up
 #pragma unroll
   for (int k = 9; k <= 15; ++k) {
     const uint32_t lo = (uint32_t)S[k];
     S[k - 9] = mad64(lo, FOLD0, S[k - 9]);
     S[k - 8] = mad64(lo, f8, S[k - 8]);
-    if (EGES_FOLD == 2 && !(k & 1)) {  // fold hi down
-      const uint32_t hi = (uint32_t)(S[k] >> 32);
-      S[k - 8] = mad64(hi, opaque_u32(FOLD0 << 3), S[k - 8]);
-      S[k - 7] = mad64(hi, opaque_u32(1u << 11), S[k - 7]);
-    }
   }
   {
     // column 16: hi 2^32 2^(29*16) = 8 hi 2^(29*17), and
@@ -147,7 +124,6 @@ DEV fe fe_reduce_cols(uint64_t S[17]) {
     S[1] = mad64(hi, opaque_u32(1u << 19), S[1]);
     S[0] = mad64(hi, opaque_u32(FOLD0 << 11), S[0]);
   }
-#endif
   fe r;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -404,13 +380,6 @@ DEV fe fe_inv(const fe& a) {
   uint32_t x[8], y[8];
   fe_to_u256(x, fe_normalize(a));
   modinv256<ModP>(y, x);
-  return fe_from_u256(y);
-}
-// Variable-time form, for wave-uniform data only (the latency kernel).
-DEV fe fe_inv_var(const fe& a) {
-  uint32_t x[8], y[8];
-  fe_to_u256(x, fe_normalize(a));
-  modinv256_var<ModP>(y, x);
   return fe_from_u256(y);
 }
 

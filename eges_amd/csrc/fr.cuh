@@ -15,8 +15,9 @@
 // every lane does 9 MADs instead of 81. Column 16 = a_8 b_8 is the row-uniform "tail". The
 // reduction is three parallel carry rounds (DPP row_shr:1) around one fold of columns 9..17
 // into 0..8 with 2^261 == 2^37 + 31264 (mod p) (DPP row_shl:8 / :9), and a last fold of the
-// carry out of limb 8. (A lane-level Python model of this reduction, checked on weak and
-// lazy-magnitude inputs, was used to derive the bounds in the comments.) Same values as libsecp256k1's field (field_10x26_impl.h:440,769); the
+// carry out of limb 8. (The lane-level model of this product and reduction that the bounds in
+// the comments come from is tests/test_fr_model.py, checked there on the CPU against big
+// integers at worst-case and random magnitudes and every fr_mul_sub preset.) Same values as libsecp256k1's field (field_10x26_impl.h:440,769); the
 // representation is this engine's own.
 //
 // Magnitude (as fe.cuh): every limb <= m * 2^29 (limb 0 may carry up to 2^18 more). fr_mul /
@@ -93,13 +94,9 @@ DEV fr fr_neg(fr a) { return fr_sub<M>(fr_zero(), a); }
 DEV fr fr_mul_small(fr a, uint32_t k) { return fr{a.v * k}; }
 DEV fr fr_select(bool c, fr a, fr b) { return fr{c ? a.v : b.v}; }
 
-// EGES_FR_LEAN (default 1): the row-form carry chains with fewer dependent steps (round 5; a lone
-// wave waits on each dependent instruction's latency). 0: the round-4 code, kept
-// for same-box A/Bs. Same field values either way (a lane-level model of both reductions, checked
-// on worst-case and random magnitudes, and the GPU field tests).
-#ifndef EGES_FR_LEAN
-#define EGES_FR_LEAN 1
-#endif
+// The row-form carry chains have few dependent steps (round 5; a lone wave waits on each dependent
+// instruction's latency). The round-4 code (two 64-bit carry rounds before the
+// fold) is kept only as a patch, profiles/r06/removed_ab_branches_r06.diff.
 // One parallel carry round: limbs < 2^32 -> magnitude 1 (limb 0 <= 2^29 + 2^18). (A four-step form
 // that keeps limb 8's carry out of lane 9 instead of masking at the end measured no faster.)
 DEV fr fr_normalize_weak(fr a) {
@@ -119,11 +116,9 @@ DEV void mac(uint64_t& acc, uint32_t a, uint32_t b) {
 }
 }  // namespace frdetail
 
-#if EGES_FR_LEAN
-// Shorter dependent chains (the same values as the EGES_FR_LEAN=0 code below): carry rounds 1
-// and 2 replaced by one split of every column into 29 + 29 + 6 bits added into its own and the
-// next two lanes (one level of independent shifts and masks, then one three-way add) before the
-// fold and carry round 3; column 16's product takes its carries as the addend; the three MAD
+// Shorter dependent chains (the same values as the round-4 code): carry rounds 1 and 2 replaced
+// by one split of every column into 29 + 29 + 6 bits added into its own and the next two lanes
+// (one level of independent shifts and masks, then one three-way add) before the fold and carry round 3; column 16's product takes its carries as the addend; the three MAD
 // chains start from an inline 0 (no zeroed accumulators). Same-box A/Bs, profiles/r05/fr_*:
 // C3 kernel 0.1683-0.1703 -> 0.1610-0.1622 ms, single recover p50 0.1124-0.1143 -> 0.108-0.110 ms.
 DEV void fr_cols(uint64_t& col, uint32_t& a8, uint32_t& b8, fr a, fr b) {
@@ -156,7 +151,7 @@ DEV fr fr_reduce(uint64_t col, uint32_t a8, uint32_t b8) {
   const uint32_t s16 = p1 + shr<1>(p2);
   const uint64_t T = mad64(a8, b8, (uint64_t)bcast<15>(s16));  // < 2^60.8
   const uint32_t t16 = (uint32_t)T & M29, t17 = (uint32_t)(T >> 29) + bcast<15>(p2);  // t17 < 2^32
-  // fold columns 9..17 into 0..8 as the EGES_FR_LEAN=0 reduction (a fold with the tail's terms
+  // fold columns 9..17 into 0..8 as the round-4 reduction did (a fold with the tail's terms
   // summed first and no lane selects measured no better: the tail path then sets the pace)
   uint32_t X = shl<9>(n);
   X = L == 7 ? t16 : X;
@@ -186,83 +181,6 @@ DEV fr fr_mul_sub(fr a, fr b, fr c) {
   static_assert(M >= 1 && M <= 3 && SH >= 0 && SH <= 3, "fr_mul_sub");
   return fr_mul_col(a, b, (uint64_t)(kconst<M>() - c.v) << SH);
 }
-#else
-// columns 0..15 of a * b (lane L = column L) on top of `col`; tail = column 16 = a_8 b_8.
-// Three independent MAD chains (the asm barriers keep the compiler from re-associating them
-// into one 9-deep dependent chain: at one wave per SIMD the kernel is latency-bound).
-DEV void fr_cols(uint64_t& col, uint64_t& tail, fr a, fr b) {
-  uint64_t c1 = 0, c2 = 0;
-  asm volatile("" : "+v"(c1), "+v"(c2));
-  col = mad64(bcast<0>(a.v), b.v, col);
-  frdetail::mac<1>(c1, a.v, b.v);
-  frdetail::mac<2>(c2, a.v, b.v);
-  frdetail::mac<3>(col, a.v, b.v);
-  frdetail::mac<4>(c1, a.v, b.v);
-  frdetail::mac<5>(c2, a.v, b.v);
-  frdetail::mac<6>(col, a.v, b.v);
-  frdetail::mac<7>(c1, a.v, b.v);
-  const uint32_t a8 = bcast<8>(a.v);
-  c2 = mad64(a8, shr<8>(b.v), c2);
-  asm volatile("" : "+v"(c1), "+v"(c2));
-  col += c1 + c2;
-  tail = (uint64_t)a8 * bcast<8>(b.v);
-}
-
-// columns (lane L = column L, < 2^63.9) + tail (column 16) -> reduced row element, magnitude 1
-DEV fr fr_reduce(uint64_t col, uint64_t tail) {
-  const uint32_t L = row_lane();
-  // carry round 1 (64-bit carries, 35 bits)
-  const uint32_t lo = (uint32_t)col & M29;
-  const uint64_t c = col >> 29;
-  const uint32_t clo = (uint32_t)c, chi = (uint32_t)(c >> 32);
-  const uint64_t N = (uint64_t)lo + (((uint64_t)shr<1>(chi) << 32) | shr<1>(clo));
-  tail += ((uint64_t)bcast<15>(chi) << 32) | bcast<15>(clo);
-  // carry round 2 (carries < 2^6)
-  const uint32_t d = (uint32_t)(N >> 29);
-  const uint32_t m = ((uint32_t)N & M29) + shr<1>(d);
-  tail += bcast<15>(d);
-  const uint32_t t16 = (uint32_t)tail & M29, t17 = (uint32_t)(tail >> 29);  // t17 < 2^32
-  // fold columns 9..16 into 0..8: column k adds 31264 x into k-9 and 2^8 x into k-8.
-  // Column 17 (2^493 == 31264 2^232 + 2^16 2^29 + 8003584 (mod p)) folds straight into
-  // lanes 8, 1 and 0.
-  uint32_t X = shl<9>(m);  // columns 9..15 -> lanes 0..6 (lanes 8.. get 0)
-  X = L == 7 ? t16 : X;
-  uint32_t Y = shl<8>(m);  // columns 9..15 -> lanes 1..7 (lane 0 would get column 8: excluded)
-  Y = L == 0 ? 0u : Y;
-  Y = L == 8 ? t16 : Y;
-  const uint32_t c17 = lane_pick(L, 0, FOLD0 * 256u, 1, 65536u) + (L == 8 ? FOLD0 : 0u);
-  const uint64_t R = mad64(c17, t17, mad64(X, FOLD0, mad64(Y, 256u, (uint64_t)m)));  // < 2^54.6
-  // carry round 3, with limb 8's carry (a multiple of 2^261) folded into lanes 0 and 1
-  const uint32_t e = (uint32_t)(R >> 29);  // < 2^25.6 (lane 0), 2^18.8 (lane 1), 2^17.7 (lane 8)
-  const uint32_t e8 = bcast<8>(e);
-  const uint64_t z = mad64(e8, cfold(), (uint64_t)((uint32_t)R & M29));  // < 2^32.6
-  const uint32_t zc = (uint32_t)(z >> 29);
-  return fr{low9(((uint32_t)z & M29) + shr<1>(e + zc))};
-}
-
-// a * b on top of a per-lane column preset (quad steps whose rows subtract different values)
-DEV fr fr_mul_col(fr a, fr b, uint64_t col) {
-  uint64_t tail;
-  fr_cols(col, tail, a, b);
-  return fr_reduce(col, tail);
-}
-
-DEV fr fr_mul(fr a, fr b) {
-  uint64_t col = 0, tail;
-  fr_cols(col, tail, a, b);
-  return fr_reduce(col, tail);
-}
-DEV fr fr_sqr(fr a) { return fr_mul(a, a); }
-
-// a * b - 2^SH c with the subtraction preset into the columns (magnitude(c) < 2M)
-template <int M, int SH = 0>
-DEV fr fr_mul_sub(fr a, fr b, fr c) {
-  static_assert(M >= 1 && M <= 3 && SH >= 0 && SH <= 3, "fr_mul_sub");
-  uint64_t col = (uint64_t)(kconst<M>() - c.v) << SH, tail;
-  fr_cols(col, tail, a, b);
-  return fr_reduce(col, tail);
-}
-#endif
 template <int M, int SH = 0>
 DEV fr fr_sqr_sub(fr a, fr c) { return fr_mul_sub<M, SH>(a, a, c); }
 

@@ -3,10 +3,6 @@
 #include "core.cuh"
 #include "modinv_row.cuh"
 
-#ifndef EGES_LS_BATCHINV
-#define EGES_LS_BATCHINV 1  // phases B / D across the wave (sc_inv_wave / fe_inv_wave_z); 0: per thread
-#endif
-
 namespace eges {
 
 // ------------------------------------------------------------------ recover kernel
@@ -78,9 +74,9 @@ DEV void recover_body(const RecoverParams& prm, uint64_t* stamps) {
     okm |= (ok ? 1u : 0u) << k;
   }
   st->mark(0);
-  // --- phase B: one scalar inversion per thread, or (EGES_LS_BATCHINV) one per wave: the 64
-  // threads' products batched again across the lanes, inverted once by the row-form safegcd
-  sc rinv_acc = EGES_LS_BATCHINV ? sc_inv_wave(pre) : sc_inv(pre);
+  // --- phase B: one scalar inversion per wave: the 64 threads' products batched again across
+  // the lanes, inverted once by the row-form safegcd
+  sc rinv_acc = sc_inv_wave(pre);
   st->mark(1);
   // --- phase C: k = K-1 .. 0: r^-1, u1 = -z/r, u2 = s/r, Q = u2 R + u1 G, prefix products of Z
   fe zpre = fe_one();
@@ -126,8 +122,8 @@ DEV void recover_body(const RecoverParams& prm, uint64_t* stamps) {
     zz.y = zpre;
     slot_put_pt(slot, np, 7, idx, zz);
   }
-  // --- phase D: one field inversion per thread (or per wave, as phase B)
-  fe zinv_acc = EGES_LS_BATCHINV ? fe_inv_wave_z(zpre) : fe_inv(zpre);
+  // --- phase D: one field inversion per wave, as phase B
+  fe zinv_acc = fe_inv_wave_z(zpre);
   st->mark(5);
   // --- phase E: k = 0 .. K-1 (reverse of phase C's product order): affine, address, stores
 #pragma unroll 1
@@ -172,10 +168,7 @@ DEV void recover_body(const RecoverParams& prm, uint64_t* stamps) {
   }
 }
 
-#ifndef EGES_RECOVER_WAVES
-#define EGES_RECOVER_WAVES 2
-#endif
-__global__ void __launch_bounds__(WG, EGES_RECOVER_WAVES) recover_kernel(RecoverParams prm) { recover_body<NoStamp>(prm, nullptr); }
+__global__ void __launch_bounds__(WG, 2) recover_kernel(RecoverParams prm) { recover_body<NoStamp>(prm, nullptr); }
 
 #ifdef EGES_PHASE_STAMPS
 __global__ void __launch_bounds__(WG, 2) recover_kernel_stamped(RecoverParams prm, uint64_t* stamps) {

@@ -40,18 +40,10 @@ namespace eges {
 
 // One signature per workgroup of two waves (narrow form); the split form has four (LAT_WG_SPLIT).
 constexpr int LAT_WG = 128;
-#ifndef EGES_LAT_HOIST
-#define EGES_LAT_HOIST 1  // hoisted additions in the Strauss windows (strauss_win_fast); 0: plain steps
-#endif
-#ifndef EGES_LAT_DBL2
-#define EGES_LAT_DBL2 1  // doublings in pairs (frg.cuh gejq_double2: 5 quad levels per pair); 0: single
-#endif
 // k doublings of a (the unchecked chains: Strauss windows, D = 2^k R')
 DEV gejr gejq_double_n(gejr a, int k) {
-#if EGES_LAT_DBL2
 #pragma unroll 1
   for (; k >= 2; k -= 2) a = gejq_double2(a);
-#endif
 #pragma unroll 1
   for (; k > 0; --k) a = gejq_double(a);
   return a;
@@ -59,10 +51,7 @@ DEV gejr gejq_double_n(gejr a, int k) {
 constexpr int LAT_STAGE = 512;  // wire form: encodings up to this size decode out of LDS
 // Split form: windows [0, SPLIT_W0) of both GLV halves against the R' table on wave 0, windows
 // [SPLIT_W0, RWIN) against a table of D = 2^(RBITS SPLIT_W0) R' on waves 2 (R) and 3 (lambda R).
-#ifndef EGES_SPLIT_W0
-#define EGES_SPLIT_W0 15
-#endif
-constexpr int SPLIT_W0 = EGES_SPLIT_W0;
+constexpr int SPLIT_W0 = 15;
 static_assert(SPLIT_W0 > 0 && SPLIT_W0 < RWIN, "split point");
 // the high part (bits from RBITS * SPLIT_W0 up, < 2^(130 - RBITS SPLIT_W0) with the recoding
 // carry) in signed 4-bit windows against an 8-entry table of D: half the table build of a
@@ -73,10 +62,7 @@ constexpr int HWIN = (130 - RBITS * SPLIT_W0 + HBITS) / HBITS;
 // Three-wave form: windows [0, TRI_W0) of both halves on wave 0, the rest of both halves on
 // wave 2 against one table of D = 2^(RBITS TRI_W0) R' (and its beta x), so the two chains
 // (table + TRI_W0 windows / RBITS TRI_W0 doublings + D's table + TRI_HWIN windows) are about even.
-#ifndef EGES_TRI_W0
-#define EGES_TRI_W0 20
-#endif
-constexpr int TRI_W0 = EGES_TRI_W0;
+constexpr int TRI_W0 = 20;
 static_assert(TRI_W0 > 0 && TRI_W0 < RWIN, "three-wave split point");
 constexpr int TRI_HWIN = (130 - RBITS * TRI_W0 + HBITS) / HBITS;
 static_assert(TRI_HWIN <= HWIN, "the high digits fit LatLds::hdig");
@@ -459,11 +445,7 @@ DEV void strauss_win_fast(gejr& acc, bool& inf, const TabT<NT>& tab, const ColT<
 template <int BITS, int NT>
 DEV void strauss_win_exact(gejr& acc, bool& inf, const TabT<NT>& tab, const ColT<NT>& btab, const int8_t* d0,
                            const int8_t* d1, int jmask, int wlo, int whi, const Diag& dg) {
-#if EGES_LAT_HOIST
   strauss_win_fast<BITS, NT>(acc, inf, tab, btab, d0, d1, jmask, wlo, whi, dg);
-#else
-  strauss_win<false, BITS, NT>(acc, inf, tab, btab, d0, d1, jmask, wlo, whi, dg);
-#endif
   if (dg.force || __any(!inf && fr_is_zero(acc.z))) {
     diag_bump(dg, EGES_DIAG_LAT_REDO);
     strauss_win<true, BITS, NT>(acc, inf, tab, btab, d0, d1, jmask, wlo, whi, dg);
@@ -526,11 +508,7 @@ DEV void strauss_gcomb_fast(gejr& acc, bool& inf, const LatLds& S, const uint32_
 // u_g G, unchecked, with the exact redo (every digit is nonzero-checked, so a poisoned sum
 // shows as Z == 0 and not infinity)
 DEV void gcomb_exact(gejr& A, bool& ainf, const LatLds& S, const uint32_t* gcomb, const Diag& dg) {
-#if EGES_LAT_HOIST
   strauss_gcomb_fast(A, ainf, S, gcomb);
-#else
-  strauss_gcomb<false>(A, ainf, S, gcomb, dg);
-#endif
   if (dg.force || __any(!ainf && fr_is_zero(A.z))) {
     diag_bump(dg, EGES_DIAG_COMB_REDO);
     strauss_gcomb<true>(A, ainf, S, gcomb, dg);
@@ -593,9 +571,7 @@ DEV void helper_wave(LatLds& S, const uint32_t* gcomb, bool need_y, const fr& c,
                      const Diag& dg) {
   fr y = y_given;
   bool ok = true;
-#ifndef EGES_PROBE_NO_SQRT  // diagnostic probe only: the narrow form's time without the root
   if (need_y) ok = lift_y(y, c, odd);
-#endif
   S.ylift[row_lane()] = y.v;
   if (lane_id() == 0) S.yok = ok ? 1u : 0u;
   gejr A;
@@ -945,12 +921,7 @@ DEV void recover_lat_item(const RecoverParams& prm, uint32_t idx, LatLds& S, uin
   ok = ok && S.yok != 0 && !qinf && !fault;  // ge_set_xo_var failure, main_impl.h:120
   // --- affine, serialize, address
   const fr zq = fr_select(ok, Q.z, fr_one());
-#ifdef EGES_STAMP_MODINV  // diagnostic: slots 2 / 7 carry Z^-1's divsteps / update ticks instead
-  uint64_t mprof[2] = {0, 0};
-  const fr zi = fr_inv_var(zq, mprof);
-#else
   const fr zi = fr_inv_var(zq);  // row-parallel safegcd (modinv_row.cuh)
-#endif
   fr zi2, zi3;
   zi2 = fr_sqr(zi);
   fr X1, Y1;
@@ -983,15 +954,10 @@ DEV void recover_lat_item(const RecoverParams& prm, uint32_t idx, LatLds& S, uin
   }
   st->mark(6);
   if constexpr (!std::is_same<ST, NoStamp>::value) {
-#ifdef EGES_STAMP_MODINV
-    st_.acc[2] = mprof[0];
-    st_.acc[7] = mprof[1];
-#else
     // wave 1's phases in the unused slots (not part of wave 0's total); the high words carry
     // where wave 1 (slot 2) and wave 0 (slot 7) ran (hw_place)
     st_.acc[2] = S.w1t[0];
     st_.acc[7] = S.w1t[1] | ((uint64_t)hw_place() << 32);
-#endif
     if (lane_id() == 0) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) stamps[(size_t)idx * 8 + i] = st_.acc[i];

@@ -34,13 +34,7 @@ namespace eges {
 
 constexpr int MID_WG = 256;  // four waves
 constexpr int MID_L = 64;    // signatures per workgroup (one per lane)
-#ifndef EGES_MID_BATCHINV
-#define EGES_MID_BATCHINV 1  // final Z^-1 by Montgomery's trick across the wave (fe_inv_wave); 0: per lane
-#endif
-#ifndef EGES_MID_W0
-#define EGES_MID_W0 15
-#endif
-constexpr int MID_W0 = EGES_MID_W0;  // windows [0, MID_W0) on wave A, the rest on waves B / C
+constexpr int MID_W0 = 15;  // windows [0, MID_W0) on wave A, the rest on waves B / C
 constexpr int MID_HBITS = 4;
 constexpr int MID_HTAB = 1 << (MID_HBITS - 1);
 constexpr int MID_HWIN = (130 - RBITS * MID_W0 + MID_HBITS) / MID_HBITS;
@@ -409,7 +403,7 @@ DEV void recover_mid_body(const RecoverParams& prm, uint64_t* stamps) {
   // (a zero factor would zero the whole wave's batch inversion: such a lane, which the exceptional-sum
   // argument excludes, takes 1 and keeps its own wrong value to itself)
   const fe zq = fe_select(ok && !fe_is_zero(Q.z), Q.z, fe_one());
-  const fe zi = EGES_MID_BATCHINV ? fe_inv_wave(zq) : fe_inv(zq);
+  const fe zi = fe_inv_wave(zq);
   const fe zi2 = fe_sqr(zi);
   uint32_t X[8], Y[8];
   fe_to_u256(X, fe_normalize(fe_mul(Q.x, zi2)));
@@ -475,13 +469,7 @@ constexpr int BK_BITS = 3;
 // 128 bits + the recoding carry, 43 windows, 126 doublings
 constexpr int BK_WIN = (129 + BK_BITS - 1) / BK_BITS;
 constexpr int BK_NB = 1 << (BK_BITS - 1);             // buckets for |digit| = 1..4
-#ifndef EGES_BK_RING
-#define EGES_BK_RING 10
-#endif
-#ifndef EGES_BK_VARINV
-#define EGES_BK_VARINV 0  // variable-time safegcd for r^-1 and Z^-1: slower here (lanes diverge)
-#endif
-constexpr int BK_RING = EGES_BK_RING;
+constexpr int BK_RING = 10;
 constexpr int GJ_WORDS = 3 * FE_LIMBS;
 
 enum {
@@ -723,7 +711,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
     // recovery: r^-1, u2 = s / r, u1 = -z / r (main_impl.h:114-117); verification: s^-1,
     // u2 = r / s, u1 = z / s (ecdsa_impl.h:203-271)
     const sc R = sc_select(pok, VERIFY ? q.Sv : q.R, sc_one());
-    const sc rinv = EGES_BK_VARINV ? sc_inv_var(R) : sc_inv(R);
+    const sc rinv = sc_inv(R);
     const sc u2 = sc_select(pok, sc_mul(rinv, VERIFY ? q.R : q.Sv), sc_one());
     st_.mark(1);
     glv_half h1, h2;
@@ -935,7 +923,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
   if (__any(ok && fe_is_zero(Q.z))) diag_bump(dg, EGES_DIAG_MID_EXC);  // never (see above)
   st_.mark(5);
   const fe zq = fe_select(ok && !fe_is_zero(Q.z), Q.z, fe_one());  // (see recover_mid_body)
-  const fe zi = EGES_BK_VARINV ? fe_inv_var(zq) : EGES_MID_BATCHINV ? fe_inv_wave(zq) : fe_inv(zq);
+  const fe zi = fe_inv_wave(zq);
   const fe zi2 = fe_sqr(zi);
   uint32_t X[8], Y[8];
   fe_to_u256(X, fe_normalize(fe_mul(Q.x, zi2)));

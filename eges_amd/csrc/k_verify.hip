@@ -1,10 +1,6 @@
 #include "core.cuh"
 #include "modinv_row.cuh"
 
-#ifndef EGES_LS_BATCHINV
-#define EGES_LS_BATCHINV 1
-#endif
-
 namespace eges {
 
 // ------------------------------------------------------------------ verify kernels
@@ -111,8 +107,8 @@ __global__ void __launch_bounds__(WG, 2) verify_kernel(VerifyParams prm) {
     slot_put_sc(slot, np, 5, j, pre);
     okm |= (ok ? 1u : 0u) << k;
   }
-  // --- phase B: one scalar inversion per thread (or per wave: k_recover.hip EGES_LS_BATCHINV)
-  sc sinv_acc = EGES_LS_BATCHINV ? sc_inv_wave(pre) : sc_inv(pre);
+  // --- phase B: one scalar inversion per wave (as k_recover.hip phase B)
+  sc sinv_acc = sc_inv_wave(pre);
   // --- phase C: k = K-1 .. 0: s^-1, u1 = z/s, u2 = r/s, Q = u2 P + u1 G, x(Q) == r
 #pragma unroll 1
   for (int k = (int)K - 1; k >= 0; --k) {

@@ -21,10 +21,6 @@ DEV uint64_t wave_gather64(uint64_t v, int addr) {  // v of lane addr / 4
   return ((uint64_t)hi << 32) | lo;
 }
 
-#ifndef EGES_KECCAK_HALVES
-#define EGES_KECCAK_HALVES 1
-#endif
-#if EGES_KECCAK_HALVES
 // The rounds are bound by ds_bpermute issue (a form with fewer dependent steps but more gathers
 // was slower), so the state is held as 32-bit halves: lane x + 5y the low half of A[x, y], lane
 // 32 + x + 5y the high half, and every gather moves one dword. Rotations need the other half of
@@ -79,34 +75,6 @@ DEV void keccak_f1600_wave(uint64_t& a) {
   const uint32_t hi_out = wave_gather32(v, (int)(4 * ((lane & 31) + 32)));
   a = ((uint64_t)hi_out << 32) | v;
 }
-#else
-// a: this lane's state word A[x + 5y] for lanes 0..24 (other lanes: anything)
-DEV void keccak_f1600_wave(uint64_t& a) {
-  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-  const int li = lane < 25 ? (int)lane : 0;
-  const int x = li % 5, y = li / 5;
-  // byte addresses of the lanes each step reads
-  const int c1 = 4 * (x + 5 * ((y + 1) % 5)), c2 = 4 * (x + 5 * ((y + 2) % 5));
-  const int c3 = 4 * (x + 5 * ((y + 3) % 5)), c4 = 4 * (x + 5 * ((y + 4) % 5));
-  const int xm1 = 4 * ((x + 4) % 5 + 5 * y), xp1 = 4 * ((x + 1) % 5 + 5 * y), xp2 = 4 * ((x + 2) % 5 + 5 * y);
-  // pi: B[X, Y] = A'[x, y] with X = y, Y = 2x + 3y, i.e. lane X + 5Y reads lane (X + 3Y) % 5 + 5X
-  const int pis = 4 * ((x + 3 * y) % 5 + 5 * x);
-  const uint32_t rho = KECCAK_RHO[li];
-#pragma unroll 1
-  for (int round = 0; round < 24; ++round) {
-    // theta: C[x] = xor over y of A[x, y]; A ^= C[x - 1] ^ rotl(C[x + 1], 1)
-    const uint64_t c = a ^ wave_gather64(a, c1) ^ wave_gather64(a, c2) ^ wave_gather64(a, c3) ^ wave_gather64(a, c4);
-    const uint64_t cp = wave_gather64(c, xp1);
-    a ^= wave_gather64(c, xm1) ^ rotl64(cp, 1);
-    // rho (this lane's offset; 0 on lane 0), then pi
-    a = (a << rho) | (a >> ((64 - rho) & 63));
-    const uint64_t b = wave_gather64(a, pis);
-    // chi, iota
-    a = b ^ (~wave_gather64(b, xp1) & wave_gather64(b, xp2));
-    if (lane == 0) a ^= KECCAK_RC[round];
-  }
-}
-#endif
 
 // Keccak-256(X || Y)[12:32] as 5 little-endian words, X and Y canonical and wave-uniform
 // (core.cuh pub_address, computed across the lanes of the wave).

@@ -206,81 +206,4 @@ DEV void modinv256(uint32_t out[8], const uint32_t x[8]) {
   s30_to_u256(out, d);
 }
 
-// ------------------------------------------------------------------ variable time
-// Same values, variable-time divsteps (the "divsteps_n_matrix_var" form of the safegcd paper and
-// of upstream libsecp256k1's modinv32_var, MIT; restated here): runs of zero bits of g are
-// shifted out at once (count trailing zeros), and when g is odd up to min(eta + 1, remaining, 12)
-// low bits of g are cancelled in one step by adding w f, w = -g f^-1 mod 2^k (f^-1 by Newton
-// from f itself: f f == 1 mod 8, each step doubles the valid bits). eta = -delta, starting at
-// -1 (delta = 1). Batches of 30 divsteps until g == 0. Only for data that is uniform across a
-// wave (the latency kernel: one signature per wave): the loops are data-dependent branches.
-DEV int32_t divsteps_30_var(int32_t eta, uint32_t f0, uint32_t g0, trans2x2& t) {
-  uint32_t u = 1, v = 0, q = 0, r = 1;
-  uint32_t f = f0, g = g0;
-  int i = 30;
-#pragma unroll 1
-  for (;;) {
-    const int zeros = __builtin_ctz(g | (0xFFFFFFFFu << i));  // sentinel: at most i
-    g >>= zeros;
-    u <<= zeros;
-    v <<= zeros;
-    eta -= zeros;
-    i -= zeros;
-    if (i == 0) break;
-    if (eta < 0) {  // swap: f, g <- g, -f
-      eta = -eta;
-      const uint32_t tf = f, tu = u, tv = v;
-      f = g;
-      u = q;
-      v = r;
-      g = 0u - tf;
-      q = 0u - tu;
-      r = 0u - tv;
-    }
-    int limit = eta + 1 < i ? eta + 1 : i;
-    limit = limit < 12 ? limit : 12;
-    uint32_t x = f;        // f^-1 mod 2^3
-    x *= 2u - f * x;       // mod 2^6
-    x *= 2u - f * x;       // mod 2^12
-    const uint32_t m = (0xFFFFFFFFu >> (32 - limit));
-    const uint32_t w = (g * (0u - x)) & m;
-    g += f * w;
-    q += u * w;
-    r += v * w;
-  }
-  t.u = (int32_t)u;
-  t.v = (int32_t)v;
-  t.q = (int32_t)q;
-  t.r = (int32_t)r;
-  return eta;
-}
-
-template <class Mod>
-DEV void modinv256_var(uint32_t out[8], const uint32_t x[8]) {
-  s30 d, e, f, g;
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    d.v[i] = 0;
-    e.v[i] = i == 0 ? 1 : 0;
-    f.v[i] = Mod::m[i];
-  }
-  g = s30_from_u256(x);
-  int32_t eta = -1;
-  // g reaches 0 within 741 divsteps (Bernstein-Yang bound for delta = 1, 256 bits); the cap only
-  // guarantees the loop ends whatever the data
-#pragma unroll 1
-  for (int it = 0; it < 32; ++it) {
-    trans2x2 t;
-    eta = divsteps_30_var(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
-    update_de_30<Mod>(d, e, t);
-    update_fg_30(f, g, t);
-    int32_t any = 0;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) any |= g.v[i];
-    if (any == 0) break;
-  }
-  normalize_30<Mod>(d, f.v[8]);
-  s30_to_u256(out, d);
-}
-
 }  // namespace eges

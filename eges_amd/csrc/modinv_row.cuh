@@ -3,8 +3,8 @@
 // scalar ALU (wave-uniform data), and the 2x2 transition-matrix update of the four 270-bit
 // states f, g, d, e runs limb-parallel over a 16-lane row (lane L = signed radix-2^30 limb L,
 // lanes 9..15 zero), so a batch costs a few dependent VALU steps instead of a 9-limb serial
-// carry chain per state. Same algorithm and values as modinv.cuh's modinv256_var (Bernstein-Yang
-// divsteps; update_de_30's md / me correction by M^-1 mod 2^30, after upstream libsecp256k1's
+// carry chain per state. Same values as modinv.cuh's constant-time modinv256 (Bernstein-Yang
+// divsteps, variable-time here; update_de_30's md / me correction by M^-1 mod 2^30, after upstream libsecp256k1's
 // modinv32, MIT).
 //
 // Limbs are kept "almost normalised" instead of exact: after each update, two parallel carry
@@ -52,61 +52,15 @@ DEV bool s30_ge(const s30& a, const s30& b) {
   return true;
 }
 
-#ifndef EGES_DIVSTEPS_ASM
-#define EGES_DIVSTEPS_ASM 1
-#endif
-// divsteps_30_var (modinv.cuh) for wave-uniform f, g: the same steps, kept on the scalar ALU (the
-// two-sided min of the lookahead limit would otherwise become a v_min3 and a v_readfirstlane
-// round trip through the VALU in every inner iteration). C version: EGES_DIVSTEPS_ASM=0.
-DEV int32_t divsteps_30_var_c(int32_t eta, uint32_t f0, uint32_t g0, trans2x2& t) {
-  uint32_t u = 1, v = 0, q = 0, r = 1;
-  uint32_t f = f0, g = g0;
-  int i = 30;
-  // f^-1 mod 2^12 (Newton from 3 bits), recomputed only when f changes (the swaps)
-  uint32_t x = f;
-  x *= 2u - f * x;
-  x *= 2u - f * x;
-  uint32_t nx = 0u - x;
-#pragma unroll 1
-  for (;;) {
-    const int zeros = __builtin_ctz(g | (0xFFFFFFFFu << i));  // sentinel: at most i
-    g >>= zeros;
-    u <<= zeros;
-    v <<= zeros;
-    eta -= zeros;
-    i -= zeros;
-    if (i == 0) break;
-    if (eta < 0) {  // swap: f, g <- g, -f
-      eta = -eta;
-      const uint32_t tf = f, tu = u, tv = v;
-      f = g;
-      u = q;
-      v = r;
-      g = 0u - tf;
-      q = 0u - tu;
-      r = 0u - tv;
-      x = f;
-      x *= 2u - f * x;
-      x *= 2u - f * x;
-      nx = 0u - x;
-    }
-    int limit = eta + 1 < i ? eta + 1 : i;
-    asm volatile("" : "+s"(limit));  // s_min_i32, then s_min_i32 (no VALU min3)
-    limit = limit < 12 ? limit : 12;
-    const uint32_t m = (0xFFFFFFFFu >> (32 - limit));
-    const uint32_t w = (g * nx) & m;
-    g += f * w;
-    q += u * w;
-    r += v * w;
-  }
-  t.u = (int32_t)u;
-  t.v = (int32_t)v;
-  t.q = (int32_t)q;
-  t.r = (int32_t)r;
-  return eta;
-}
-
-// The same 30 divsteps as scalar-ALU assembly (one wave alone issues ~1 instruction per 6-8
+// Variable-time divsteps (the "divsteps_n_matrix_var" form of the safegcd paper and of upstream
+// libsecp256k1's modinv32_var, MIT; restated here) for wave-uniform f, g, 30 per batch: runs of
+// zero bits of g are shifted out at once (count trailing zeros), and when g is odd up to
+// min(eta + 1, remaining, 6) low bits of g are cancelled in one step by adding w f,
+// w = -g f^-1 mod 2^k. eta = -delta, starting at -1 (delta = 1). Only for data that is uniform
+// across a wave: the loops are data-dependent branches. The compiled C loop (round 3) and the
+// lane-serial form it was restated from are in profiles/r06/removed_ab_branches_r06.diff.
+//
+// As scalar-ALU assembly (one wave alone issues ~1 instruction per 6-8
 // cycles, tools/ubench_lat.hip, so the loop is priced by its instruction count):
 //  - a swap happens in ~97 % of the iterations (the eta rule), so the loop is written twice with
 //    the registers' roles exchanged (copy A: f = A, g = B, (u, v) = (uA, vA), (q, r) = (uB, vB);
@@ -208,13 +162,6 @@ DEV int32_t divsteps_30_var_asm(int32_t eta, uint32_t f0, uint32_t g0, trans2x2&
   t.r = (int32_t)vB;
   return eta;
 }
-DEV int32_t divsteps_30_var_s(int32_t eta, uint32_t f0, uint32_t g0, trans2x2& t) {
-#if EGES_DIVSTEPS_ASM
-  return divsteps_30_var_asm(eta, f0, g0, t);
-#else
-  return divsteps_30_var_c(eta, f0, g0, t);
-#endif
-}
 
 // x^-1 mod M for x in [0, M), x wave-uniform (0 maps to 0)
 // prof (diagnostic builds only): accumulates [0] divsteps ticks, [1] state-update ticks
@@ -235,7 +182,7 @@ DEV void modinv256_row_var(uint32_t out[8], const uint32_t x[8], uint64_t* prof 
   for (int it = 0; it < 26; ++it) {
     trans2x2 t;
     const uint64_t p0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-    eta = divsteps_30_var_s(eta, (uint32_t)__builtin_amdgcn_readlane(f, 0), (uint32_t)__builtin_amdgcn_readlane(g, 0), t);
+    eta = divsteps_30_var_asm(eta, (uint32_t)__builtin_amdgcn_readlane(f, 0), (uint32_t)__builtin_amdgcn_readlane(g, 0), t);
     const uint64_t p1 = prof ? __builtin_amdgcn_s_memtime() : 0;
     // update_de_30's correction, from lane 0's limbs and the top limbs' signs
     const int32_t d0 = __builtin_amdgcn_readlane(d, 0), e0 = __builtin_amdgcn_readlane(e, 0);

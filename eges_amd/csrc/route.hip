@@ -98,7 +98,9 @@ hipError_t launch_recover_pass(Dev& d, const Route& rt, const RecoverParams& p0,
 #endif
   if (mid) return launch_recover_mid(p, mid_bucket(d, rt, p.n), dev_ws_bytes(d), st);
   if (p.n <= rt.lat_max || p.raw_sig) return launch_recover_lat(p, st);
-  const int mb = gens > 0 ? std::max(1, d.mb_recover / d.gm * gens) : d.mb_recover;
+  // (EGES_HOST_GENS above the device's EGES_GRID_MULT is clamped to it: the workspace holds
+  // ws_blocks, sized for d.gm generations, and a larger grid would be refused)
+  const int mb = gens > 0 ? std::max(1, d.mb_recover / d.gm * std::min(gens, d.gm)) : d.mb_recover;
   return launch_recover(p, mb, d.ws_blocks, st);
 }
 

@@ -265,12 +265,6 @@ DEV sc sc_inv(const sc& a) {
   modinv256<ModN>(r.v, a.v);
   return r;
 }
-// Variable-time form, for wave-uniform data only (the latency kernel).
-DEV sc sc_inv_var(const sc& a) {
-  sc r;
-  modinv256_var<ModN>(r.v, a.v);
-  return r;
-}
 
 // ---------------------------------------------------------------------------------
 // GLV split: k = k1 + k2*lambda (mod n), |k1|,|k2| < 2^129, returned as sign + 160-bit

@@ -50,8 +50,9 @@ void resident_stop(Dev& d) {
   resident_halt(d, d.res);
 }
 
-// One job on the resident server of device d: fill(data, job) writes the inputs, read(data)
-// takes the outputs. Returns -1 when the server is off, busy or the group too large (the caller
+// One job on the resident server of device d: fill(data, layout) writes the inputs, read(data,
+// layout) takes the outputs, both at the offsets of the running server's own capacity (r.cap,
+// which the kernel was launched with: it changes only while no server runs), never the knob's. Returns -1 when the server is off, busy or the group too large (the caller
 // takes a lane), else an EGES status.
 uint32_t resident_cap() { return (uint32_t)std::max<long long>(1, std::min<long long>(knob(KNOB_RESIDENT_CAP), 4096)); }
 template <class Fill, class Read>
@@ -115,7 +116,8 @@ int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& re
     const int rc = launch();
     if (rc) return rc;
   }
-  fill(r.data, r.job);
+  const ResidentLayout L = resident_layout(r.cap);
+  fill(r.data, L);
   __atomic_store_n(&r.job->n, (uint32_t)n, __ATOMIC_RELAXED);
   __atomic_store_n(&r.job->kind, (uint32_t)kind, __ATOMIC_RELAXED);
   const uint32_t seq = ++r.seq;
@@ -135,7 +137,7 @@ int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& re
       return set_err(EGES_E_HIP, "resident server: job %u not served within 2 s", seq);
     }
   }
-  read(r.data);
+  read(r.data, L);
   r.last_use = std::chrono::steady_clock::now();
   return EGES_SUCCESS;
 }
@@ -144,16 +146,15 @@ void run_group(std::vector<RecoverReq*>& g) {
   const size_t n = g.size();
   if (ensure_init() == EGES_SUCCESS) {
     if (DevPtr d = first_dev()) {
-      const ResidentLayout L = resident_layout(resident_cap());
       const int rc = resident_job(
           *d, d->res, RESIDENT_RECOVER, n,
-          [&](uint8_t* D, ResidentJob*) {
+          [&](uint8_t* D, const ResidentLayout& L) {
             for (size_t i = 0; i < n; ++i) {
               std::memcpy(D + L.msg + i * 32, g[i]->msg, 32);
               std::memcpy(D + L.sig + i * 65, g[i]->sig, 65);
             }
           },
-          [&](const uint8_t* D) {
+          [&](const uint8_t* D, const ResidentLayout& L) {
             bool fault = false;
             for (size_t i = 0; i < n; ++i) fault = fault || D[L.status + i] == EGES_ENGINE_FAULT;
             const int rc2 = fault ? set_err(EGES_E_HIP, "a kernel hand-off timed out (EGES_ENGINE_FAULT items)") : EGES_SUCCESS;
@@ -190,10 +191,9 @@ void run_group(std::vector<VerifyReq*>& g) {
   const size_t n = g.size();
   if (ensure_init() == EGES_SUCCESS) {
     if (DevPtr d = first_dev()) {
-      const ResidentLayout L = resident_layout(resident_cap());
       const int rc = resident_job(
           *d, d->res, RESIDENT_VERIFY, n,
-          [&](uint8_t* D, ResidentJob*) {
+          [&](uint8_t* D, const ResidentLayout& L) {
             *reinterpret_cast<uint32_t*>(D + L.vfault) = 0u;
             for (size_t i = 0; i < n; ++i) {
               std::memset(D + L.vpub + i * 65, 0, 65);
@@ -203,7 +203,7 @@ void run_group(std::vector<VerifyReq*>& g) {
               std::memcpy(D + L.vsig + i * 64, g[i]->sig, 64);
             }
           },
-          [&](const uint8_t* D) {
+          [&](const uint8_t* D, const ResidentLayout& L) {
             const bool fault = *reinterpret_cast<const volatile uint32_t*>(D + L.vfault) != 0u;
             const int rc2 = fault ? set_err(EGES_E_HIP, "a kernel hand-off timed out (EGES_DIAG_HANDOFF)") : EGES_SUCCESS;
             for (size_t i = 0; i < n; ++i) {

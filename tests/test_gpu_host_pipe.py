@@ -55,3 +55,17 @@ def test_chunked_path_verify_golden_tiled(engine):
         ok = engine.verify_batch(cols["pub"], cols["publen"], cols["msg"], cols["sig"])
     assert np.array_equal(ok, cols["ok"])
 
+
+
+def test_host_gens_above_grid_mult(engine):
+    """EGES_HOST_GENS larger than the device's EGES_GRID_MULT (default 2): the chunk launch's
+    grid is clamped to the generations the workspace was sized for (route.hip
+    launch_recover_pass) instead of being refused with EGES_E_HIP. Two chunks of
+    ~300k items each would ask for more blocks than ws_blocks at 8 generations."""
+    g = load_golden("recover.npz")
+    n = 600011
+    msg, sig = _tile(g["msg"], n), _tile(g["sig"], n)
+    with knobs(engine, {"EGES_HOST_PARTS": 2, "EGES_HOST_GENS": 8}):
+        pub, addr, st = engine.ecrecover_batch(msg, sig)
+    assert np.array_equal(st, _tile(g["status"], n))
+    assert np.array_equal(pub, _tile(g["pub"], n))
