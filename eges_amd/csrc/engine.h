@@ -155,9 +155,9 @@ extern std::atomic<long long> g_knob[KNOB_COUNT];
 struct Route {
   size_t lat_max = 0, mid_max = 0;
   uint32_t wide_max = 0, tri_max = 0;
-  long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, gate = 1, gate_step = 8;
+  long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, gate = 1, gate_step = 8, gate_word = 1;
   size_t host_parts = EGES_PIPE_PARTS;
-  uint32_t force_redo = 0, skip_flag = 0, delay_x = 0;
+  uint32_t force_redo = 0, skip_flag = 0, delay_x = 0, recheck = 0;
   int host_gens = 0, verify_mid_gens = 1;
   static Route now() {
     Route r;
@@ -169,12 +169,14 @@ struct Route {
     r.overlap = knob(KNOB_OVERLAP);
     r.sender_fused = knob(KNOB_SENDER_FUSED);
     r.gate = knob(KNOB_GATE);
+    r.gate_word = knob(KNOB_GATE_WORD);
     r.gate_step = std::max<long long>(0, std::min<long long>(knob(KNOB_GATE_STEP), 1 << 20));
     r.host_gens = (int)std::max<long long>(0, std::min<long long>(knob(KNOB_HOST_GENS), 8));
     r.verify_mid_gens = (int)std::max<long long>(0, std::min<long long>(knob(KNOB_VERIFY_MID_GENS), 64));
     r.tri_max = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_LAT_TRI_MAX), 1u << 30));
     r.host_parts = (size_t)std::max<long long>(2, std::min<long long>(knob(KNOB_HOST_PARTS), 64));
     r.force_redo = knob(KNOB_FORCE_REDO) != 0 ? 1u : 0u;
+    r.recheck = knob(KNOB_TEST_RECHECK) != 0 ? 1u : 0u;
     r.skip_flag = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TEST_SKIP_FLAG), 64));
     r.delay_x = (uint32_t)std::max<long long>(0, std::min<long long>(knob(KNOB_TEST_DELAY_X), 4096));
     return r;

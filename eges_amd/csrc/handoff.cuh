@@ -95,6 +95,33 @@ DEV void gate_wait(const P& prm) {
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
+// Stores into pinned host memory and a later flag: round 6 found (tools/host_one_probe2.py on round
+// 5's one-launch form, profiles/r06/host_one_probe2_r06_d.txt) that the host can see a flag word
+// before bytes the same workgroup stored earlier, although every wave waited for its stores
+// (s_waitcnt vmcnt(0)) and thread 0 released at system scope before the flag: the stale bytes were
+// whole 256-byte spans of the outputs written last, a second read microseconds later already saw
+// them, and they never appeared when the host waited 20 us after the flag or when each lane first
+// loaded back, at system scope, a dword of what it had stored. A load of an address cannot complete
+// before the store to the same address has landed, so before a workgroup counts itself done the
+// lanes that wrote outputs read back the first and the last dword of every output they stored
+// (an item's bytes touch at most two 128-byte lines): out_readback, consumed by out_settle so the
+// loads have returned before the barrier. (Streams drained by the kernel-end signal need none of
+// this: the command processor's end-of-kernel release waits for the writes' confirmation.)
+DEV uint32_t rb_sys(const uint8_t* p) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
+  return __hip_atomic_load(const_cast<uint32_t*>(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+DEV uint32_t rb_span(const uint8_t* p, size_t len) { return rb_sys(p) ^ rb_sys(p + len - 1); }
+// every output of item idx (status, address, key) that a recover kernel stored into pinned memory
+template <class P>
+DEV uint32_t out_readback(const P& prm, uint32_t idx) {
+  uint32_t acc = rb_sys(prm.status + idx);
+  if (prm.addr) acc ^= rb_span(prm.addr + (size_t)idx * prm.addr_stride, 20);
+  if (prm.pub) acc ^= rb_span(prm.pub + (size_t)idx * 65, 65);
+  return acc;
+}
+DEV void out_settle(uint32_t acc) { asm volatile("" ::"v"(acc)); }  // (the loads' values are used: they have returned)
+
 // A gated call's completion (hostpath.hip run_host_shard): after its last output each workgroup
 // counts itself done (system-scope release first); the last one stores the call's sequence into
 // gate[2], which the host polls instead of synchronising the stream (the kernel-end signal's
@@ -104,7 +131,7 @@ DEV void gate_wait(const P& prm) {
 // it saved (C3 0.184-0.188 -> 0.201-0.207 ms, profiles/r04/gate_r04_q.txt).
 template <class P>
 DEV void gate_done(const P& prm) {
-  if (!prm.gate) return;
+  if (!prm.gate || !prm.gate_word) return;
   __syncthreads();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");

@@ -200,6 +200,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     p.gate_seq = gate.seq;
     p.gate_step = pieces > 1 ? step : 0u;
     p.gate_pieces = pieces;
+    p.gate_word = rt.gate_word != 0 && nreg == 1 && !(j.kind == HostJob::SENDER_RAW && j.sighash) ? 1u : 0u;
     gopen.w = gate.w;
     gopen.seq = gate.seq;
     gopen.pieces = pieces;
@@ -434,7 +435,7 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   // stream's completion signal (handoff.cuh gate_done); later work on the stream stays ordered
   // after it, and nothing of this call reads the pinned buffer any more once the word is set
   bool done = false;
-  if (gated && nreg == 1 && !(j.kind == HostJob::SENDER_RAW && j.sighash)) {
+  if (gated && nreg == 1 && rt.gate_word != 0 && !(j.kind == HostJob::SENDER_RAW && j.sighash)) {
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t spins = 0; !(done = __atomic_load_n(&gate.w[2], __ATOMIC_ACQUIRE) == gate.seq); ++spins) {
       cpu_relax();
@@ -445,7 +446,8 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   if (!done) {
     HIPCHK(hipStreamSynchronize(sx));
     if (sx != st) HIPCHK(hipStreamSynchronize(st));  // (st's last work is already behind sx's events)
-    if (gated && __atomic_load_n(&gate.w[2], __ATOMIC_ACQUIRE) != gate.seq) {
+    if (gated && rt.gate_word != 0 && nreg == 1 && !(j.kind == HostJob::SENDER_RAW && j.sighash) &&
+        __atomic_load_n(&gate.w[2], __ATOMIC_ACQUIRE) != gate.seq) {
       (void)hipMemset(gate.dev + 1, 0, 4);  // (the workgroup count, for the next call)
       return set_err(EGES_E_HIP, "a gated launch ended without its completion word");
     }
@@ -458,6 +460,21 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
   }
   if (pinned && have_prev) unpack(prev);
   HSTAMP(5);
+  if (rt.recheck && pinned && have_prev) {  // tests: did any returned byte change after it was read?
+    HIPCHK(hipStreamSynchronize(st));
+    const uint8_t* o_pub = pin + prev.g.o_out;
+    const uint8_t* o_addr = o_pub + prev.m * 65;
+    const uint8_t* o_st = o_addr + prev.m * 32;
+    size_t changed = 0;
+    for (size_t i = 0; i < prev.m; ++i) {
+      const size_t q = prev.base + i;
+      const bool same = (!j.status || j.status[q] == o_st[i]) &&
+                        (!j.addr || std::memcmp(j.addr + q * astride, o_addr + i * astride, astride) == 0) &&
+                        (!j.pub || std::memcmp(j.pub + q * 65, o_pub + i * 65, 65) == 0);
+      changed += same ? 0 : 1;
+    }
+    if (changed) return set_err(EGES_E_HIP, "recheck: %zu items of the pinned outputs changed after the call read them", changed);
+  }
   if (j.kind == HostJob::VERIFY && __atomic_load_n(vfault, __ATOMIC_ACQUIRE) != 0u)
     return set_err(EGES_E_HIP, "a kernel hand-off timed out (items read invalid; EGES_DIAG_HANDOFF)");
   // items a kernel marked EGES_ENGINE_FAULT (a wave hand-off timed out, handoff.cuh) have no

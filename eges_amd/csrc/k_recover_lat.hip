@@ -935,7 +935,8 @@ DEV void recover_lat_item(const RecoverParams& prm, uint32_t idx, LatLds& S, uin
   pub_address_wave(a, X, Y);  // Keccak across the wave's lanes (keccak_wave.cuh)
   if (lane_id() == 0) {
     const uint32_t pre_st = (meta >> 8) & 0xffu;
-    prm.status[idx] = (uint8_t)(fault ? ST_ENGINE_FAULT : pre_st != ST_OK ? pre_st : (ok ? ST_OK : ST_RECOVER_FAILED));
+    const uint32_t stv = fault ? ST_ENGINE_FAULT : pre_st != ST_OK ? pre_st : (ok ? ST_OK : ST_RECOVER_FAILED);
+    prm.status[idx] = (uint8_t)stv;
     if (prm.addr) {
       uint32_t* dst = reinterpret_cast<uint32_t*>(prm.addr + (size_t)idx * prm.addr_stride);
 #pragma unroll
@@ -950,6 +951,15 @@ DEV void recover_lat_item(const RecoverParams& prm, uint32_t idx, LatLds& S, uin
       } else {
         for (int i = 0; i < 65; ++i) dst[i] = 0;
       }
+    }
+    if (prm.out_tag) {  // the resident server (launch.h out_tag_recover): over the bytes just stored
+      uint32_t be[16];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        be[j] = (ok && prm.pub) ? X[7 - j] : 0u;
+        be[8 + j] = (ok && prm.pub) ? Y[7 - j] : 0u;
+      }
+      prm.out_tag[idx] = out_tag_recover(prm.tag_seq, stv, (ok && prm.pub) ? 4u : 0u, be);
     }
   }
   st->mark(6);
@@ -1059,8 +1069,10 @@ DEV void verify_lat_item(const VerifyParams& prm, uint32_t idx, LatLds& S) {
     eq = fr_equal(Q.x, fr_mul(fe_to_fr(fe_from_u256(rn)), z2));
   }
   if (lane_id() == 0) {  // ok stays 0 / 1 (eges.h): a faulted item reads invalid, the fault word says why
-    prm.ok[idx] = (!fault && ok && eq) ? 1 : 0;
+    const uint32_t v = (!fault && ok && eq) ? 1u : 0u;
+    prm.ok[idx] = (uint8_t)v;
     if (fault && prm.fault) __hip_atomic_store(prm.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (prm.out_tag) prm.out_tag[idx] = out_tag_verify(prm.tag_seq, v, fault ? 1u : 0u);  // (launch.h)
   }
 }
 
@@ -1182,7 +1194,9 @@ DEV void resident_next(const ResidentParams& rp, uint32_t seen, uint64_t last, R
     __builtin_amdgcn_s_sleep(8);
   }
 }
-// thread 0: this workgroup is done with job seq; the last one publishes it
+// thread 0: this workgroup is done with job seq; the last one publishes it. (The host does not
+// rely on `done` reaching it after the outputs: each item carries a tag over its output bytes,
+// launch.h out_tag_recover / out_tag_verify, which the host checks.)
 DEV void resident_done(const ResidentParams& rp, uint32_t seq) {
   if (blockIdx.x == 0 && rp.diag) __hip_atomic_fetch_add(rp.diag + EGES_DIAG_RESIDENT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this workgroup's outputs (thread 0 wrote them), system scope
@@ -1214,12 +1228,16 @@ __global__ void __launch_bounds__(LAT_WG_SPLIT) lat_resident_kernel(ResidentPara
         p.raw_sig = rp.data + L.sig;
         p.wide = FORM_SPLIT;
         p.diag = rp.diag;
+        p.out_tag = reinterpret_cast<uint64_t*>(rp.data + L.tag);
+        p.tag_seq = seq;
         recover_lat_item<NoStamp, FORM_SPLIT>(p, idx, S, nullptr, 0u);
       } else {
         VerifyParams v{rp.data + L.vpub, rp.data + L.vpublen, rp.data + L.vmsg, rp.data + L.vsig, n,
                        rp.data + L.vok, rp.gtab, nullptr};
         v.diag = rp.diag;
         v.fault = reinterpret_cast<uint32_t*>(rp.data + L.vfault);
+        v.out_tag = reinterpret_cast<uint64_t*>(rp.data + L.tag);
+        v.tag_seq = seq;
         verify_lat_item<true>(v, idx, S);
       }
       __syncthreads();  // every wave done with this item's LDS

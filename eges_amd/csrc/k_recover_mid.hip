@@ -429,6 +429,7 @@ DEV void recover_mid_body(const RecoverParams& prm, uint64_t* stamps) {
         for (int i = 0; i < 65; ++i) dst[i] = 0;
       }
     }
+    if (prm.gate_word) out_settle(out_readback(prm, idx));  // (before gate_done's count: handoff.cuh)
   }
   st_.mark(6);
   stamp_out();
@@ -949,6 +950,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
         for (int i = 0; i < 65; ++i) dst[i] = 0;
       }
     }
+    if (prm.gate_word) out_settle(out_readback(prm, idx));  // (before gate_done's count: handoff.cuh)
   }
   st_.mark(7);
   stamp_out();

@@ -55,6 +55,9 @@ struct RecoverParams {
   // gate_step workgroups each (the word reaches gate_seq - gate_pieces + p + 1 once piece p is
   // in place); workgroup b waits for its own piece b / gate_step only. gate_step 0: one gate.
   uint32_t gate_step = 0, gate_pieces = 1;
+  // 1: the host waits for the last workgroup's completion word (handoff.cuh gate_done) instead of
+  // the stream, so the output lanes first read their outputs back at system scope (out_readback)
+  uint32_t gate_word = 0;
   // tests only (KNOB_FORCE_REDO): run every exact-redo pass as if an accumulator was poisoned
   uint32_t force_redo = 0;
   // tests only (KNOB_TEST_SKIP_FLAG, handoff.cuh): workgroup test_skip_block's producer of hand-off
@@ -82,6 +85,11 @@ struct RecoverParams {
   int wire_signer = 0;
   uint64_t wire_chain_id = 0;
   uint8_t* wire_sighash = nullptr;
+  // latency kernels (the resident server): after item idx's outputs, out_tag[idx] =
+  // out_tag_recover(tag_seq, status, pub bytes) (below), which the host checks against the bytes
+  // it reads instead of trusting the order in which they arrive
+  uint64_t* out_tag = nullptr;
+  uint32_t tag_seq = 0;
 };
 
 struct VerifyParams {
@@ -103,7 +111,33 @@ struct VerifyParams {
   // a wave hand-off of an item timed out (handoff.cuh): its ok byte is 0 and a kernel stores 1
   // here (system scope: host-buffer calls give a word of coherent pinned memory; nullable)
   uint32_t* fault = nullptr;
+  uint64_t* out_tag = nullptr;  // as RecoverParams (out_tag_verify)
+  uint32_t tag_seq = 0;
 };
+// Output tags of the resident server (single.hip resident_job). Stores into pinned host memory can
+// reach the host after a later store of the same workgroup (handoff.cuh, round 6), so the server's
+// done word does not by itself make the outputs readable: every item also gets a 64-bit tag over
+// the job's sequence and the exact output bytes, and the host accepts an item only when the tag it
+// reads matches the bytes it reads (a stale tag, stale bytes or a mix of both do not match; it
+// reads again until they do). The same function on both sides.
+__host__ __device__ inline uint64_t out_tag_mix(uint64_t h, uint32_t w) {
+  h = (h ^ w) * 0x9E3779B97F4A7C15ull;
+  return h ^ (h >> 29);
+}
+// status byte, then the 65-byte key as its first byte and 16 big-endian words
+__host__ __device__ inline uint64_t out_tag_recover(uint32_t seq, uint32_t status, uint32_t pub0, const uint32_t be[16]) {
+  uint64_t h = out_tag_mix(0x6A09E667F3BCC908ull, seq);
+  h = out_tag_mix(h, status);
+  h = out_tag_mix(h, pub0);
+  for (int j = 0; j < 16; ++j) h = out_tag_mix(h, be[j]);
+  return out_tag_mix(h, 0x52u);
+}
+__host__ __device__ inline uint64_t out_tag_verify(uint32_t seq, uint32_t ok, uint32_t fault) {
+  uint64_t h = out_tag_mix(0xBB67AE8584CAA73Bull, seq);
+  h = out_tag_mix(h, ok);
+  h = out_tag_mix(h, fault);
+  return out_tag_mix(h, 0x56u);
+}
 // Verify scratch: slot rows (P affine, prefix product of s), the order, the two counters.
 constexpr int VERIFY_SLOT_ROWS = 7;
 inline size_t verify_scratch_bytes(size_t n_pad) { return n_pad * ((size_t)VERIFY_SLOT_ROWS * 16 + 4) + 256; }
@@ -182,6 +216,7 @@ enum { RESIDENT_RECOVER = 0, RESIDENT_VERIFY = 1 };
 struct ResidentLayout {
   size_t msg, sig, pub, status;        // recover
   size_t vpub, vpublen, vmsg, vsig, vok, vfault;  // verify
+  size_t tag;                                     // cap 64-bit output tags (both kinds)
   size_t total;
 };
 __host__ __device__ inline ResidentLayout resident_layout(uint32_t cap) {
@@ -197,7 +232,9 @@ __host__ __device__ inline ResidentLayout resident_layout(uint32_t cap) {
   L.vsig = L.vmsg + c * 32;
   L.vok = L.vsig + c * 64;
   L.vfault = (L.vok + c + 3) / 4 * 4;
-  L.total = L.status + c > L.vfault + 4 ? L.status + c : L.vfault + 4;
+  const size_t end = L.status + c > L.vfault + 4 ? L.status + c : L.vfault + 4;
+  L.tag = (end + 7) / 8 * 8;
+  L.total = L.tag + c * 8;
   return L;
 }
 // bytes of ResidentParams::counter: the completion counters, then the job mirror

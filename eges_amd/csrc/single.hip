@@ -137,8 +137,51 @@ int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& re
       return set_err(EGES_E_HIP, "resident server: job %u not served within 2 s", seq);
     }
   }
-  read(r.data, L);
+  // the outputs count only once every item's tag matches the bytes read (launch.h out_tag_*: the
+  // done word can reach this thread before the outputs do); a faulted verify item says so in its tag
+  bool tag_fault = false;
+  for (uint64_t spins = 0;; ++spins) {
+    size_t bad = 0;
+    tag_fault = false;
+    for (size_t i = 0; i < n; ++i) {
+      const uint64_t t = __atomic_load_n(reinterpret_cast<const uint64_t*>(r.data + L.tag) + i, __ATOMIC_ACQUIRE);
+      if (kind == RESIDENT_RECOVER) {
+        const uint8_t* pb = r.data + L.pub + i * 65;
+        uint32_t be[16];
+        for (int w = 0; w < 16; ++w)
+          be[w] = (uint32_t)pb[1 + 4 * w] << 24 | (uint32_t)pb[2 + 4 * w] << 16 | (uint32_t)pb[3 + 4 * w] << 8 | pb[4 + 4 * w];
+        bad += t != out_tag_recover(seq, r.data[L.status + i], pb[0], be);
+      } else {
+        const uint32_t ok = r.data[L.vok + i];
+        if (t == out_tag_verify(seq, ok, 1u)) tag_fault = true;
+        else bad += t != out_tag_verify(seq, ok, 0u);
+      }
+    }
+    if (bad == 0) break;
+    if ((spins & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+      resident_halt(d, r);
+      return set_err(EGES_E_HIP, "resident server: %zu outputs of job %u never matched their tags", bad, seq);
+    }
+    cpu_relax();
+  }
+  if (tag_fault) __atomic_store_n(reinterpret_cast<uint32_t*>(r.data + L.vfault), 1u, __ATOMIC_RELAXED);
+  if (knob(KNOB_TEST_RECHECK) == 0) {
+    read(r.data, L);
+    r.last_use = std::chrono::steady_clock::now();
+    return EGES_SUCCESS;
+  }
+  // tests: the call returns what a snapshot taken at the done word holds; 200 us later the live
+  // outputs must still be the same bytes
+  std::vector<uint8_t> snap(r.data, r.data + L.total);
+  read(snap.data(), L);
   r.last_use = std::chrono::steady_clock::now();
+  const auto w0 = std::chrono::steady_clock::now();
+  while (std::chrono::steady_clock::now() - w0 < std::chrono::microseconds(200)) cpu_relax();
+  const bool rec = kind == RESIDENT_RECOVER;
+  const size_t a0 = rec ? L.pub : L.vok, a1 = rec ? L.pub + n * 65 : L.vok + n;
+  const size_t b0 = rec ? L.status : L.vfault, b1 = rec ? L.status + n : L.vfault + 4;
+  if (std::memcmp(snap.data() + a0, r.data + a0, a1 - a0) != 0 || std::memcmp(snap.data() + b0, r.data + b0, b1 - b0) != 0)
+    return set_err(EGES_E_HIP, "recheck: the resident server's outputs changed after the call read them (job %u)", seq);
   return EGES_SUCCESS;
 }
 

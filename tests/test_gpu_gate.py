@@ -108,3 +108,47 @@ def test_gate_pieces_wire_and_golden(engine, step):
                 a, s_ = engine.sender_batch(gs["sighash"][k], gs["r"][k], gs["s"][k], gs["v"][k], gs["vflags"][k], 2,
                                             930412)
                 assert np.array_equal(s_, gs["status"][k]) and np.array_equal(a, gs["addr"][k]), (form, step, rep)
+
+
+def test_gated_outputs_reread_after_drain(engine):
+    """a gated mid-size call returns its outputs from the pinned buffer as soon
+    as the last workgroup's completion word appears (handoff.cuh gate_done), not after the stream's
+    completion signal. With EGES_TEST_RECHECK the call then synchronises the stream, re-reads the
+    pinned outputs and fails if any byte differs from what it returned. C1-sized recover calls
+    (10k signatures) and C1 wire-format calls (10k transfers), two different batches alternating
+    (a byte read before its store arrived would be the other batch's), 40 calls each, every
+    returned address and status also checked against its signer."""
+    import torch
+    from eges_amd import txs
+    from eges_amd._lib import SIGNER_EIP155
+    sets = []
+    for first in (11 << 20, 23 << 20):
+        m, s, e = engine.synth_sign_dev(first, 10000, 0)
+        torch.cuda.synchronize()
+        sets.append((m.cpu().numpy(), s.cpu().numpy(), e.cpu().numpy()))
+    wires = [_c1_batch(engine, first, 10000) for first in (0, 70000)]
+    with knobs(engine, {"EGES_GATE": 1, "EGES_RESIDENT": 0, "EGES_TEST_RECHECK": 1}):
+        for rep in range(40):
+            m, s, e = sets[rep % 2]
+            _, addr, st = engine.ecrecover_batch(m, s, want_pub=False)
+            assert (st == 0).all() and np.array_equal(addr, e), rep
+            raws, exp = wires[rep % 2]
+            a, st2, _ = engine.sender_raw_batch(raws, SIGNER_EIP155, txs.GEEC_CHAIN_ID)
+            assert (st2 == 0).all() and np.array_equal(a, exp), rep
+
+
+def test_resident_outputs_reread(engine):
+    """The resident single-call server publishes each job with the same primitive (outputs, then a
+    system-scope release and the done word the host polls). With EGES_TEST_RECHECK the call returns
+    a snapshot taken at the done word and fails if the live outputs differ 200 us later: 400
+    single recoveries alternating two golden items, every one checked."""
+    from test_gpu_resident import _single_recover
+    g = load_golden("recover.npz")
+    ok = np.nonzero((g["status"] == 0) & (g["sig"][:, 64] < 4))[0][:2]
+    with knobs(engine, {"EGES_RESIDENT": 1, "EGES_TEST_RECHECK": 1}):
+        engine.diag_counters(reset=True)
+        for rep in range(400):
+            i = int(ok[rep % 2])
+            rc, pub = _single_recover(g["msg"][i], g["sig"][i])
+            assert rc == 1 and pub == g["pub"][i].tobytes(), rep
+        assert engine.diag_counters(reset=True)["resident"] >= 300
