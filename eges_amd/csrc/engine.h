@@ -76,8 +76,8 @@ int env_int(const char* name, int dflt);
 // single-chunk host calls that run on the latency kernel (which needs no shared workspace) do
 // not queue behind each other on the device mutex.
 constexpr int NLANES = 4;
-// A host-buffer call's input gate (handoff.cuh gate_wait / gate_done): word 0 the last sequence
-// opened, word 1 set by a wave whose wait ran out, word 2 the last completed sequence. Coherent
+// A host-buffer call's input gate (handoff.cuh gate_wait): word 0 the last sequence opened, word 1
+// set by a wave whose wait ran out. Coherent
 // pinned memory, one per device (the gated mid-size calls hold the device mutex).
 struct Gate {
   uint32_t* w = nullptr;
@@ -155,7 +155,7 @@ extern std::atomic<long long> g_knob[KNOB_COUNT];
 struct Route {
   size_t lat_max = 0, mid_max = 0;
   uint32_t wide_max = 0, tri_max = 0;
-  long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, gate = 1, gate_step = 8, gate_word = 1;
+  long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, gate = 1, gate_step = 8;
   size_t host_parts = EGES_PIPE_PARTS;
   uint32_t force_redo = 0, skip_flag = 0, delay_x = 0, recheck = 0;
   int host_gens = 0, verify_mid_gens = 1;
@@ -169,7 +169,6 @@ struct Route {
     r.overlap = knob(KNOB_OVERLAP);
     r.sender_fused = knob(KNOB_SENDER_FUSED);
     r.gate = knob(KNOB_GATE);
-    r.gate_word = knob(KNOB_GATE_WORD);
     r.gate_step = std::max<long long>(0, std::min<long long>(knob(KNOB_GATE_STEP), 1 << 20));
     r.host_gens = (int)std::max<long long>(0, std::min<long long>(knob(KNOB_HOST_GENS), 8));
     r.verify_mid_gens = (int)std::max<long long>(0, std::min<long long>(knob(KNOB_VERIFY_MID_GENS), 64));

@@ -95,53 +95,17 @@ DEV void gate_wait(const P& prm) {
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
-// Stores into pinned host memory and a later flag: round 6 found (tools/host_one_probe2.py on round
-// 5's one-launch form, profiles/r06/host_one_probe2_r06_d.txt) that the host can see a flag word
-// before bytes the same workgroup stored earlier, although every wave waited for its stores
-// (s_waitcnt vmcnt(0)) and thread 0 released at system scope before the flag: the stale bytes were
-// whole 256-byte spans of the outputs written last, a second read microseconds later already saw
-// them, and they never appeared when the host waited 20 us after the flag or when each lane first
-// loaded back, at system scope, a dword of what it had stored. A load of an address cannot complete
-// before the store to the same address has landed, so before a workgroup counts itself done the
-// lanes that wrote outputs read back the first and the last dword of every output they stored
-// (an item's bytes touch at most two 128-byte lines): out_readback, consumed by out_settle so the
-// loads have returned before the barrier. (Streams drained by the kernel-end signal need none of
-// this: the command processor's end-of-kernel release waits for the writes' confirmation.)
-DEV uint32_t rb_sys(const uint8_t* p) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
-  return __hip_atomic_load(const_cast<uint32_t*>(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-DEV uint32_t rb_span(const uint8_t* p, size_t len) { return rb_sys(p) ^ rb_sys(p + len - 1); }
-// every output of item idx (status, address, key) that a recover kernel stored into pinned memory
-template <class P>
-DEV uint32_t out_readback(const P& prm, uint32_t idx) {
-  uint32_t acc = rb_sys(prm.status + idx);
-  if (prm.addr) acc ^= rb_span(prm.addr + (size_t)idx * prm.addr_stride, 20);
-  if (prm.pub) acc ^= rb_span(prm.pub + (size_t)idx * 65, 65);
-  return acc;
-}
-DEV void out_settle(uint32_t acc) { asm volatile("" ::"v"(acc)); }  // (the loads' values are used: they have returned)
-
-// A gated call's completion (hostpath.hip run_host_shard): after its last output each workgroup
-// counts itself done (system-scope release first); the last one stores the call's sequence into
-// gate[2], which the host polls instead of synchronising the stream (the kernel-end signal's
-// path measured ~5 us from the kernel's end to the sync's return). At kernel level, after the
-// body: every wave of the workgroup reaches the barrier. The mid-size kernels only: on the
-// latency kernels' 1,000-workgroup grids the per-workgroup system-scope release cost more than
-// it saved (C3 0.184-0.188 -> 0.201-0.207 ms, profiles/r04/gate_r04_q.txt).
-template <class P>
-DEV void gate_done(const P& prm) {
-  if (!prm.gate || !prm.gate_word) return;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    const uint32_t c = __hip_atomic_fetch_add(prm.gate_dev + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (c == gridDim.x - 1) {
-      __hip_atomic_store(prm.gate_dev + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(const_cast<uint32_t*>(prm.gate) + 2, prm.gate_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-}
+// Outputs in pinned host memory are read by the host only after the stream's completion signal
+// (the command processor's end-of-kernel release waits for the writes' confirmation). Round 6
+// found (tools/host_one_probe2.py on round 5's one-launch form, profiles/r06/) that a flag word a
+// workgroup stores after its outputs, even after every wave's s_waitcnt vmcnt(0) and a system-scope
+// release, can reach the host before those outputs: the stale bytes were whole 256-byte spans of
+// the outputs written last, a second read microseconds later already saw them, and they never
+// appeared when the host waited 20 us after the flag or when each lane first loaded back, at system
+// scope, a dword of what it had stored. The gated calls' completion word (a flag of that kind) is
+// gone (measured slower than the stream's signal once made safe, profiles/r06/
+// removed_gate_word_r06.diff); the resident server's done word is backed by per-item output tags
+// the host checks (launch.h out_tag_recover / out_tag_verify).
 // tests only: workgroup 0's producer of flag k skips publishing it once per launch
 template <class P>
 DEV bool ho_skip(const P& prm, int k) {

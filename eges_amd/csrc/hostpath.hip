@@ -186,7 +186,6 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     ~GateOpen() { open(); }
   } gopen;
   bool defer = false;  // this chunk's inputs wait for gopen.open()
-  bool gated = false;  // a gated mid-size launch ran: its last workgroup stores the sequence into gate.w[2]
   auto arm = [&](RecoverParams& p) {  // a deferred chunk's kernels wait at the gate
     if (!defer || p.n == 0) return;
     // pieces of GATE_STEP workgroups (64 items each) when the grid has several of them
@@ -194,13 +193,11 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     const uint32_t step = rt.gate_step > 0 ? (uint32_t)rt.gate_step : wgs;
     const uint32_t pieces = (wgs + step - 1) / step;
     gate.seq += pieces;  // (wraps harmlessly: every comparison is a sequence difference)
-    gated = true;  // (a mid-size launch: its kernels store the completion word)
     p.gate = gate.w;
     p.gate_dev = gate.dev;
     p.gate_seq = gate.seq;
     p.gate_step = pieces > 1 ? step : 0u;
     p.gate_pieces = pieces;
-    p.gate_word = rt.gate_word != 0 && nreg == 1 && !(j.kind == HostJob::SENDER_RAW && j.sighash) ? 1u : 0u;
     gopen.w = gate.w;
     gopen.seq = gate.seq;
     gopen.pieces = pieces;
@@ -431,27 +428,10 @@ int run_host_shard(Dev& d, const Route& rt, const HostJob& j, size_t off, size_t
     if (rc) return rc;
   }
   if (!small) HIPCHK(hipEventRecord(d.last, sx));
-  // a gated single launch with nothing queued behind it: its completion word instead of the
-  // stream's completion signal (handoff.cuh gate_done); later work on the stream stays ordered
-  // after it, and nothing of this call reads the pinned buffer any more once the word is set
-  bool done = false;
-  if (gated && nreg == 1 && rt.gate_word != 0 && !(j.kind == HostJob::SENDER_RAW && j.sighash)) {
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint64_t spins = 0; !(done = __atomic_load_n(&gate.w[2], __ATOMIC_ACQUIRE) == gate.seq); ++spins) {
-      cpu_relax();
-      if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
-    }
-    if (done) (void)hipStreamQuery(st);  // (lets the runtime retire the launch)
-  }
-  if (!done) {
-    HIPCHK(hipStreamSynchronize(sx));
-    if (sx != st) HIPCHK(hipStreamSynchronize(st));  // (st's last work is already behind sx's events)
-    if (gated && rt.gate_word != 0 && nreg == 1 && !(j.kind == HostJob::SENDER_RAW && j.sighash) &&
-        __atomic_load_n(&gate.w[2], __ATOMIC_ACQUIRE) != gate.seq) {
-      (void)hipMemset(gate.dev + 1, 0, 4);  // (the workgroup count, for the next call)
-      return set_err(EGES_E_HIP, "a gated launch ended without its completion word");
-    }
-  }
+  // every output is read after the streams' completion signal (handoff.cuh: an in-kernel flag
+  // word can reach the host before the outputs stored ahead of it)
+  HIPCHK(hipStreamSynchronize(sx));
+  if (sx != st) HIPCHK(hipStreamSynchronize(st));  // (st's last work is already behind sx's events)
   HSTAMP(4);
   drain.armed = false;
   if (gating && __atomic_load_n(&gate.w[1], __ATOMIC_ACQUIRE) != 0u) {

@@ -429,7 +429,6 @@ DEV void recover_mid_body(const RecoverParams& prm, uint64_t* stamps) {
         for (int i = 0; i < 65; ++i) dst[i] = 0;
       }
     }
-    if (prm.gate_word) out_settle(out_readback(prm, idx));  // (before gate_done's count: handoff.cuh)
   }
   st_.mark(6);
   stamp_out();
@@ -950,7 +949,6 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
         for (int i = 0; i < 65; ++i) dst[i] = 0;
       }
     }
-    if (prm.gate_word) out_settle(out_readback(prm, idx));  // (before gate_done's count: handoff.cuh)
   }
   st_.mark(7);
   stamp_out();
@@ -958,7 +956,6 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
 
 __global__ void __launch_bounds__(MID_WG, 1) recover_bkt_kernel(RecoverParams prm) {
   recover_bkt_body<NoStamp>(prm, nullptr);
-  gate_done(prm);
 }
 
 __global__ void __launch_bounds__(MID_WG, 1) verify_bkt_kernel(RecoverParams prm) {
@@ -967,7 +964,6 @@ __global__ void __launch_bounds__(MID_WG, 1) verify_bkt_kernel(RecoverParams prm
 
 __global__ void __launch_bounds__(MID_WG, 2) recover_mid_kernel(RecoverParams prm) {
   recover_mid_body<NoStamp>(prm, nullptr);
-  gate_done(prm);
 }
 
 size_t mid_ws_bytes_per_block() { return MID_WS_WORDS * sizeof(uint32_t); }
@@ -1005,11 +1001,9 @@ hipError_t launch_recover_mid(const RecoverParams& p, bool bucket, size_t ws_byt
 #ifdef EGES_PHASE_STAMPS
 __global__ void __launch_bounds__(MID_WG, 2) recover_mid_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
   recover_mid_body<Stamper>(prm, stamps);
-  gate_done(prm);
 }
 __global__ void __launch_bounds__(MID_WG, 1) recover_bkt_kernel_stamped(RecoverParams prm, uint64_t* stamps) {
   recover_bkt_body<Stamper>(prm, stamps);
-  gate_done(prm);
 }
 hipError_t launch_recover_mid_stamped(const RecoverParams& p, bool bucket, size_t ws_bytes, hipStream_t st,
                                       uint64_t* stamps) {

@@ -51,8 +51,6 @@ enum KnobId : int {
   KNOB_VERIFY_MID_GENS,   // VerifySignature batches above LAT_MAX take the bucket form's verify mode while
                           //   its grid is at most this many generations of one workgroup per CU (2: 20k-32k
                           //   items 0.78 -> 0.66-0.67 ms; profiles/r05/formcurve_verify_gens_r05_m.jsonl)
-  KNOB_GATE_WORD,         //   1: a gated single launch returns at its last workgroup's completion word (the
-                          //   outputs read back at system scope first); 0: at the stream's completion signal
   KNOB_TEST_RECHECK,      // tests: a host-buffer call whose outputs come back through pinned memory (the
                           //   lanes, the gated mid-size launches, the resident server) re-reads them after the
                           //   work has drained (the stream, or 200 us for the resident server) and fails

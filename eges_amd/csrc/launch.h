@@ -55,9 +55,6 @@ struct RecoverParams {
   // gate_step workgroups each (the word reaches gate_seq - gate_pieces + p + 1 once piece p is
   // in place); workgroup b waits for its own piece b / gate_step only. gate_step 0: one gate.
   uint32_t gate_step = 0, gate_pieces = 1;
-  // 1: the host waits for the last workgroup's completion word (handoff.cuh gate_done) instead of
-  // the stream, so the output lanes first read their outputs back at system scope (out_readback)
-  uint32_t gate_word = 0;
   // tests only (KNOB_FORCE_REDO): run every exact-redo pass as if an accumulator was poisoned
   uint32_t force_redo = 0;
   // tests only (KNOB_TEST_SKIP_FLAG, handoff.cuh): workgroup test_skip_block's producer of hand-off

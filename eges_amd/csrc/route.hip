@@ -85,7 +85,7 @@ hipError_t launch_recover_pass(Dev& d, const Route& rt, const RecoverParams& p0,
   const bool mid = use_mid(d, rt, p.n);
   if (p.wire_raw && !(mid ? mid_bucket(d, rt, p.n) : p.n <= rt.lat_max)) return hipErrorInvalidValue;  // wire_fused() decides
   if (p.snd_r && !(mid || p.n <= rt.lat_max)) return hipErrorInvalidValue;  // sender_fused() decides
-  if (p.gate && !mid) return hipErrorInvalidValue;  // (the host waits for the mid-size kernels' completion word)
+  if (p.gate && !mid) return hipErrorInvalidValue;  // (only the mid-size kernels wait at the gate)
 #ifdef EGES_PHASE_STAMPS
   if (mid) {
     hipError_t e = stamp_buf((p.n + 63) / 64 * 4, st);  // one row per wave

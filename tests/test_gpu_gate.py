@@ -1,7 +1,7 @@
 """Host-buffer calls that launch before their inputs are copied (EGES_GATE = 1, the default:
-hostpath.hip run_host_shard GateOpen, handoff.cuh gate_wait / gate_done): the fused mid-size kernels
-(bucket, windowed) wait at the call's gate word while the host copies the inputs into the pinned
-buffer, and their last workgroup stores the completion word the host waits on. The latency forms
+hostpath.hip run_host_shard GateOpen, handoff.cuh gate_wait): the fused mid-size kernels (bucket,
+windowed) wait at the call's gate word while the host copies the inputs into the pinned buffer;
+the host reads the outputs after the stream's completion signal. The latency forms
 run ungated either way (measured slower gated). Every golden recovery and sender item through
 each form with the gate on and off, byte for byte the fixtures, and many back-to-back calls of
 changing sizes across the routes (the gate's sequence advancing per call)."""
@@ -111,10 +111,11 @@ def test_gate_pieces_wire_and_golden(engine, step):
 
 
 def test_gated_outputs_reread_after_drain(engine):
-    """a gated mid-size call returns its outputs from the pinned buffer as soon
-    as the last workgroup's completion word appears (handoff.cuh gate_done), not after the stream's
-    completion signal. With EGES_TEST_RECHECK the call then synchronises the stream, re-reads the
-    pinned outputs and fails if any byte differs from what it returned. C1-sized recover calls
+    """a gated mid-size call returns its outputs from the pinned buffer (round 5:
+    at the last workgroup's completion word, which round 6 found can reach the host before the
+    outputs stored ahead of it, handoff.cuh; now at the stream's completion signal). With
+    EGES_TEST_RECHECK the call then synchronises the stream again, re-reads the pinned outputs and
+    fails if any byte differs from what it returned. C1-sized recover calls
     (10k signatures) and C1 wire-format calls (10k transfers), two different batches alternating
     (a byte read before its store arrived would be the other batch's), 40 calls each, every
     returned address and status also checked against its signer."""
