@@ -64,6 +64,9 @@ METRIC = "secp256k1 ecrecover+address/sec at 1/8 MI355X; % of INT32 VALU peak"
 # algorithm = 80 x 3085.2 field ops + 128 x 301 scalar ops + 6,300 (Keccak-f) = 291,644.
 W_RECOVER = 291_644
 W_VERIFY65 = 242_216
+# Algorithmic HBM bytes per recovered address: 32 B msg + 65 B sig in, 20 B
+# address + 1 B status out
+ALGO_BYTES = 118
 # The roofline's `peak` / `frac`: the guide's INT32 VALU peak (MI355X_MICROARCH.md "Wave
 # scheduling": one wave64 VALU instruction per 2 cycles per SIMD), 1024 SIMDs x 32 lane-ops/clk x
 # 2.4 GHz = 7.86e13 lane-ops/s. The same achieved rate is also given against two named ceilings
@@ -90,6 +93,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="c2: skip the secondary C1 / C3 / C5 measurements")
     ap.add_argument("--stub", action="store_true", help="CPU rehearsal of the rank logic (gloo, sleep as the step)")
+    ap.add_argument("--other-process-kernels", action="store_true",
+                    help="(internal) the second process of secondary.single.resident_tax")
     ap.add_argument("--c4-total", type=int, default=None,
                     help="c2: the secondary configs[3] strong-scaled leg's total batch (default 64M; 0 skips it)")
     return ap.parse_args()
@@ -167,10 +172,18 @@ def cpu_baseline(msg_h, sig_h, target_s, gpu_addr=None):
             bad = int((addr_ref != gpu_addr[:n]).any(axis=1).sum())
             agree = {"items": n, "mismatches": bad,
                      "note": "the timed GPU steps' addresses vs the reference libsecp256k1's, item for item"}
-        return {"value": round(n / dt, 1), "unit": "sigs/s", "cores": threads, "kind": "reference",
+        rate = n / dt
+        return {"value": round(rate, 1), "unit": "sigs/s", "cores": threads, "kind": "reference",
                 "reference_check": agree, "host": dict(host, threads=threads),
                 "ratio_basis": "the GPU/CPU ratio is per granted CPU set of the host (all threads above), "
                                "not per core",
+                # per-core and whole-socket figures beside the granted-set one (VERDICT r5
+                # item 6): the measured per-thread rate, and that rate times every host thread (nproc),
+                # an extrapolation (the box grants `threads` of them)
+                "per_thread": round(rate / threads, 1),
+                "whole_host_extrapolated": {"threads": host["nproc"], "sigs_per_s": round(rate / threads * host["nproc"], 1),
+                                            "basis": "per_thread x nproc (not measured: this process may use "
+                                                     f"{threads} of the host's {host['nproc']} threads)"},
                 "sample": f"first {n} signatures of the same synthetic batch: reference libsecp256k1 ecrecover "
                           f"(cgo build flags) + Keccak address, {threads} pthreads, {dt:.1f} s"}
     o = Oracle()
@@ -355,6 +368,23 @@ def roofline(per_gpu_rate, work, batch, kern_ms, kernel="eges::recover_kernel"):
                 "waves_per_launch": pmc.get("SQ_WAVES"),
                 "valu_util_vs_guide": round(lane_insts / (kern_ms / 1e3) / PEAK_GUIDE_VALU, 4),
                 "valu_util_vs_survey_contract": round(lane_insts / (kern_ms / 1e3) / PEAK_INT32_OPS, 4)}
+            # what the waves wait on, and how much of the traffic the L2 absorbs:
+            # the share of wave-cycles spent waiting on anything (memory, LDS, dependencies) and the
+            # L2 hit rate; traffic_vs_algorithmic = fabric bytes per launch / (ALGO_BYTES x batch)
+            cn = r["counters"]
+            if pmc.get("SQ_WAIT_ANY") and pmc.get("SQ_WAVE_CYCLES"):
+                cn["wait_any_share_of_wave_cycles"] = round(pmc["SQ_WAIT_ANY"] / pmc["SQ_WAVE_CYCLES"], 4)
+            if pmc.get("SQ_WAIT_INST_ANY") and pmc.get("SQ_WAVE_CYCLES"):
+                cn["wait_inst_any_share_of_wave_cycles"] = round(pmc["SQ_WAIT_INST_ANY"] / pmc["SQ_WAVE_CYCLES"], 4)
+            hit, miss = pmc.get("TCC_HIT_sum"), pmc.get("TCC_MISS_sum")
+            if hit is not None and miss is not None and hit + miss > 0:
+                cn["l2_hit_rate"] = round(hit / (hit + miss), 4)
+            if r["traffic"]:
+                cn["traffic_vs_algorithmic"] = round(r["traffic"] / (ALGO_BYTES * batch), 1)
+            cn["bound_note"] = ("VALU issue-bound, not traffic-bound, when valu_util is near the measured "
+                                "v_mad_u64_u32 rate (frac_vs_measured_mad_rate) and the wait share is small; "
+                                "the fabric traffic is the per-lane R-table workspace and fixed-base gathers, "
+                                "mostly served by the Infinity Cache (DESIGN.md section 4)")
     return r
 
 
@@ -429,6 +459,9 @@ def run_throughput(c, strong):
             "config": {"workload": wl, "batch_per_gpu": B, "shards": shards, "total_batch": total,
                        "parallelism": f"index-sharded x{c.world}", "correct": ok},
             "roofline": roofline(per_gpu_rate, W_RECOVER, B, kern_ms), "cpu_baseline": cpu}
+    if cpu and cpu.get("kind") == "reference":
+        cpu["gpu_vs"] = {"granted_set": round(value / cpu["value"], 1), "per_thread": round(value / cpu["per_thread"], 1),
+                         "whole_host_extrapolated": round(value / cpu["whole_host_extrapolated"]["sigs_per_s"], 1)}
     sec = {"note": "measured after the timed C2 region, same processes; not part of value"}
     c4_total = C4_TOTAL if a.c4_total is None else a.c4_total
     if not strong and not a.no_secondary and c4_total > 0:
@@ -454,6 +487,7 @@ def run_throughput(c, strong):
         ref = cpu if cpu and cpu.get("kind") == "reference" else None
         sec["single"] = measure_single(ref["cores"] if ref else 16, 2000, ref["value"] if ref else None,
                                        ref_one_call_us(msg.cpu().numpy(), sig.cpu().numpy()))
+        sec["single"]["resident_tax"] = measure_resident_tax(c, msg[0].cpu().numpy(), sig[0].cpu().numpy())
         line["secondary"] = sec
         ok = ok and all(v.get("correct", True) for v in sec.values() if isinstance(v, dict))
         line["config"]["correct"] = ok
@@ -762,6 +796,89 @@ def measure_single(callers=16, calls=2000, ref_rate=None, ref_one_us=None):
         # one caller: the reference's serial per-call cost beside this seam's p50
         out["reference_one_call_us"] = ref_one_us
         out["one_caller_vs_reference"] = round(ref_one_us / (m["p50_ms_one_caller"] * 1e3), 3)
+    return out
+
+
+def other_process_kernels():
+    """--other-process-kernels: the second process of measure_resident_tax. A device-resident 1M
+    batch on device 0, timed with HIP events each time a line "go" arrives on stdin; prints one
+    number per launch (ms). Its own engine never starts a resident server."""
+    import torch
+    import eges_amd
+    eges_amd.init(1)
+    eges_amd.set_knob("EGES_RESIDENT", 0)
+    n = 1 << 20
+    msg, sig, exp = eges_amd.synth_sign_dev(5 << 30, n, 0)
+    addr = torch.empty((n, 20), dtype=torch.uint8, device=msg.device)
+    st = torch.empty((n,), dtype=torch.uint8, device=msg.device)
+    s = torch.cuda.Stream()
+    for _ in range(2):
+        eges_amd.ecrecover_batch_dev(msg, sig, addr=addr, status=st, stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    print("ready", flush=True)
+    ok = True
+    for line in sys.stdin:
+        if line.strip() != "go":
+            continue
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        eges_amd.ecrecover_batch_dev(msg, sig, addr=addr, status=st, stream=s.cuda_stream)
+        e1.record(s)
+        torch.cuda.synchronize()
+        ok = ok and bool(torch.equal(addr, exp))
+        print(f"{e0.elapsed_time(e1):.4f}", flush=True)
+    print("ok" if ok else "wrong", flush=True)
+
+
+def measure_resident_tax(c, msg1, sig1, reps=8):
+    """What the resident single-call server costs another tenant of the GPU:
+    a second process launches a device-resident 1M batch right after one single recovery of this
+    process, alternately with the server alive (EGES_RESIDENT=1: its workgroups poll for
+    EGES_RESIDENT_IDLE_MS after the call) and without it; the medians of the other process's kernel
+    time, their ratio, and how often the server was still running when the other launch was
+    requested (eges_diag_resident_running)."""
+    import numpy as np
+    from eges_amd._lib import lib
+    dev = c.dev.index if c.dev.index is not None else 0
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    try:
+        child = subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), "--other-process-kernels"],
+                                 stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
+    except Exception as e:  # noqa: BLE001
+        return {"note": f"second process failed to start: {e}"}
+    out = {"note": "second process did not finish"}
+    try:
+        if child.stdout.readline().strip() != "ready":
+            return {"note": "second process not ready"}
+        old = c.eges.get_knob("EGES_RESIDENT")
+        pub = (ctypes.c_ubyte * 65)()
+        on, off, alive = [], [], []
+        for rep in range(2 * reps):
+            with_server = rep % 2 == 0
+            c.eges.set_knob("EGES_RESIDENT", 1 if with_server else 0)
+            time.sleep(0.02)  # (a previous server idles out first)
+            rc = lib.eges_ecdsa_recover(pub, sig1.tobytes(), msg1.tobytes())
+            if with_server:
+                alive.append(lib.eges_diag_resident_running(dev) == 1)
+            child.stdin.write("go\n")
+            child.stdin.flush()
+            ms = float(child.stdout.readline())
+            (on if with_server else off).append(ms)
+            if rc != 1:
+                return {"note": "single recovery failed", "correct": False}
+        c.eges.set_knob("EGES_RESIDENT", old)
+        child.stdin.close()
+        tail = child.stdout.read().strip()
+        child.wait(timeout=60)
+        m_on, m_off = float(np.median(on)), float(np.median(off))
+        out = {"other_process_1m_kernel_ms_server_alive": round(m_on, 4), "other_process_1m_kernel_ms_no_server": round(m_off, 4),
+               "slowdown": round(m_on / m_off - 1.0, 4), "server_alive_at_launch": f"{sum(alive)}/{len(alive)}",
+               "idle_window_ms": c.eges.get_knob("EGES_RESIDENT_IDLE_MS"), "resident_workgroups": c.eges.get_knob("EGES_RESIDENT_WGS"),
+               "pairs": reps, "correct": tail.endswith("ok")}
+    finally:
+        if child.poll() is None:
+            child.kill()
     return out
 
 
@@ -1087,6 +1204,9 @@ def run_c4host(c):
 
 def main():
     args = parse()
+    if args.other_process_kernels:
+        other_process_kernels()
+        return
     launch_ranks(args)  # --gpus N: one process per GPU (before anything touches the GPU)
     c = Ctx(args)
     if args.stub and args.config not in ("c2", "c4", "c4host"):

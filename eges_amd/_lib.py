@@ -73,6 +73,7 @@ SIGNATURES = {
     "eges_synth_sign_dev": (_I, [_I, _U64, _SZ, _P, _P, _P, _P]),
     "eges_synth_sign_msg_dev": (_I, [_I, _U64, _SZ, _P, _P, _P, _P]),
     "eges_diag_counters": (_I, [_I, _P, _SZ, _I]),
+    "eges_diag_resident_running": (_I, [_I]),
     "eges_test_set_knob": (_I, [ctypes.c_char_p, ctypes.c_longlong]),
     "eges_test_get_knob": (_I, [ctypes.c_char_p, _P]),
 }

@@ -308,6 +308,22 @@ int eges_synth_sign_msg_dev(int device, uint64_t first_index, size_t n, const ui
   return synth_common(device, first_index, n, msg_in, nullptr, sig, addr_expected, stream);
 }
 
+int eges_diag_resident_running(int device) {
+  std::vector<DevPtr> devs;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (const DevPtr& d : g_devs)
+      if (d->id == device) devs.push_back(d);
+  }
+  if (devs.empty()) return set_err(EGES_E_INVALID_ARG, "device %d not managed by the engine", device);
+  for (const DevPtr& d : devs) {
+    std::unique_lock<std::mutex> lk(d->res.mu, std::try_to_lock);
+    if (!lk.owns_lock()) return 1;  // (a job is being handed over right now)
+    if (d->res.running && hipStreamQuery(d->res.stream) == hipErrorNotReady) return 1;
+  }
+  return 0;
+}
+
 int eges_diag_counters(int device, uint64_t* out, size_t n, int reset) {
   if (!out && n) return set_err(EGES_E_NULLPTR, "out is NULL");
   std::vector<DevPtr> devs;

@@ -233,6 +233,11 @@ int eges_synth_sign_msg_dev(int device, uint64_t first_index, size_t n, const ui
 /* Copies min(n, EGES_DIAG_COUNT) counters of `device` (summed over the engine's instances of
  * it) into out; reset != 0 zeroes them afterwards. Synchronises the device. */
 int eges_diag_counters(int device, uint64_t *out, size_t n, int reset);
+/* 1 while the resident single-call server of `device` is running (its persistent launch has not
+ * ended: it serves jobs, or polls for one until its idle window runs out), 0 when it is not,
+ * EGES_E_INVALID_ARG for a device the engine does not manage. Does not synchronise anything
+ * (bench.py and tests use it to record whether the server was alive at a given moment). */
+int eges_diag_resident_running(int device);
 
 /* Engine knobs. Read from the environment once, at the first eges_init (EGES_LAT_MAX,
  * EGES_LAT_WIDE_MAX, EGES_MID_MAX, EGES_TXROWS_WAVE_MAX, EGES_TEST_ROOT_HELPERS, EGES_OVERLAP,

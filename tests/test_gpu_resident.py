@@ -113,9 +113,12 @@ def test_resident_idle_window_and_another_process(engine):
     """the resident server's workgroups keep polling for EGES_RESIDENT_IDLE_MS
     after a call, on CUs another process may want. A second process launches a 1M batch right
     after this process's single call (the server alive for EGES_RESIDENT_IDLE_MS, 1 ms by default)
-    and after the same call on a lane (no server), alternating; its kernel may not slow down by
-    more than 3 % in the median (the server's 16 workgroups hold 16 of the 512 resident recover
-    blocks' places for at most the idle window)."""
+    and after the same call on a lane (no server), alternating. ADVICE r5: the server's liveness at
+    each launch request is recorded (eges_diag_resident_running) and must have been seen, so the
+    'alive' case did overlap the other kernel; the slowdown is reported (bench.py carries it as
+    secondary.single.resident_tax) and only guarded loosely here (< 10 % in the median: the
+    server's 16 workgroups hold 16 of the 512 resident recover blocks' places for at most the idle
+    window), so clock noise on a shared box cannot fail the suite."""
     import os
     import subprocess
     import sys
@@ -133,12 +136,14 @@ def test_resident_idle_window_and_another_process(engine):
             engine.set_knob("EGES_RESIDENT", 1 if with_server else 0)
             rc, _ = _single_recover(g["msg"][i], g["sig"][i])
             assert rc == 1
+            if with_server:
+                alive.append(_lib.lib.eges_diag_resident_running(0) == 1)
             child.stdin.write("go\n")
             child.stdin.flush()
             return float(child.stdout.readline())
 
         with knobs(engine, {"EGES_RESIDENT": 1}):
-            on, off = [], []
+            on, off, alive = [], [], []
             for _ in range(8):
                 time.sleep(0.02)  # (the previous server idles out first)
                 on.append(other(True))
@@ -151,5 +156,7 @@ def test_resident_idle_window_and_another_process(engine):
         if child.poll() is None:
             child.kill()
     m_on, m_off = float(np.median(on)), float(np.median(off))
-    print(f"other process 1M kernel: server alive {m_on:.3f} ms, stopped {m_off:.3f} ms")
-    assert m_on <= 1.03 * m_off, (on, off)
+    print(f"other process 1M kernel: server alive {m_on:.3f} ms, stopped {m_off:.3f} ms, "
+          f"server running at {sum(alive)}/{len(alive)} launch requests")
+    assert sum(alive) >= len(alive) // 2, alive
+    assert m_on <= 1.10 * m_off, (on, off)
