@@ -155,7 +155,7 @@ extern std::atomic<long long> g_knob[KNOB_COUNT];
 struct Route {
   size_t lat_max = 0, mid_max = 0;
   uint32_t wide_max = 0, tri_max = 0;
-  long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, gate = 1, gate_step = 8;
+  long long mid_form = 1, wire_fused = 1, overlap = -1, sender_fused = 1, gate = 1, gate_step = 8, bkt2 = 1;
   size_t host_parts = EGES_PIPE_PARTS;
   uint32_t force_redo = 0, skip_flag = 0, delay_x = 0, recheck = 0;
   int host_gens = 0, verify_mid_gens = 1;
@@ -169,6 +169,7 @@ struct Route {
     r.overlap = knob(KNOB_OVERLAP);
     r.sender_fused = knob(KNOB_SENDER_FUSED);
     r.gate = knob(KNOB_GATE);
+    r.bkt2 = knob(KNOB_BKT2);
     r.gate_step = std::max<long long>(0, std::min<long long>(knob(KNOB_GATE_STEP), 1 << 20));
     r.host_gens = (int)std::max<long long>(0, std::min<long long>(knob(KNOB_HOST_GENS), 8));
     r.verify_mid_gens = (int)std::max<long long>(0, std::min<long long>(knob(KNOB_VERIFY_MID_GENS), 64));
@@ -256,6 +257,7 @@ P with_diag(const Dev& d, P p, const Route& rt) {
 // ------------------------------------------------------------------ routing (route.hip)
 bool mid_bucket(const Dev& d, const Route& rt, size_t n);
 bool use_mid(const Dev& d, const Route& rt, size_t n);
+bool mid_bkt2(const Dev& d, const Route& rt, size_t n);
 bool verify_mid(const Dev& d, const Route& rt, size_t n);
 hipError_t launch_verify_any(Dev& d, const Route& rt, const VerifyParams& p, bool small, hipStream_t st);
 bool fused_parse(const Dev& d, const Route& rt, size_t n);

@@ -68,6 +68,7 @@ static const KnobDef KNOB_DEFS[] = {
     {"EGES_GATE_STEP", 8},
     {"EGES_HOST_GENS", 0},
     {"EGES_VERIFY_MID_GENS", 2},
+    {"EGES_BKT2", 1},
     {"EGES_TEST_RECHECK", 0},
 };
 static_assert(sizeof(KNOB_DEFS) / sizeof(KNOB_DEFS[0]) == KNOB_COUNT, "a name and default for every knob");

@@ -482,12 +482,19 @@ constexpr int BK_ASLOT = 3;
 static_assert(BK_RING > BK_ASLOT + 1 && BK_WIN - BK_RING > BK_ASLOT + 1, "partial-sum slots");
 
 constexpr int BK_STAGE_WORDS = 2 * GJ_WORDS * MID_L;  // wire form: staged encodings (13.5 KB)
-struct BktLds {
-  uint32_t ring[BK_RING][GJ_WORDS][MID_L];           // published P_{3k}, slot k % BK_RING
+// Two-per-CU variant (G2, round 6, VERIFY r5 item 3: the 16k-32k band): the ring and the two
+// parts live in a per-workgroup area of the device workspace instead of LDS (BK2_WS_WORDS, the
+// same [word][lane] layout, so every access stays coalesced), which leaves ~64 KB of LDS per
+// workgroup: two workgroups per CU, one generation up to 128 x CUs signatures. No wire form.
+constexpr size_t BK2_RING_WORDS = (size_t)BK_RING * GJ_WORDS * MID_L;
+constexpr size_t BK2_WS_WORDS = BK2_RING_WORDS + (size_t)2 * GJ_WORDS * MID_L;
+template <bool G2>
+struct BktLdsT {
+  uint32_t ring[G2 ? 1 : BK_RING][GJ_WORDS][MID_L];  // published P_{3k}, slot k % BK_RING (G2: unused)
   uint32_t bucket[2][BK_NB][GJ_WORDS][MID_L];        // per half; lanes index their own bucket
   union {
-    uint32_t part[2][GJ_WORDS][MID_L];               // 0: u1 G (E), 1: Q2 (E')
-    uint32_t stage[BK_STAGE_WORDS];                  // wire form: the workgroup's encodings, until
+    uint32_t part[G2 ? 1 : 2][GJ_WORDS][MID_L];      // 0: u1 G (E), 1: Q2 (E') (G2: unused)
+    uint32_t stage[G2 ? 1 : BK_STAGE_WORDS];         // wire form: the workgroup's encodings, until
   } u;                                               //   wave S has hashed them (BF_STAGE_FREE)
   uint32_t meta[MID_L];                              // wire form: wave S's pre-check meta and ok
   uint8_t pok[MID_L];
@@ -499,7 +506,10 @@ struct BktLds {
   int8_t dig[2][BK_WIN][MID_L];
   uint32_t flag[BF_N];
 };
+using BktLds = BktLdsT<false>;
 static_assert(sizeof(BktLds) <= 160 * 1024, "bucket form LDS");
+static_assert(2 * sizeof(BktLdsT<true>) <= 160 * 1024, "bucket form, two per CU");
+
 
 DEV void lds_put_gej(uint32_t (*a)[MID_L], const gej& p, uint32_t l) {
   lds_put_fe<FE_LIMBS>(a, p.x.v, l);
@@ -513,6 +523,48 @@ DEV gej lds_get_gej(const uint32_t (*a)[MID_L], uint32_t l) {
   lds_get_fe<FE_LIMBS>(a + 2 * FE_LIMBS, p.z.v, l);
   return p;
 }
+
+// the ring slots and parts: LDS, or (G2) the workgroup's area of the device workspace
+template <bool G2>
+struct BktStore {
+  BktLdsT<G2>& S;
+  uint32_t* g;  // G2: ring [BK_RING][GJ_WORDS][MID_L], then part [2][GJ_WORDS][MID_L]
+  DEV void ring_put(uint32_t slot, const gej& p, uint32_t l) {
+    if constexpr (G2) gput(g + (size_t)slot * GJ_WORDS * MID_L, p, l);
+    else lds_put_gej(S.ring[slot], p, l);
+  }
+  DEV gej ring_get(uint32_t slot, uint32_t l) {
+    if constexpr (G2) return gget(g + (size_t)slot * GJ_WORDS * MID_L, l);
+    else return lds_get_gej(S.ring[slot], l);
+  }
+  DEV void part_put(int i, const gej& p, uint32_t l) {
+    if constexpr (G2) gput(g + BK2_RING_WORDS + (size_t)i * GJ_WORDS * MID_L, p, l);
+    else lds_put_gej(S.u.part[i], p, l);
+  }
+  DEV gej part_get(int i, uint32_t l) {
+    if constexpr (G2) return gget(g + BK2_RING_WORDS + (size_t)i * GJ_WORDS * MID_L, l);
+    else return lds_get_gej(S.u.part[i], l);
+  }
+  // [GJ_WORDS][MID_L] in global memory: word w of lane l at a[w * MID_L + l] (coalesced)
+  static DEV void gput(uint32_t* a, const gej& p, uint32_t l) {
+#pragma unroll
+    for (int i = 0; i < FE_LIMBS; ++i) {
+      a[i * MID_L + l] = p.x.v[i];
+      a[(FE_LIMBS + i) * MID_L + l] = p.y.v[i];
+      a[(2 * FE_LIMBS + i) * MID_L + l] = p.z.v[i];
+    }
+  }
+  static DEV gej gget(const uint32_t* a, uint32_t l) {
+    gej p;
+#pragma unroll
+    for (int i = 0; i < FE_LIMBS; ++i) {
+      p.x.v[i] = a[i * MID_L + l];
+      p.y.v[i] = a[(FE_LIMBS + i) * MID_L + l];
+      p.z.v[i] = a[(2 * FE_LIMBS + i) * MID_L + l];
+    }
+    return p;
+  }
+};
 
 // Flags and LDS counters (handoff.cuh): the producer publishes a flag or a running count after
 // a workgroup release fence, consumers wait (bounded) until it reaches k and acquire.
@@ -661,19 +713,21 @@ DEV void verify_parse_lane(const RecoverParams& prm, uint32_t idx, LatParse& q, 
   q.recid = 0;
 }
 
-template <class ST, bool VERIFY = false>
+template <class ST, bool VERIFY = false, bool G2 = false>
 DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
   gate_wait(prm);
-  __shared__ BktLds S;
+  __shared__ BktLdsT<G2> S;
+  BktStore<G2> rg{S, G2 ? prm.ws + (size_t)blockIdx.x * BK2_WS_WORDS : nullptr};
   ST st_;
   const Diag dg = diag_of(prm);
   const uint32_t l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t idx = blockIdx.x * MID_L + l;
   const bool live = idx < prm.n;
-  const bool wire = !VERIFY && prm.wire_raw != nullptr;  // kernel-uniform
+  const bool wire = !VERIFY && !G2 && prm.wire_raw != nullptr;  // kernel-uniform
   uint64_t stage_a0 = 0, stage_end = 0;
   if (threadIdx.x < BF_N) S.flag[threadIdx.x] = 0u;
-  if (wire) wire_stage(S, prm, stage_a0, stage_end);
+  if constexpr (!G2)
+    if (wire) wire_stage(S, prm, stage_a0, stage_end);
   __syncthreads();  // the only barrier
   LatParse q;
   Payload m;
@@ -684,14 +738,14 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
   } else if (!wire) {
     q = prm.snd_r ? sender_parse_lane(prm, live ? idx : prm.n - 1) : lat_parse(prm, live ? idx : prm.n - 1);
   } else if (wv == 1) {
-    wire_parse(S, prm, live ? idx : prm.n - 1, stage_a0, stage_end, q, m);
+    if constexpr (!G2) wire_parse(S, prm, live ? idx : prm.n - 1, stage_a0, stage_end, q, m);
     S.meta[l] = q.meta;
     S.pok[l] = live && q.ok ? 1u : 0u;
     BFLAG_SET(BF_PARSED);
   } else if (wv == 0) {  // R's x straight from the encoding, without waiting for S's checks
 #pragma unroll 1
     for (uint32_t k = 0; k < prm.test_delay_x; ++k) __builtin_amdgcn_s_sleep(127);  // tests only
-    q.ok = live && wire_r_only(S, prm, idx, stage_a0, stage_end, q.xr);
+    if constexpr (!G2) q.ok = live && wire_r_only(S, prm, idx, stage_a0, stage_end, q.xr);
   } else {
     q.ok = false;  // Y waves: read from LDS at the end
   }
@@ -775,7 +829,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
     // it publishes its first point, so that count is the stage's release for this write (wave S's
     // own reads end at BF_STAGE_FREE; part[1] is written after BF_A1, i.e. after X's whole chain)
     if (wire) CNT_WAIT(BF_PUB, 1u);
-    lds_put_gej(S.u.part[0], Ga, l);
+    rg.part_put(0, Ga, l);
     S.pinf[0][l] = ginf ? 1u : 0u;
     BFLAG_SET(BF_G);
     st_.mark(4);
@@ -805,7 +859,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
         freed = (c0 < c1 ? c0 : c1) + BK_RING;
         st_.mark(2);
       }
-      lds_put_gej(S.ring[k % BK_RING], P, l);
+      rg.ring_put((uint32_t)(k % BK_RING), P, l);
       CNT_SET(BF_PUB, (uint32_t)(k + 1));
     }
     st_.mark(1);
@@ -820,7 +874,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
       bool ia;
       const gej a = join_mid(lds_get_gej(S.bucket[h][0], l), S.binf[h][0][l] != 0, lds_get_gej(S.bucket[h][2], l),
                              S.binf[h][2][l] != 0, ia, dg);
-      lds_put_gej(S.ring[slot], a, l);
+      rg.ring_put(slot, a, l);
       S.ainf[h][l] = ia ? 1u : 0u;
       BFLAG_SET(BF_A0 + h);
     }
@@ -844,7 +898,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
       avail = ho_load(&S.flag[BF_PUB]);
       st_.mark(3);
     }
-    gej P = lds_get_gej(S.ring[k % BK_RING], l);
+    gej P = rg.ring_get((uint32_t)(k % BK_RING), l);
     const int d = (int)S.dig[h][k][l];
     CNT_SET(BF_CON0 + h, (uint32_t)(k + 1));  // (the release fence orders this wave's ring reads first)
     const int a = d < 0 ? -d : d;
@@ -869,12 +923,12 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
   Jb = join_mid(Jb, ib, gej_double(lds_get_gej(S.bucket[h][3], l)), S.binf[h][3][l] != 0, ib, dg);
   Jb = gej_double(Jb);
   BFLAG_WAIT(BF_A0 + h);
-  gej T = join_mid(lds_get_gej(S.ring[BK_ASLOT + h], l), S.ainf[h][l] != 0, Jb, ib, tinf, dg);
+  gej T = join_mid(rg.ring_get((uint32_t)(BK_ASLOT + h), l), S.ainf[h][l] != 0, Jb, ib, tinf, dg);
   st_.mark(4);
   if (h == 1) {
     T.x = fe_mul(T.x, fe_const(FE_BETA));  // lambda (X, Y, Z) = (beta X, Y, Z)
     if (wire) BFLAG_WAIT(BF_STAGE_FREE);  // part[1] shares LDS with the stage
-    lds_put_gej(S.u.part[1], T, l);
+    rg.part_put(1, T, l);
     S.pinf[1][l] = tinf ? 1u : 0u;
     BFLAG_SET(BF_Q2);
     stamp_out();
@@ -883,7 +937,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
   // ---- Y1: the joins and the address
   BFLAG_WAIT(BF_Q2);
   bool qinf, oinf;
-  gej Q = join_mid(T, tinf, lds_get_gej(S.u.part[1], l), S.pinf[1][l] != 0, qinf, dg);
+  gej Q = join_mid(T, tinf, rg.part_get(1, l), S.pinf[1][l] != 0, qinf, dg);
   BFLAG_WAIT(BF_Y);
   fe y;
   lds_get_fe<FE_LIMBS>(S.y, y.v, l);
@@ -891,7 +945,7 @@ DEV void recover_bkt_body(const RecoverParams& prm, uint64_t* stamps) {
   Q.z = fe_mul(Q.z, y);  // E' -> E: (X, Y, Z) is (X, Y, Z y)
   BFLAG_WAIT(BF_G);
   st_.mark(5);
-  Q = join_mid(Q, qinf, lds_get_gej(S.u.part[0], l), S.pinf[0][l] != 0, oinf, dg);
+  Q = join_mid(Q, qinf, rg.part_get(0, l), S.pinf[0][l] != 0, oinf, dg);
   qinf = oinf;
   if (wire) {
     BFLAG_WAIT(BF_PARSED);
@@ -961,6 +1015,14 @@ __global__ void __launch_bounds__(MID_WG, 1) recover_bkt_kernel(RecoverParams pr
 __global__ void __launch_bounds__(MID_WG, 1) verify_bkt_kernel(RecoverParams prm) {
   recover_bkt_body<NoStamp, true>(prm, nullptr);
 }
+// two workgroups per CU (ring and parts in the workspace, no wire form)
+__global__ void __launch_bounds__(MID_WG, 2) recover_bkt2_kernel(RecoverParams prm) {
+  recover_bkt_body<NoStamp, false, true>(prm, nullptr);
+}
+__global__ void __launch_bounds__(MID_WG, 2) verify_bkt2_kernel(RecoverParams prm) {
+  recover_bkt_body<NoStamp, true, true>(prm, nullptr);
+}
+size_t bkt2_ws_bytes_per_block() { return BK2_WS_WORDS * sizeof(uint32_t); }
 
 __global__ void __launch_bounds__(MID_WG, 2) recover_mid_kernel(RecoverParams prm) {
   recover_mid_body<NoStamp>(prm, nullptr);
@@ -968,9 +1030,11 @@ __global__ void __launch_bounds__(MID_WG, 2) recover_mid_kernel(RecoverParams pr
 
 size_t mid_ws_bytes_per_block() { return MID_WS_WORDS * sizeof(uint32_t); }
 
-hipError_t launch_verify_mid(const VerifyParams& v, hipStream_t st) {
+hipError_t launch_verify_mid(const VerifyParams& v, bool two, size_t ws_bytes, hipStream_t st) {
   if (v.n == 0) return hipSuccess;
-  RecoverParams p{nullptr, v.n, v.n, nullptr, nullptr, nullptr, v.gtab, nullptr};
+  const uint32_t grid = (v.n + MID_L - 1) / MID_L;
+  if (two && (!v.ws || (size_t)grid * bkt2_ws_bytes_per_block() > ws_bytes)) return hipErrorInvalidValue;
+  RecoverParams p{nullptr, v.n, v.n, nullptr, nullptr, nullptr, v.gtab, two ? v.ws : nullptr};
   p.diag = v.diag;
   p.force_redo = v.force_redo;
   p.test_skip_flag = v.test_skip_flag;
@@ -981,7 +1045,16 @@ hipError_t launch_verify_mid(const VerifyParams& v, hipStream_t st) {
   p.v_sig = v.sig;
   p.v_ok = v.ok;
   p.v_fault = v.fault;
-  hipLaunchKernelGGL(verify_bkt_kernel, dim3((v.n + MID_L - 1) / MID_L), dim3(MID_WG), 0, st, p);
+  if (two) hipLaunchKernelGGL(verify_bkt2_kernel, dim3(grid), dim3(MID_WG), 0, st, p);
+  else hipLaunchKernelGGL(verify_bkt_kernel, dim3(grid), dim3(MID_WG), 0, st, p);
+  return hipGetLastError();
+}
+// the two-per-CU bucket form: ws holds ceil(n / 64) blocks of bkt2_ws_bytes_per_block(); no wire form
+hipError_t launch_recover_bkt2(const RecoverParams& p, size_t ws_bytes, hipStream_t st) {
+  if (p.n == 0) return hipSuccess;
+  const uint32_t grid = (p.n + MID_L - 1) / MID_L;
+  if (p.wire_raw || !p.ws || (size_t)grid * bkt2_ws_bytes_per_block() > ws_bytes) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(recover_bkt2_kernel, dim3(grid), dim3(MID_WG), 0, st, p);
   return hipGetLastError();
 }
 

@@ -189,7 +189,11 @@ constexpr uint32_t MID_SIGS_PER_BLOCK = 64;
 hipError_t launch_verify(const VerifyParams& p, int max_blocks, int ws_blocks, hipStream_t st);
 // VerifySignature on the mid-size kernel's bucket form (64 items per 4-wave workgroup, one per CU
 // at most: n <= 64 x CUs; no workspace)
-hipError_t launch_verify_mid(const VerifyParams& p, hipStream_t st);
+// two: the two-per-CU bucket form (ring in p.ws: ceil(n / 64) blocks of bkt2_ws_bytes_per_block(),
+// refused beyond ws_bytes)
+hipError_t launch_verify_mid(const VerifyParams& p, bool two, size_t ws_bytes, hipStream_t st);
+hipError_t launch_recover_bkt2(const RecoverParams& p, size_t ws_bytes, hipStream_t st);
+size_t bkt2_ws_bytes_per_block();
 // one item per 128-thread workgroup (k_recover_lat.hip; wide: 192 threads, three partial sums);
 // uses pub/publen/msg/sig/n/ok/gtab only
 hipError_t launch_verify_lat(const VerifyParams& p, bool wide, hipStream_t st);

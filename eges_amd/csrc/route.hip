@@ -32,9 +32,20 @@ bool mid_bucket(const Dev& d, const Route& rt, size_t n) {
   if (f >= 2) return true;
   return (n + MID_SIGS_PER_BLOCK - 1) / MID_SIGS_PER_BLOCK <= (size_t)d.cus;
 }
+// The bucket form at two workgroups per CU (k_recover_mid.hip G2: its ring and parts in the
+// workspace, ~76 KB of LDS): for batches past one generation of the one-per-CU form, up to one
+// generation at two per CU, instead of the windowed form or a second bucket generation (round 6,
+// VERDICT r5 item 3). No wire form: such batches take the unfused rows (wire_fused()).
+bool mid_bkt2(const Dev& d, const Route& rt, size_t n) {
+  if (rt.bkt2 == 0 || rt.mid_form == 0) return false;
+  const size_t wgs = (n + MID_SIGS_PER_BLOCK - 1) / MID_SIGS_PER_BLOCK;
+  if (wgs * bkt2_ws_bytes_per_block() > dev_ws_bytes(d)) return false;
+  if (rt.bkt2 >= 2) return true;
+  return rt.mid_form == 1 && wgs > (size_t)d.cus && wgs <= 2 * (size_t)d.cus;
+}
 bool use_mid(const Dev& d, const Route& rt, size_t n) {
   if (n <= rt.lat_max || n > rt.mid_max) return false;
-  if (mid_bucket(d, rt, n)) return true;
+  if (mid_bucket(d, rt, n) || mid_bkt2(d, rt, n)) return true;
   // the windowed form: in auto mode only while its grid is one generation (two workgroups per
   // CU); a second, partial one costs more than the lane-serial kernel's one chain (36k-40k
   // signatures 0.98 against 0.80 ms, profiles/r05/formcurve_cut_r05_zb.jsonl)
@@ -47,11 +58,12 @@ bool use_mid(const Dev& d, const Route& rt, size_t n) {
 // chain (one generation 0.35 ms, two 0.66 ms, the lane-serial kernel 0.78-0.82 ms up to 65k items)
 bool verify_mid(const Dev& d, const Route& rt, size_t n) {
   return rt.mid_form != 0 && n > rt.lat_max && n <= rt.mid_max &&
-         (n + MID_SIGS_PER_BLOCK - 1) / MID_SIGS_PER_BLOCK <= (size_t)d.cus * (size_t)rt.verify_mid_gens;
+         ((n + MID_SIGS_PER_BLOCK - 1) / MID_SIGS_PER_BLOCK <= (size_t)d.cus * (size_t)rt.verify_mid_gens ||
+          mid_bkt2(d, rt, n));
 }
 hipError_t launch_verify_any(Dev& d, const Route& rt, const VerifyParams& p, bool small, hipStream_t st) {
   if (small || p.n <= rt.lat_max) return launch_verify_lat(p, p.n <= rt.wide_max, st);
-  if (verify_mid(d, rt, p.n)) return launch_verify_mid(p, st);
+  if (verify_mid(d, rt, p.n)) return launch_verify_mid(p, p.ws != nullptr && mid_bkt2(d, rt, p.n), dev_ws_bytes(d), st);
   return launch_verify(p, d.mb_verify, d.ws_blocks, st);
 }
 // the recover kernels that parse msg / sig bytes themselves (no prep launch)
@@ -96,6 +108,7 @@ hipError_t launch_recover_pass(Dev& d, const Route& rt, const RecoverParams& p0,
     return e != hipSuccess ? e : launch_recover_lat_stamped(p, st, g_stamps);
   }
 #endif
+  if (mid && !p.wire_raw && p.ws && mid_bkt2(d, rt, p.n)) return launch_recover_bkt2(p, dev_ws_bytes(d), st);
   if (mid) return launch_recover_mid(p, mid_bucket(d, rt, p.n), dev_ws_bytes(d), st);
   if (p.n <= rt.lat_max || p.raw_sig) return launch_recover_lat(p, st);
   // (EGES_HOST_GENS above the device's EGES_GRID_MULT is clamped to it: the workspace holds

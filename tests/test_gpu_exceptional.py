@@ -33,6 +33,8 @@ FORMS = {  # knob settings per form (recovery / verification)
     "tri": {"EGES_LAT_MAX": LAT_ALL, "EGES_LAT_WIDE_MAX": 0, "EGES_LAT_TRI_MAX": LAT_ALL},
     "mid": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": LAT_ALL, "EGES_MID_FORM": 0},
     "mid_bucket": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": LAT_ALL, "EGES_MID_FORM": 2},
+    # the bucket form at two workgroups per CU (ring and parts in the workspace; round 6)
+    "mid_bucket2": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": LAT_ALL, "EGES_MID_FORM": 2, "EGES_BKT2": 2},
 }
 
 
@@ -104,7 +106,7 @@ def test_recover_exceptional_sums_every_form(engine, oracle):
         elif form == "mid":
             # the split1 / split2 constructions meet the windowed form's joins ((A + u1 G) + H, as split)
             assert d["mid_join"] > 0 and d["mid_redo"] == 0 and d["mid_exc"] == 0, d
-        elif form == "mid_bucket":
+        elif form in ("mid_bucket", "mid_bucket2"):
             # the ls / join constructions (u2 R == +-u1 G) meet the bucket form's final join
             assert d["mid_join"] > 0 and d["mid_redo"] == 0 and d["mid_exc"] == 0, d
         else:
@@ -138,12 +140,12 @@ def test_precompile_and_single_item_exceptional(engine, oracle):
     cases, msg, sig = _recover_inputs(seed=12)
     est, epub = _expected_recover(oracle, msg, sig)
     inputs = [msg[i].tobytes() + bytes(31) + bytes([27 + sig[i, 64]]) + sig[i, :64].tobytes() for i in range(len(msg))]
-    for form in ("narrow", "split", "mid", "mid_bucket"):
+    for form in ("narrow", "split", "mid", "mid_bucket", "mid_bucket2"):
         engine.diag_counters(reset=True)
         with knobs(engine, FORMS[form]):
             out, st = engine.ecrecover_precompile_batch(inputs)
         d = engine.diag_counters(reset=True)
-        if form in ("mid", "mid_bucket"):
+        if form in ("mid", "mid_bucket", "mid_bucket2"):
             assert d["mid_join"] > 0, d
         else:
             assert d["join_dbl"] > 0 and d["join_inf"] > 0, (form, d)
@@ -187,7 +189,7 @@ def test_verify_exceptional_sums_every_form(engine, oracle):
             assert d["ls_redo"] > 0 and d["ls_exc"] > 0, d
         elif form == "mid":  # (verification has no windowed mid-size form: lane-serial runs)
             assert d["ls_redo"] > 0 and d["ls_exc"] > 0, d
-        elif form == "mid_bucket":  # the bucket form's verify mode: the exact final join
+        elif form in ("mid_bucket", "mid_bucket2"):  # the bucket form's verify mode: the exact final join
             assert d["mid_join"] > 0 and d["mid_exc"] == 0, d
         else:
             assert d["join_dbl"] > 0 and d["join_inf"] > 0, (form, d)
@@ -213,7 +215,7 @@ def test_forced_redo_every_form_golden(engine):
             assert d["ls_redo"] > 0, d
         elif form == "mid":
             assert d["mid_redo"] > 0 and d["ls_redo"] > 0, d  # recovery: mid-size; verification: lane-serial
-        elif form == "mid_bucket":
+        elif form in ("mid_bucket", "mid_bucket2"):
             assert d["mid_redo"] > 0, d  # recovery and verification both on the bucket form
         else:
             assert d["lat_redo"] > 0 and d["comb_redo"] > 0, (form, d)

@@ -18,6 +18,7 @@ FORMS = {
     "split": {"EGES_LAT_MAX": 1 << 20, "EGES_LAT_WIDE_MAX": 1 << 20},
     "bucket": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2},
     "windowed": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 0},
+    "bucket2": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2, "EGES_BKT2": 2},
 }
 
 
@@ -98,7 +99,7 @@ def test_gate_pieces_wire_and_golden(engine, step):
     idx = [np.arange(n) % len(g["msg"]), (np.arange(n) * 7 + 3) % len(g["msg"])]
     sel = np.nonzero((gs["signer"] == 2) & (gs["chain_id"] == 930412))[0]
     sidx = [sel[np.arange(n) % len(sel)], sel[(np.arange(n) * 5 + 1) % len(sel)]]
-    for form in ("bucket", "windowed"):
+    for form in ("bucket", "windowed", "bucket2"):
         with knobs(engine, dict(FORMS[form], EGES_GATE=1, EGES_GATE_STEP=step, EGES_RESIDENT=0)):
             for rep in range(4):
                 i = idx[rep % 2]

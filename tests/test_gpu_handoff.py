@@ -22,6 +22,7 @@ pytestmark = pytest.mark.gpu
 
 BUCKET = {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2}
 WINDOWED = dict(BUCKET, EGES_MID_FORM=0)
+BUCKET2 = dict(BUCKET, EGES_BKT2=2)  # two workgroups per CU, ring in the workspace (round 6)
 SPLIT = {"EGES_LAT_MAX": 1 << 20, "EGES_LAT_WIDE_MAX": 1 << 20}
 
 
@@ -80,6 +81,11 @@ def _check_fault(engine, form, flag, n_fault, golden="recover.npz", n=None):
 @pytest.mark.parametrize("flag", [0, 2, 3, 12])
 def test_bucket_form_skipped_flag_faults_one_workgroup(engine, flag):
     _check_fault(engine, BUCKET, flag, 64)
+
+
+@pytest.mark.parametrize("flag", [0, 2, 3, 12])
+def test_bucket2_form_skipped_flag_faults_one_workgroup(engine, flag):
+    _check_fault(engine, BUCKET2, flag, 64)
 
 
 @pytest.mark.parametrize("flag", [0, 3])
@@ -154,15 +160,17 @@ def test_verify_split_form_skipped_flag_faults_one_item(engine):
     engine.diag_counters(reset=True)
 
 
-def test_verify_bucket_form_skipped_flag_faults_one_workgroup(engine):
-    """the bucket form's VerifySignature mode: a skipped digit flag faults workgroup 0's items"""
+@pytest.mark.parametrize("two", [False, True])
+def test_verify_bucket_form_skipped_flag_faults_one_workgroup(engine, two):
+    """the bucket form's VerifySignature mode (one and two workgroups per CU): a skipped digit flag
+    faults workgroup 0's items"""
     g = load_golden("verify.npz")
     n = 300
     rep = -(-n // len(g["pub"]))
     pub, publen, msg, sig, exp = (np.ascontiguousarray(np.concatenate([g[k]] * rep)[:n])
                                   for k in ("pub", "publen", "msg", "sig", "ok"))
     ok = np.full(n, 0xEE, np.uint8)
-    with knobs(engine, dict(BUCKET, EGES_TEST_SKIP_FLAG=1)):
+    with knobs(engine, dict(BUCKET2 if two else BUCKET, EGES_TEST_SKIP_FLAG=1)):
         rc = _lib.lib.eges_verify_batch(_p(pub), _p(publen), _p(msg), _p(sig), n, _p(ok))
     assert rc == -3
     assert (ok[:64] == 0).all()

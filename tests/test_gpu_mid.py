@@ -15,7 +15,8 @@ pytestmark = pytest.mark.gpu
 
 MID = {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2}
 MID_WIN = dict(MID, EGES_MID_FORM=0)
-FORMS = {"bucket": MID, "windowed": MID_WIN}
+MID_B2 = dict(MID, EGES_BKT2=2)  # the bucket form at two workgroups per CU (round 6)
+FORMS = {"bucket": MID, "windowed": MID_WIN, "bucket2": MID_B2}
 LANE = {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 0}
 
 

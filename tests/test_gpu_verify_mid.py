@@ -49,12 +49,13 @@ def test_verify_bucket_tiled_ragged_dev(engine):
     cols = {k: np.ascontiguousarray(np.concatenate([g[k]] * rep)[:n]) for k in ("pub", "publen", "msg", "sig", "ok")}
     dev = {k: torch.from_numpy(cols[k]).cuda() for k in ("pub", "publen", "msg", "sig")}
     outs = {}
-    for name, kv in (("bucket", BUCKET), ("lane", LANE)):
+    for name, kv in (("bucket", BUCKET), ("bucket2", dict(BUCKET, EGES_BKT2=2)), ("lane", LANE)):
         with knobs(engine, kv):
             ok = engine.verify_batch_dev(dev["pub"], dev["publen"], dev["msg"], dev["sig"])
             torch.cuda.synchronize()
         outs[name] = ok.cpu().numpy()
     assert np.array_equal(outs["bucket"], cols["ok"])
+    assert np.array_equal(outs["bucket2"], cols["ok"])
     assert np.array_equal(outs["lane"], cols["ok"])
 
 

@@ -21,6 +21,8 @@ sys.path.insert(0, ROOT)
 
 FORMS = {
     "auto": {},  # the product routing (latency / mid-size / lane-serial by batch size)
+    "auto_nob2": {"EGES_BKT2": 0},  # round 5's routing: no two-per-CU bucket form
+    "b2": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2, "EGES_BKT2": 2},
     "lat": {"EGES_LAT_MAX": 1 << 20, "EGES_MID_MAX": 0},
     "mid": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2},
     "midw": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 0},

@@ -20,6 +20,7 @@ sys.path.insert(0, ROOT)
 
 FORMS = {
     "auto": {},
+    "auto_nob2": {"EGES_BKT2": 0},  # round 5's routing: no two-per-CU bucket form
     "auto2": {"EGES_VERIFY_MID_GENS": 2},  # the bucket form for up to two generations of workgroups
     "lat": {"EGES_LAT_MAX": 1 << 20},
     "bucket": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2},
