@@ -52,9 +52,9 @@ enum KnobId : int {
                           //   its grid is at most this many generations of one workgroup per CU (2: 20k-32k
                           //   items 0.78 -> 0.66-0.67 ms; profiles/r05/formcurve_verify_gens_r05_m.jsonl)
   KNOB_BKT2,              // the bucket form at two workgroups per CU (ring in the workspace, no wire form):
-                          //   1 for non-wire recover and verify batches past one generation of the one-per-CU
-                          //   form up to one generation at two per CU (64 x CUs < n <= 128 x CUs); 2 wherever
-                          //   the bucket form runs (tests); 0 never
+                          //   1 for non-wire recover and verify batches of the mid-size band up to one
+                          //   generation at two per CU (n <= 128 x CUs; route.hip mid_bkt2); 2 wherever the
+                          //   bucket form runs (tests); 0 never
   KNOB_TEST_RECHECK,      // tests: a host-buffer call whose outputs come back through pinned memory (the
                           //   lanes, the gated mid-size launches, the resident server) re-reads them after the
                           //   work has drained (the stream, or 200 us for the resident server) and fails

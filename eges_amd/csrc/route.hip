@@ -33,15 +33,20 @@ bool mid_bucket(const Dev& d, const Route& rt, size_t n) {
   return (n + MID_SIGS_PER_BLOCK - 1) / MID_SIGS_PER_BLOCK <= (size_t)d.cus;
 }
 // The bucket form at two workgroups per CU (k_recover_mid.hip G2: its ring and parts in the
-// workspace, ~76 KB of LDS): for batches past one generation of the one-per-CU form, up to one
-// generation at two per CU, instead of the windowed form or a second bucket generation (round 6,
-// VERDICT r5 item 3). No wire form: such batches take the unfused rows (wire_fused()).
+// workspace, ~76 KB of LDS, 215 registers): every non-wire bucket-band batch up to one generation
+// at two per CU (round 6). Past one generation of the one-per-CU form it
+// replaces the windowed form / a second bucket generation (16,385-32,768 signatures 0.70 -> 0.51-
+// 0.54 ms, verify 0.64 -> 0.50-0.52 ms); below it, it is also 1-3 % (recovery) and 3-6 % (verify)
+// faster than the one-per-CU kernel (profiles/r06/formcurve_b2_*). Wire-format batches whose
+// decode is fused in keep the one-per-CU form (its LDS stage); past 64 x CUs they take the
+// unfused rows (wire_fused()). EGES_MID_FORM = 2 (tests) keeps the one-per-CU form unless
+// EGES_BKT2 = 2.
 bool mid_bkt2(const Dev& d, const Route& rt, size_t n) {
   if (rt.bkt2 == 0 || rt.mid_form == 0) return false;
   const size_t wgs = (n + MID_SIGS_PER_BLOCK - 1) / MID_SIGS_PER_BLOCK;
   if (wgs * bkt2_ws_bytes_per_block() > dev_ws_bytes(d)) return false;
   if (rt.bkt2 >= 2) return true;
-  return rt.mid_form == 1 && wgs > (size_t)d.cus && wgs <= 2 * (size_t)d.cus;
+  return rt.mid_form == 1 && wgs <= 2 * (size_t)d.cus;
 }
 bool use_mid(const Dev& d, const Route& rt, size_t n) {
   if (n <= rt.lat_max || n > rt.mid_max) return false;

@@ -103,12 +103,14 @@ def test_verify_bucket_two_generations(engine):
     rep = -(-n // len(g["pub"]))
     cols = {k: np.ascontiguousarray(np.concatenate([g[k]] * rep)[:n]) for k in ("pub", "publen", "msg", "sig", "ok")}
     dev = {k: torch.from_numpy(cols[k]).cuda() for k in ("pub", "publen", "msg", "sig")}
-    for gens, form in ((2, "mid_redo"), (1, "ls_redo")):
+    # (round 6: 1.5 generations at one workgroup per CU are one at two per CU, EGES_BKT2, the
+    # default; without it the lane-serial kernel runs)
+    for gens, b2, form in ((2, 0, "mid_redo"), (1, 0, "ls_redo"), (1, 1, "mid_redo")):
         engine.diag_counters(reset=True)
-        with knobs(engine, {"EGES_VERIFY_MID_GENS": gens, "EGES_TEST_FORCE_REDO": 1}):
+        with knobs(engine, {"EGES_VERIFY_MID_GENS": gens, "EGES_TEST_FORCE_REDO": 1, "EGES_BKT2": b2}):
             ok = engine.verify_batch_dev(dev["pub"], dev["publen"], dev["msg"], dev["sig"])
             torch.cuda.synchronize()
         d = engine.diag_counters(reset=True)
-        assert np.array_equal(ok.cpu().numpy(), cols["ok"]), gens
-        assert d[form] > 0, (gens, d)
+        assert np.array_equal(ok.cpu().numpy(), cols["ok"]), (gens, b2)
+        assert d[form] > 0, (gens, b2, d)
         assert d["mid_redo" if form == "ls_redo" else "ls_redo"] == 0, (gens, d)

@@ -24,6 +24,7 @@ FORMS = {
     "auto2": {"EGES_VERIFY_MID_GENS": 2},  # the bucket form for up to two generations of workgroups
     "lat": {"EGES_LAT_MAX": 1 << 20},
     "bucket": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2},
+    "b2": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 1 << 20, "EGES_MID_FORM": 2, "EGES_BKT2": 2},
     "lane": {"EGES_LAT_MAX": 0, "EGES_MID_MAX": 0},
 }
 
