@@ -834,7 +834,7 @@ def measure_resident_tax(c, msg1, sig1, reps=8):
     """What the resident single-call server costs another tenant of the GPU:
     a second process launches a device-resident 1M batch right after one single recovery of this
     process, alternately with the server alive (EGES_RESIDENT=1: its workgroups poll for
-    EGES_RESIDENT_IDLE_MS after the call) and without it; the medians of the other process's kernel
+    EGES_RESIDENT_IDLE_US after the call) and without it; the medians of the other process's kernel
     time, their ratio, and how often the server was still running when the other launch was
     requested (eges_diag_resident_running)."""
     import numpy as np
@@ -874,7 +874,7 @@ def measure_resident_tax(c, msg1, sig1, reps=8):
         m_on, m_off = float(np.median(on)), float(np.median(off))
         out = {"other_process_1m_kernel_ms_server_alive": round(m_on, 4), "other_process_1m_kernel_ms_no_server": round(m_off, 4),
                "slowdown": round(m_on / m_off - 1.0, 4), "server_alive_at_launch": f"{sum(alive)}/{len(alive)}",
-               "idle_window_ms": c.eges.get_knob("EGES_RESIDENT_IDLE_MS"), "resident_workgroups": c.eges.get_knob("EGES_RESIDENT_WGS"),
+               "idle_window_us": c.eges.get_knob("EGES_RESIDENT_IDLE_US"), "resident_workgroups": c.eges.get_knob("EGES_RESIDENT_WGS"),
                "pairs": reps, "correct": tail.endswith("ok")}
     finally:
         if child.poll() is None:

@@ -63,7 +63,7 @@ static const KnobDef KNOB_DEFS[] = {
     {"EGES_RESIDENT", 1},
     {"EGES_RESIDENT_WGS", 16},
     {"EGES_RESIDENT_CAP", 64},
-    {"EGES_RESIDENT_IDLE_MS", 1},
+    {"EGES_RESIDENT_IDLE_US", 500},
     {"EGES_GATE", 1},
     {"EGES_GATE_STEP", 8},
     {"EGES_HOST_GENS", 0},

@@ -37,9 +37,10 @@ enum KnobId : int {
   KNOB_RESIDENT,          // 1: coalesced single calls go to the resident server (single.hip Resident)
   KNOB_RESIDENT_WGS,      //   its workgroups (split form, four waves each)
   KNOB_RESIDENT_CAP,      //   the largest group it takes (larger groups launch on a lane)
-  KNOB_RESIDENT_IDLE_MS,  //   it exits after this long without a job (restarted on demand; 1 ms: its workgroups
+  KNOB_RESIDENT_IDLE_US,  //   it exits after this many us without a job (restarted on demand; 500: its workgroups
                           //   leave the CUs to other work soon after a burst of calls, and back-to-back
-                          //   callers keep it alive: single p50 0.1128 ms at 1 ms against 0.1131-0.1136 at 4)
+                          //   callers keep it alive; another process's 1M launch right after a single call
+                          //   ran 0.95-1.05 % slower at 1 ms, bench.py secondary.single.resident_tax)
   KNOB_GATE,              // 1: single-chunk host-buffer calls on the mid-size kernels launch first and copy
                           //   their inputs while the launch is in flight (hostpath.hip Gate; the latency
                           //   kernels run ungated)

@@ -87,11 +87,11 @@ int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& re
       return set_err(EGES_E_NOMEM, "hipHostMalloc(resident data)");
     r.cap = cap;
   }
-  const long long idle_ms = std::max<long long>(1, knob(KNOB_RESIDENT_IDLE_MS));
+  const long long idle_us = std::max<long long>(50, knob(KNOB_RESIDENT_IDLE_US));
   const auto now = std::chrono::steady_clock::now();
   // a server idle for half its bound may be deciding to exit: restart it rather than race it
   if (r.running &&
-      (hipStreamQuery(r.stream) == hipSuccess || now - r.last_use > std::chrono::microseconds(idle_ms * 500)))
+      (hipStreamQuery(r.stream) == hipSuccess || now - r.last_use > std::chrono::microseconds(idle_us / 2)))
     resident_halt(d, r);
   auto launch = [&]() -> int {
     if (!r.running) {  // the lane finishes what it runs and takes no more calls
@@ -101,7 +101,7 @@ int resident_job(Dev& d, Resident& r, int kind, size_t n, Fill&& fill, Read&& re
     HIPCHK(hipMemsetAsync(r.counter, 0, RESIDENT_COUNTER_BYTES, r.stream));
     if (++r.inst == 0) r.inst = 1;
     ResidentParams rp{r.job, r.data, r.cap, __atomic_load_n(&r.job->done, __ATOMIC_ACQUIRE), r.counter,
-                      (uint64_t)idle_ms * 100000ull, r.inst, d.gtab, d.diag};
+                      (uint64_t)idle_us * 100ull, r.inst, d.gtab, d.diag};  // (s_memrealtime: 100 MHz)
     r.wgs = (uint32_t)std::max<long long>(1, std::min<long long>(knob(KNOB_RESIDENT_WGS), 1024));
     if (!r.data || !r.counter) return set_err(EGES_E_HIP, "resident server: buffers missing");
     if (launch_lat_resident(rp, r.wgs, r.stream) != hipSuccess) {

@@ -90,7 +90,7 @@ def test_knobs_set_and_read_without_gpu():
                 "EGES_LAT_TRI_MAX": 448, "EGES_SENDER_FUSED": 1}
     for name, want in defaults.items():
         assert eges_amd.get_knob(name) == want, name
-    for name in ("EGES_RESIDENT_WGS", "EGES_RESIDENT_CAP", "EGES_RESIDENT_IDLE_MS", "EGES_TEST_DELAY_X",
+    for name in ("EGES_RESIDENT_WGS", "EGES_RESIDENT_CAP", "EGES_RESIDENT_IDLE_US", "EGES_TEST_DELAY_X",
                  "EGES_TEST_SKIP_FLAG"):
         eges_amd.get_knob(name)
     for gone in ("EGES_HOST_PIPE", "EGES_PIPE_SEG", "EGES_HOST_STREAMS", "EGES_RESIDENT_BLOCK",

@@ -90,7 +90,7 @@ def test_resident_idle_exit_and_restart(engine):
     g = load_golden("recover.npz")
     ok = np.nonzero((g["status"] == 0) & (g["sig"][:, 64] < 4))[0]
     engine.diag_counters(reset=True)
-    with knobs(engine, {"EGES_RESIDENT": 1, "EGES_RESIDENT_IDLE_MS": 4}):
+    with knobs(engine, {"EGES_RESIDENT": 1, "EGES_RESIDENT_IDLE_US": 4000}):
         for rep in range(12):
             i = int(ok[rep])
             rc, pub = _single_recover(g["msg"][i], g["sig"][i])
@@ -110,9 +110,9 @@ def test_resident_off_uses_the_lanes(engine):
 
 
 def test_resident_idle_window_and_another_process(engine):
-    """the resident server's workgroups keep polling for EGES_RESIDENT_IDLE_MS
+    """the resident server's workgroups keep polling for EGES_RESIDENT_IDLE_US
     after a call, on CUs another process may want. A second process launches a 1M batch right
-    after this process's single call (the server alive for EGES_RESIDENT_IDLE_MS, 1 ms by default)
+    after this process's single call (the server alive for EGES_RESIDENT_IDLE_US, 0.5 ms by default)
     and after the same call on a lane (no server), alternating. ADVICE r5: the server's liveness at
     each launch request is recorded (eges_diag_resident_running) and must have been seen, so the
     'alive' case did overlap the other kernel; the slowdown is reported (bench.py carries it as

@@ -1,4 +1,4 @@
-"""How the resident single-call server's idle window (EGES_RESIDENT_IDLE_MS) delays another
+"""How the resident single-call server's idle window (EGES_RESIDENT_IDLE_US) delays another
 process's kernel on the same GPU: this process makes one eges_ecdsa_recover call (the server starts
 and polls for the idle window) and a second process (tests/gpu_child.py other_process_kernels)
 launches a device-resident 1M batch right after; the same with the server stopped. Medians over
@@ -39,8 +39,8 @@ def main():
         return float(child.stdout.readline())
 
     try:
-        for idle in [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "4,2,1").split(",")]:
-            eges_amd.set_knob("EGES_RESIDENT_IDLE_MS", idle)
+        for idle in [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "4000,2000,1000,500").split(",")]:
+            eges_amd.set_knob("EGES_RESIDENT_IDLE_US", idle)
             on, off = [], []
             for _ in range(6):
                 eges_amd.set_knob("EGES_RESIDENT", 1)
@@ -51,7 +51,7 @@ def main():
                 single()
                 time.sleep(0.02)
                 off.append(go())
-            print(json.dumps({"idle_ms": idle, "other_kernel_ms_server_alive": round(float(np.median(on)), 3),
+            print(json.dumps({"idle_us": idle, "other_kernel_ms_server_alive": round(float(np.median(on)), 3),
                               "other_kernel_ms_server_stopped": round(float(np.median(off)), 3),
                               "ratio": round(float(np.median(on)) / float(np.median(off)), 4), "on": on, "off": off}),
                   flush=True)
