@@ -202,6 +202,14 @@ def test_verify_lane_serial_multi_item(engine):
     torch.cuda.synchronize()
     got = ok.cpu().numpy()
     assert int((got != exp).sum()) == 0
+    # and item for item against the reference's secp256k1_ext_ecdsa_verify (ext.h:58-75), so
+    # the expectations above are not the only check
+    from oracle import RefLib, have_ref
+    if have_ref():
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        want = RefLib().verify_batch_mt(P, publen, msg.cpu().numpy(), sig_h, threads)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, [(int(i), int(got[i]), int(want[i])) for i in bad[:10]]
 
 
 def _verify_mix(pub_h, sig_h, seed, comp_frac=0.25, mut_frac=0.10):
