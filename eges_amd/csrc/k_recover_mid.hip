@@ -482,10 +482,10 @@ constexpr int BK_ASLOT = 3;
 static_assert(BK_RING > BK_ASLOT + 1 && BK_WIN - BK_RING > BK_ASLOT + 1, "partial-sum slots");
 
 constexpr int BK_STAGE_WORDS = 2 * GJ_WORDS * MID_L;  // wire form: staged encodings (13.5 KB)
-// Two-per-CU variant (G2, round 6, VERIFY r5 item 3: the 16k-32k band): the ring and the two
+// Two-per-CU variant (G2, round 6, VERDICT r5 item 3: the 16k-32k band): the ring and the two
 // parts live in a per-workgroup area of the device workspace instead of LDS (BK2_WS_WORDS, the
-// same [word][lane] layout, so every access stays coalesced), which leaves ~64 KB of LDS per
-// workgroup: two workgroups per CU, one generation up to 128 x CUs signatures. No wire form.
+// same [word][lane] layout, so every access stays coalesced): ~76 KB of LDS per workgroup and
+// 215 registers, two workgroups per CU, one generation up to 128 x CUs signatures. No wire form.
 constexpr size_t BK2_RING_WORDS = (size_t)BK_RING * GJ_WORDS * MID_L;
 constexpr size_t BK2_WS_WORDS = BK2_RING_WORDS + (size_t)2 * GJ_WORDS * MID_L;
 template <bool G2>

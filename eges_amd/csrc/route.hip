@@ -23,7 +23,7 @@ static hipError_t stamp_buf(size_t waves, hipStream_t st) {
 
 // batches (or chunks) the mid-size kernel takes: above LAT_MAX, up to MID_MAX and what the
 // device workspace holds
-// The bucket form (k_recover_mid.hip) holds 138 KB of LDS: one workgroup per CU. It is the
+// The bucket form (k_recover_mid.hip) holds 152 KB of LDS: one workgroup per CU. It is the
 // faster form while the grid fits one generation (n <= 64 x CUs); beyond that the windowed form
 // (two workgroups per CU) is (tools/formcurve.py).
 bool mid_bucket(const Dev& d, const Route& rt, size_t n) {
