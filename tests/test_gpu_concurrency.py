@@ -153,3 +153,68 @@ def test_coalesced_recover_and_verify_many_callers(engine):
         th.join(timeout=150)
     assert not any(th.is_alive() for th in threads), "a caller thread did not return"
     assert not errors, errors[:10]
+
+
+def test_concurrent_mid_size_callers(engine):
+    """Host threads calling the mid-size band at once (round 6): batches of 24,000 (the bucket form
+    at two workgroups per CU, its ring in the device workspace), 9,000 (one workgroup per CU) and
+    3,000 signatures, gated host-buffer recover and VerifySignature calls, beside single-item
+    callers on the resident server. The device workspace and the input gate are per device, so
+    these calls must serialize on it without mixing; every result is checked against the
+    synthetic signer's addresses (and the verify calls against all-valid / wrong-key rows)."""
+    import torch
+    from eges_amd._lib import lib
+    n = 24_000
+    msg_d, sig_d, addr_d = engine.synth_sign_dev(77 << 20, n, 0)
+    pub_d = torch.empty((n, 65), dtype=torch.uint8, device="cuda")
+    engine.ecrecover_batch_dev(msg_d, sig_d, pub=pub_d)
+    torch.cuda.synchronize()
+    msg, sig, exp, pub = (x.cpu().numpy() for x in (msg_d, sig_d, addr_d, pub_d))
+    sig64 = np.ascontiguousarray(sig[:, :64])
+    publen = np.full(n, 65, np.uint8)
+    wrong = np.roll(pub, 1, axis=0)  # another signer's key: every item rejected
+    errors = []
+
+    def recover_worker(t):
+        try:
+            for rep, m in enumerate((24_000, 9_000, 3_000)):
+                lo = (t * 1_009 + rep * 211) % (n - m + 1)
+                sl = slice(lo, lo + m)
+                _, addr, st = engine.ecrecover_batch(msg[sl], sig[sl], want_pub=False)
+                if int(st.max()) != 0 or not np.array_equal(addr, exp[sl]):
+                    errors.append(("recover", t, m, int((addr != exp[sl]).any(axis=1).sum())))
+        except Exception as e:  # surfaced in the main thread
+            errors.append(("recover-exc", t, repr(e)))
+
+    def verify_worker(t):
+        try:
+            for rep, m in enumerate((20_000, 6_000)):
+                lo = (t * 733 + rep * 97) % (n - m + 1)
+                sl = slice(lo, lo + m)
+                keys = pub if (t + rep) % 2 == 0 else wrong
+                ok = engine.verify_batch(keys[sl], publen[sl], msg[sl], sig64[sl])
+                want = 1 if keys is pub else 0
+                if int((ok != want).sum()):
+                    errors.append(("verify", t, m, int((ok != want).sum())))
+        except Exception as e:
+            errors.append(("verify-exc", t, repr(e)))
+
+    def single_worker(t):
+        try:
+            out = (ctypes.c_ubyte * 65)()
+            for i in range(t, 4_000, 37):
+                rc = lib.eges_ecdsa_recover(out, sig[i].tobytes(), msg[i].tobytes())
+                if rc != 1 or bytes(out) != pub[i].tobytes():
+                    errors.append(("single", t, i, rc))
+        except Exception as e:
+            errors.append(("single-exc", t, repr(e)))
+
+    threads = [threading.Thread(target=recover_worker, args=(t,)) for t in range(3)]
+    threads += [threading.Thread(target=verify_worker, args=(t,)) for t in range(2)]
+    threads += [threading.Thread(target=single_worker, args=(t,)) for t in range(2)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=110)
+    assert not any(th.is_alive() for th in threads), "a caller thread did not return"
+    assert not errors, errors[:10]
