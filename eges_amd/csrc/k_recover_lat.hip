@@ -747,6 +747,15 @@ DEV void root_helper(const RecoverParams& prm, uint32_t epoch, uint32_t n) {
   if (prm.wire_raw) {  // wire form: this lane decodes item j itself (x, recid, ok: the waves' record)
     uint64_t ra, len;
     const bool sp = wire_span(prm, j, ra, len);
+    // Touch every 64-byte line of the encoding first with independent byte loads, so the bytes
+    // cross the bus in one round trip (host-memory callers) instead of one per RLP head of the
+    // decode below, which then reads them from L2.
+    if (sp && len) {
+      uint32_t t = 0;
+#pragma unroll 1
+      for (uint64_t o = ra; o < ra + len; o = (o | 63u) + 1u) t ^= prm.wire_raw[o];
+      asm volatile("" ::"v"(t));
+    }
     Payload m;
     wire_item(prm.wire_raw + ra, len, sp, prm.wire_signer, prm.wire_chain_id, q, m);
   } else {
