@@ -66,11 +66,25 @@ def run_wire(n):
     raw, off = pack_raw(txs.c1_raw(0, sig.cpu().numpy()))
     addr = np.zeros((n, 20), np.uint8)
     st = np.zeros(n, np.uint8)
+    dev_in = os.environ.get("PHASES_WIRE_DEV") == "1"  # the bytes in device memory (the *_dev entry)
+    if dev_in:
+        rd = torch.from_numpy(raw).to(dev)
+        od = torch.from_numpy(off.astype(np.int64)).to(dev)
+        ad = torch.empty((n, 20), dtype=torch.uint8, device=dev)
+        sd = torch.empty(n, dtype=torch.uint8, device=dev)
     for it in range(3):
         t0 = time.perf_counter()
-        assert lib.eges_sender_raw_batch(raw.ctypes.data, off.ctypes.data, n, 2, txs.GEEC_CHAIN_ID, addr.ctypes.data,
-                                         st.ctypes.data, None) == 0, lib.eges_last_error()
+        if dev_in:
+            assert lib.eges_sender_raw_batch_dev(0, rd.data_ptr(), od.data_ptr(), n, 2, txs.GEEC_CHAIN_ID, ad.data_ptr(),
+                                                 sd.data_ptr(), None, None) == 0, lib.eges_last_error()
+            torch.cuda.synchronize()
+        else:
+            assert lib.eges_sender_raw_batch(raw.ctypes.data, off.ctypes.data, n, 2, txs.GEEC_CHAIN_ID, addr.ctypes.data,
+                                             st.ctypes.data, None) == 0, lib.eges_last_error()
         dt = time.perf_counter() - t0
+    if dev_in:
+        addr[:] = ad.cpu().numpy()
+        st[:] = sd.cpu().numpy()
     assert (addr == exp.cpu().numpy()).all() and int(st.max()) == 0, "diag build disagrees with the signer"
     return dt
 
